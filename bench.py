@@ -1,0 +1,265 @@
+#!/usr/bin/env python3
+"""bench.py — device-resident CRC-32 FCS throughput on 1518-B frames (BASELINE.json metric).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu F] [--len L]
+
+A "step" is ONE launch of the FCS kernel over one batch: F (default 64 M) x 1518-B frames per
+GPU, already resident in HBM (BASELINE configs[1]; configs[4] = the same per GPU at N = 8).
+For N > 1 the driver starts one process per GPU (torch.distributed.run); frames shard
+embarrassingly (each rank owns a contiguous slice of the global frame stream), so the only
+collectives are the timing barrier and the max-over-ranks of the elapsed time — none on the
+data path. value = bytes of all ranks / max rank time, in GiB/s.
+
+Printed (rank 0, one JSON line): the contract fields plus
+  roofline     — the FCS kernel's achieved algorithmic GB/s (frame bytes per launch / average
+                 launch time from HIP events on the launch stream) against the 8 TB/s HBM peak;
+                 `traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary
+                 (profiles/*pmc*.json), or null;
+  read_stream  — a pure read kernel over the same buffer (the measured HBM read ceiling);
+  cpu_baseline — the oracle's restatement of src/ether_fcs.c (nibble table, one host thread,
+                 -O2 and the reference's own -O0 flags) on 1 M x 1518 B, rank 0, N = 1.
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import glob
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident CRC-32 FCS GiB/s on 1518-B frames, 1/2/4/8 MI355X; % HBM peak"
+HBM_PEAK_GBS = 8000.0        # MI355X HBM3E spec (MI355X_MICROARCH.md)
+GIB = float(1 << 30)
+SEED = 0x4E535441434B        # "NSTACK"
+
+
+def shard_range(total_frames: int, world: int, rank: int):
+    """Contiguous frame range of `rank` (BASELINE configs[4]: 512 M frames over 8 GPUs)."""
+    lo = total_frames * rank // world
+    hi = total_frames * (rank + 1) // world
+    return lo, hi
+
+
+def aggregate(bytes_per_rank, times):
+    """Whole-job throughput: all ranks' bytes over the slowest rank's time."""
+    t = max(times)
+    return sum(bytes_per_rank) / t, t
+
+
+def _load_pmc_traffic(frames: int, L: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one matches."""
+    best = None
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+        try:
+            d = json.load(open(p))
+        except Exception:
+            continue
+        if d.get("frames") == frames and d.get("len") == L and d.get("hbm_bytes_per_launch"):
+            best = (d["hbm_bytes_per_launch"], os.path.relpath(p, ROOT))
+    return best
+
+
+def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
+    """Oracle restatement of ether_fcs (src/ether_fcs.c:4-19) on the SURVEY §8d dataset."""
+    import numpy as np
+    here = os.path.join(ROOT, "oracle", "_build")
+    res = {}
+    buf = np.empty(frames * L, dtype=np.uint8)
+    out = np.empty(frames, dtype=np.uint32)
+    for tag, so in (("O2", "liboracle.so"), ("O0", "liboracle_O0.so")):
+        path = os.path.join(here, so)
+        if not os.path.exists(path):
+            continue
+        o = ctypes.CDLL(path)
+        o.oracle_xorshift64_fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint64)]
+        o.oracle_time_fixed.restype = ctypes.c_double
+        o.oracle_time_fixed.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t,
+                                        ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        if "gen" not in res:
+            st = ctypes.c_uint64(42)
+            o.oracle_xorshift64_fill(buf.ctypes.data, buf.size, ctypes.byref(st))
+            res["gen"] = True
+        secs = o.oracle_time_fixed(buf.ctypes.data, L, L, frames, out.ctypes.data, 0, 1)
+        x = int(np.bitwise_xor.reduce(out))
+        res[tag] = {"gibs": frames * L / secs / GIB, "secs": secs, "xor": x}
+    if "O2" not in res:
+        return None
+    cpu_model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                cpu_model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    ok = res["O2"]["xor"] == 0x600A585E
+    sample = (f"{frames} x {L}-B frames (xorshift64 seed 42, SURVEY §8d), oracle nibble-table "
+              f"restatement of src/ether_fcs.c, 1 host thread; -O2 {res['O2']['secs']:.2f} s"
+              + (f"; reference flags -O0 -g: {res['O0']['gibs']:.4f} GiB/s ({res['O0']['secs']:.2f} s)"
+                 if "O0" in res else "")
+              + f"; XOR of CRCs 0x{res['O2']['xor']:08X} ({'ok' if ok else 'MISMATCH'}); host CPU: {cpu_model}; "
+              f"nproc {os.cpu_count()}")
+    return {"value": round(res["O2"]["gibs"], 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": sample, "value_O0": round(res["O0"]["gibs"], 4) if "O0" in res else None}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--frames-per-gpu", type=int, default=64 << 20)
+    ap.add_argument("--len", type=int, default=1518)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--no-verify", action="store_true")
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import nstack_amd as na
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device("cuda", torch.cuda.current_device())
+    na.load()
+
+    L = args.len
+    F = args.frames_per_gpu
+    total = F * world
+    lo, hi = shard_range(total, world, rank)
+    n = hi - lo
+    nbytes = n * L
+    stream = torch.cuda.current_stream()
+
+    # Synthetic frames: this rank's slice of one global counter-based byte stream.
+    arena = torch.empty(nbytes + 64, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, nbytes, SEED, lo * L, stream)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+
+    def step():
+        na.fixed_dev(arena, L, L, n, out, stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- timed region: exactly K steps, barrier + synchronize on both sides ----
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ev0 = torch.cuda.Event(enable_timing=True)
+    ev1 = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t1 = time.perf_counter()
+    wall = t1 - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
+
+    times = torch.tensor([wall], dtype=torch.float64, device=dev)
+    if dist:
+        dist.all_reduce(times, op=dist.ReduceOp.MAX)
+    tmax = float(times.item())
+    total_bytes = total * L
+    value = total_bytes * args.steps / tmax / GIB
+
+    # ---- correctness spot check of this rank's output against the oracle ----
+    verified = None
+    if not args.no_verify:
+        o = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "liboracle.so"))
+        o.oracle_splitmix_fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
+        o.oracle_crc32_fast.restype = ctypes.c_uint32
+        o.oracle_crc32_fast.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
+        crcs = out.cpu().numpy().view(np.uint32)
+        rng = np.random.default_rng(rank)
+        idx = np.unique(np.concatenate([rng.integers(0, n, 256), [0, n - 1]]))
+        buf = np.empty(L, dtype=np.uint8)
+        bad = 0
+        for i in idx:
+            o.oracle_splitmix_fill(buf.ctypes.data, L, SEED, (lo + int(i)) * L)
+            bad += int(o.oracle_crc32_fast(buf.ctypes.data, L) != int(crcs[i]))
+        flag = torch.tensor([bad], dtype=torch.int64, device=dev)
+        if dist:
+            dist.all_reduce(flag)
+        verified = int(flag.item()) == 0
+
+    # ---- read-stream ceiling over the same buffer (rank-local, untimed by the contract) ----
+    rs = torch.cuda.Event(enable_timing=True)
+    re_ = torch.cuda.Event(enable_timing=True)
+    na.read_stream_dev(arena, nbytes, sink, stream)
+    rs.record(stream)
+    for _ in range(5):
+        na.read_stream_dev(arena, nbytes, sink, stream)
+    re_.record(stream)
+    torch.cuda.synchronize()
+    read_ms = rs.elapsed_time(re_) / 5
+    read_gbs = nbytes / (read_ms * 1e-3) / 1e9
+
+    achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
+    pmc = _load_pmc_traffic(n, L)
+    roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
+                "traffic": pmc[0] if pmc else None,
+                "traffic_source": pmc[1] if pmc else None,
+                "algorithmic_bytes_per_launch": nbytes,
+                "kernel_ms_per_launch": round(kernel_ms, 4),
+                "read_stream_gbs": round(read_gbs, 1),
+                "frac_of_read_stream": round(achieved_gbs / read_gbs, 4)}
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu:
+        cpu = cpu_baseline()
+
+    if dist:
+        dist.barrier()
+    if rank == 0:
+        rec = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(tmax / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": f"synthetic: counter-based splitmix64 bytes (seed 0x{SEED:X}), frames packed at stride {L}",
+            "config": {"workload": f"{F // (1 << 20)} M x {L}-B frames per GPU, one CRC-32 per frame, "
+                                   "single HIP launch per step (BASELINE configs[1]; configs[4] at 8 GPUs)",
+                       "frames_per_gpu": F, "frame_len": L, "global_frames": total,
+                       "parallelism": f"frames sharded over {world} GPU(s), no collective on the data path"},
+            "pct_hbm_peak": round(100.0 * value * GIB / 1e9 / world / HBM_PEAK_GBS, 2),
+            "verified": verified,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "engine": na.version(),
+        }
+        print(json.dumps(rec), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

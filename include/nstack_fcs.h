@@ -1,0 +1,102 @@
+/*
+ * nstack_fcs.h — C ABI of the MI355X Ethernet FCS (IEEE 802.3 CRC-32) engine.
+ *
+ * Drop-in boundary for nstack's FCS path. Every entry point is plain C (no HIP/torch types):
+ * pointers, sizes, and an opaque `void *stream` (a hipStream_t, or NULL for the default stream).
+ *
+ * Reference interfaces replaced / served:
+ *   ether_fcs()                 replaces uint32_t ether_fcs(const void *, size_t)
+ *                               declared /root/reference/src/nstack_ether.h:80,
+ *                               defined   /root/reference/src/ether_fcs.c:4-19.
+ *                               Link libnstack_fcs.so in place of ether_fcs.o
+ *                               (/root/reference/Makefile:13) — no caller changes.
+ *   ether_fcs_batch_host()      the batched form of the per-frame call in ether_send()
+ *   ether_fcs_fixed_host()      (/root/reference/src/linux/ether.c:262); see INTEGRATION.md.
+ *   ether_fcs_tx_host()         TX mode of the same call site: computes the FCS over the first
+ *                               len bytes of each frame and stores it little-endian right after
+ *                               them, exactly as src/linux/ether.c:262-263 does per frame.
+ *   ether_fcs_*_dev()           device-resident forms (frames already in HBM).
+ *
+ * Semantics (all entry points): out[i] == ether_fcs(frame_i, len_i) of the reference, i.e.
+ * CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init/final complement), bit-exact; len 0 -> 0.
+ *
+ * Errors: the batch/device entry points return 0 on success or a negative errno
+ * (-EINVAL bad arguments, -ENODEV no usable GPU / HIP code object missing, -ENOMEM,
+ * -EIO a HIP runtime error; fcs_last_error() has the text). There is NO CPU fallback:
+ * without a GPU the engine fails loudly. ether_fcs() has no error channel in the
+ * reference (it cannot fail there), so on an engine failure it prints the reason to
+ * stderr and aborts rather than return a wrong FCS.
+ *
+ * Threading: every entry point is thread-safe and may be called concurrently (the reference
+ * calls ether_fcs from the main, ingress, egress and TCP-timer threads: SURVEY.md §8b).
+ * Device entry points run on the calling thread's current HIP device; the caller owns all
+ * buffers until the call returns (host forms, synchronous) or until the stream reaches the
+ * point after the call (device forms, asynchronous).
+ */
+#ifndef NSTACK_FCS_H
+#define NSTACK_FCS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- drop-in single frame (src/ether_fcs.c:4, src/nstack_ether.h:80) ---- */
+uint32_t ether_fcs(const void *data, size_t bsize);
+
+/* ---- engine lifetime (optional: every entry point initialises lazily) ---- */
+/* Use the first ndev visible GPUs (ndev <= 0: all). Returns the device count or -errno. */
+int fcs_engine_init(int ndev);
+void fcs_engine_fini(void);
+int fcs_engine_device_count(void);
+const char *fcs_last_error(void);
+/* Engine/kernel description string, e.g. "fcs-hip gfx950 slice4-lds32 chunk48 group32". */
+const char *fcs_engine_version(void);
+
+/* ---- device-resident batches (pointers in HBM of the current device) ---- */
+/* Variable-length frames: frame i = arena[off[i] .. off[i]+len[i]), all inside
+ * [arena, arena + arena_bytes). off/len/out are device arrays of n elements. */
+int ether_fcs_batch_dev(const void *arena, uint64_t arena_bytes, const uint64_t *off,
+                        const uint32_t *len, uint32_t *out, uint64_t n, void *stream);
+/* Fixed-length frames: frame i = base[i*stride .. i*stride+len). stride >= len. */
+int ether_fcs_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                        uint32_t *out, void *stream);
+
+/* ---- host batches (host memory in and out; sharded over the engine's GPUs,
+ *      chunked H2D -> kernel -> D2H pipeline per GPU; synchronous) ---- */
+int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
+                         const uint32_t *len, uint32_t *out, uint64_t n);
+int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                         uint32_t *out);
+/* TX mode (src/linux/ether.c:262-263): frame i occupies base[i*stride ..]; the FCS over its
+ * first len[i] bytes is written little-endian at base[i*stride + len[i] .. +4). Requires
+ * len[i] + 4 <= stride. Frames are modified in place in host memory. */
+int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n);
+
+/* ---- pinned host memory for zero-copy-staging callers (optional) ---- */
+void *fcs_host_alloc(uint64_t bytes);
+void fcs_host_free(void *p);
+
+/* ---- measurement helpers (used by bench.py; not part of the reference surface) ---- */
+/* Fill [p, p+bytes) of device memory with the counter-based splitmix64 stream:
+ * byte at stream position q = byte_offset + i is byte (q & 7) of splitmix64(seed + q/8). */
+int fcs_fill_splitmix64_dev(void *p, uint64_t bytes, uint64_t seed, uint64_t byte_offset,
+                            void *stream);
+/* Pure HBM read-stream kernel over [p, p+bytes): the measured read ceiling. */
+int fcs_read_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
+/* Average device time (ms) per launch of the last `reps` timed FCS launches measured with
+ * HIP events on the launch stream: fcs_timed_fixed_dev() launches ether_fcs_fixed_dev
+ * `reps` times back to back, bracketed by events recorded on `stream`. */
+int fcs_timed_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                        uint32_t *out, void *stream, int reps, float *ms_per_launch);
+
+/* Test introspection: copy the constant tables the kernel stages into LDS (GF(2) operators of
+ * the CRC, built on the host once; no frame data involved). Returns words written or -errno. */
+int fcs_tables_blob(uint32_t *out, uint64_t words);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSTACK_FCS_H */

@@ -1,0 +1,180 @@
+"""nstack_amd — MI355X-native Ethernet FCS engine (host-side mirror of nstack's FCS interface).
+
+The product is the C-ABI library ``nstack_amd/libnstack_fcs.so`` (declared in
+``include/nstack_fcs.h``): a gfx950 HIP kernel behind nstack's ``ether_fcs`` call surface
+(/root/reference/src/ether_fcs.c:4, src/nstack_ether.h:80). This module is a thin ctypes
+binding so Python tests, the bench and torch-based callers can drive it. It never computes a
+CRC itself: if the library (or a GPU) is missing, every call raises ``FcsError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnstack_fcs.so")
+
+__all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
+           "batch_host", "tx_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
+           "tables_blob", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+
+# Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
+EXPORTS = [
+    "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
+    "fcs_last_error", "fcs_engine_version", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "fcs_host_alloc",
+    "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
+    "fcs_tables_blob",
+]
+
+
+class FcsError(RuntimeError):
+    def __init__(self, rc: int, what: str):
+        self.rc = rc
+        name = errno.errorcode.get(-rc, str(rc)) if rc < 0 else str(rc)
+        super().__init__(f"{what}: {name}: {_last_error()}")
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load the product library (raises FcsError with a clear message if it is not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise FcsError(-errno.ENOENT, f"{path} not built (run `make -C nstack_amd`)")
+    L = ctypes.CDLL(path)
+    c = ctypes
+    u64, u32, vp, i32 = c.c_uint64, c.c_uint32, c.c_void_p, c.c_int
+    sig = {
+        "ether_fcs": (u32, [vp, c.c_size_t]),
+        "fcs_engine_init": (i32, [i32]),
+        "fcs_engine_fini": (None, []),
+        "fcs_engine_device_count": (i32, []),
+        "fcs_last_error": (c.c_char_p, []),
+        "fcs_engine_version": (c.c_char_p, []),
+        "ether_fcs_batch_dev": (i32, [vp, u64, vp, vp, vp, u64, vp]),
+        "ether_fcs_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp]),
+        "ether_fcs_batch_host": (i32, [vp, u64, vp, vp, vp, u64]),
+        "ether_fcs_fixed_host": (i32, [vp, u64, u32, u64, vp]),
+        "ether_fcs_tx_host": (i32, [vp, u64, vp, u64]),
+        "fcs_host_alloc": (vp, [u64]),
+        "fcs_host_free": (None, [vp]),
+        "fcs_fill_splitmix64_dev": (i32, [vp, u64, u64, u64, vp]),
+        "fcs_read_stream_dev": (i32, [vp, u64, vp, vp]),
+        "fcs_timed_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, i32, c.POINTER(c.c_float)]),
+        "fcs_tables_blob": (i32, [vp, u64]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def lib() -> ctypes.CDLL:
+    return load()
+
+
+def _last_error() -> str:
+    if _lib is None:
+        return ""
+    s = _lib.fcs_last_error()
+    return s.decode() if s else ""
+
+
+def _check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise FcsError(rc, what)
+    return rc
+
+
+def version() -> str:
+    return load().fcs_engine_version().decode()
+
+
+def engine_init(ndev: int = 0) -> int:
+    return _check(load().fcs_engine_init(ndev), "fcs_engine_init")
+
+
+def engine_fini() -> None:
+    load().fcs_engine_fini()
+
+
+def ether_fcs(data) -> int:
+    """Drop-in single frame (src/ether_fcs.c:4): FCS of a bytes-like object, via the GPU."""
+    b = bytes(data)
+    return load().ether_fcs(b, len(b))
+
+
+def _ptr(x):
+    """Raw pointer of a torch tensor, numpy array, int, or None."""
+    if x is None:
+        return None
+    if isinstance(x, int):
+        return x
+    if hasattr(x, "data_ptr"):
+        return x.data_ptr()
+    if hasattr(x, "ctypes"):
+        return x.ctypes.data
+    raise TypeError(f"cannot take a pointer of {type(x)}")
+
+
+def _stream(stream):
+    if stream is None:
+        return None
+    if isinstance(stream, int):
+        return stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def fixed_dev(base, stride: int, length: int, n: int, out, stream=None) -> None:
+    _check(load().ether_fcs_fixed_dev(_ptr(base), stride, length, n, _ptr(out), _stream(stream)),
+           "ether_fcs_fixed_dev")
+
+
+def batch_dev(arena, arena_bytes: int, off, length, out, n: int, stream=None) -> None:
+    _check(load().ether_fcs_batch_dev(_ptr(arena), arena_bytes, _ptr(off), _ptr(length), _ptr(out),
+                                      n, _stream(stream)), "ether_fcs_batch_dev")
+
+
+def fixed_host(base, stride: int, length: int, n: int, out) -> None:
+    _check(load().ether_fcs_fixed_host(_ptr(base), stride, length, n, _ptr(out)),
+           "ether_fcs_fixed_host")
+
+
+def batch_host(arena, arena_bytes: int, off, length, out, n: int) -> None:
+    _check(load().ether_fcs_batch_host(_ptr(arena), arena_bytes, _ptr(off), _ptr(length), _ptr(out),
+                                       n), "ether_fcs_batch_host")
+
+
+def tx_host(base, stride: int, length, n: int) -> None:
+    _check(load().ether_fcs_tx_host(_ptr(base), stride, _ptr(length), n), "ether_fcs_tx_host")
+
+
+def fill_splitmix_dev(ptr, nbytes: int, seed: int, byte_offset: int = 0, stream=None) -> None:
+    _check(load().fcs_fill_splitmix64_dev(_ptr(ptr), nbytes, seed, byte_offset, _stream(stream)),
+           "fcs_fill_splitmix64_dev")
+
+
+def read_stream_dev(ptr, nbytes: int, sink, stream=None) -> None:
+    _check(load().fcs_read_stream_dev(_ptr(ptr), nbytes, _ptr(sink), _stream(stream)),
+           "fcs_read_stream_dev")
+
+
+def timed_fixed_dev(base, stride: int, length: int, n: int, out, stream=None, reps: int = 10) -> float:
+    ms = ctypes.c_float(0.0)
+    _check(load().fcs_timed_fixed_dev(_ptr(base), stride, length, n, _ptr(out), _stream(stream),
+                                      reps, ctypes.byref(ms)), "fcs_timed_fixed_dev")
+    return float(ms.value)
+
+
+def tables_blob():
+    import numpy as np
+    buf = np.zeros(8192, dtype=np.uint32)
+    n = _check(load().fcs_tables_blob(buf.ctypes.data, buf.size), "fcs_tables_blob")
+    return buf[:n].copy()

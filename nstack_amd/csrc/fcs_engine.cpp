@@ -1,0 +1,674 @@
+// fcs_engine.cpp — the C ABI (include/nstack_fcs.h) around the gfx950 FCS kernel.
+//
+// Replaces ether_fcs() (/root/reference/src/ether_fcs.c:4-19, prototype src/nstack_ether.h:80)
+// and provides the batched forms its TX call site (src/linux/ether.c:262-263) needs.
+// Per-device state (constant tables in HBM, staging buffers, streams) is created lazily and is
+// safe to use from many threads. There is deliberately no CPU CRC path in this library: every
+// FCS is computed by the HIP kernel, and a missing GPU or code object is reported as an error
+// (or, for the error-less drop-in ether_fcs, an abort with the reason on stderr).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "../../include/nstack_fcs.h"
+#include "fcs_launch.hpp"
+#include "fcs_tables.hpp"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int err, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return -err;
+}
+
+int hip_fail(hipError_t e, const char *what) {
+    const int err = (e == hipErrorNoDevice || e == hipErrorInvalidDevice ||
+                     e == hipErrorNoBinaryForGpu || e == hipErrorInvalidDeviceFunction ||
+                     e == hipErrorInvalidImage || e == hipErrorSharedObjectInitFailed)
+                        ? ENODEV
+                        : (e == hipErrorOutOfMemory ? ENOMEM : EIO);
+    return fail(err, "%s: %s", what, hipGetErrorString(e));
+}
+
+#define HIPTRY(expr, what)                        \
+    do {                                          \
+        hipError_t e_ = (expr);                   \
+        if (e_ != hipSuccess) return hip_fail(e_, what); \
+    } while (0)
+
+// Double-buffered host pipeline resources of one device.
+struct Pipe {
+    static constexpr int kDepth = 2;
+    hipStream_t stream = nullptr;
+    hipEvent_t done[kDepth] = {nullptr, nullptr};
+    uint8_t *d_in[kDepth] = {nullptr, nullptr};
+    uint8_t *h_in[kDepth] = {nullptr, nullptr};           // pinned staging
+    uint64_t *d_off[kDepth] = {nullptr, nullptr};
+    uint32_t *d_len[kDepth] = {nullptr, nullptr};
+    uint32_t *d_out[kDepth] = {nullptr, nullptr};
+    uint64_t *h_off[kDepth] = {nullptr, nullptr};          // pinned
+    uint32_t *h_len[kDepth] = {nullptr, nullptr};          // pinned
+    uint32_t *h_out[kDepth] = {nullptr, nullptr};          // pinned
+    uint64_t cap_bytes = 0, cap_frames = 0;
+};
+
+struct DevState {
+    int dev = -1;
+    int cus = 0;
+    uint32_t *d_blob = nullptr;
+    std::mutex pipe_mu;      // one host pipeline at a time per device
+    Pipe pipe;
+    std::mutex one_mu;       // single-frame (drop-in ether_fcs) staging
+    hipStream_t one_stream = nullptr;
+    uint8_t *one_d = nullptr, *one_h = nullptr;
+    uint32_t *one_dout = nullptr, *one_hout = nullptr;
+    uint64_t one_cap = 0;
+};
+
+std::mutex g_mu;
+std::vector<std::unique_ptr<DevState>> g_dev;   // indexed by HIP device ordinal
+std::vector<int> g_engine_devs;                  // devices used by the host batch APIs
+const fcs::Tables &tables() {
+    static const fcs::Tables t;
+    return t;
+}
+
+int dev_state(int dev, DevState **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return fail(ENODEV, "no HIP device visible (%s)", hipGetErrorString(e));
+    if (dev < 0 || dev >= ndev) return fail(EINVAL, "device %d out of range (%d devices)", dev, ndev);
+    if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
+    if (!g_dev[dev]) {
+        auto st = std::make_unique<DevState>();
+        st->dev = dev;
+        int cur = 0;
+        HIPTRY(hipGetDevice(&cur), "hipGetDevice");
+        HIPTRY(hipSetDevice(dev), "hipSetDevice");
+        hipDeviceProp_t prop;
+        hipError_t pe = hipGetDeviceProperties(&prop, dev);
+        if (pe != hipSuccess) { hipSetDevice(cur); return hip_fail(pe, "hipGetDeviceProperties"); }
+        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+            hipSetDevice(cur);
+            return fail(ENODEV, "device %d is %s; this engine is built for gfx950 only", dev, prop.gcnArchName);
+        }
+        st->cus = prop.multiProcessorCount;
+        const std::vector<uint32_t> blob = tables().blob();
+        hipError_t ae = hipMalloc(&st->d_blob, blob.size() * 4);
+        if (ae == hipSuccess) ae = hipMemcpy(st->d_blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice);
+        hipSetDevice(cur);
+        if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
+        g_dev[dev] = std::move(st);
+    }
+    *out = g_dev[dev].get();
+    return 0;
+}
+
+int current_dev_state(DevState **out) {
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return hip_fail(e, "hipGetDevice");
+    return dev_state(dev, out);
+}
+
+inline uint64_t floor4(uint64_t x) { return x & ~3ull; }
+inline uint64_t ceil4(uint64_t x) { return (x + 3) & ~3ull; }
+
+uint32_t segments(uint32_t len) { return len ? (len + fcs::kSegBytes - 1) / fcs::kSegBytes : 1u; }
+
+// Leading zero bytes of the front lane of segment 0 for a frame of length len.
+uint32_t front_zeros(uint32_t len) {
+    if (!len) return 0;
+    const uint32_t l0 = len - fcs::kSegBytes * (segments(len) - 1);
+    return fcs::kChunkBytes * ((l0 + fcs::kChunkBytes - 1) / fcs::kChunkBytes) - l0;
+}
+
+int grid_for(const DevState *ds, uint64_t n) {
+    const uint64_t want = (n + 31) / 32;   // 32 half-wave frame slots per workgroup
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ds->cus, want));
+}
+
+int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                 uint32_t *out, hipStream_t st) {
+    fcs::KParams p{};
+    p.base = (uint64_t)base;
+    p.stride = stride;
+    p.out = out;
+    p.n = n;
+    p.lo4 = floor4((uint64_t)base);
+    p.hi4 = ceil4((uint64_t)base + (n - 1) * stride + len);
+    p.flen = len;
+    p.fseg = segments(len);
+    p.zmax = front_zeros(len);
+    p.blob = ds->d_blob;
+    HIPTRY(fcs::launch_fcs(false, p, grid_for(ds, n), st), "launching fcs_kernel<fixed>");
+    return 0;
+}
+
+int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint64_t *off,
+               const uint32_t *len, uint32_t *out, uint64_t n, hipStream_t st) {
+    fcs::KParams p{};
+    p.base = (uint64_t)arena;
+    p.off = off;
+    p.len = len;
+    p.out = out;
+    p.n = n;
+    p.lo4 = floor4((uint64_t)arena);
+    p.hi4 = ceil4((uint64_t)arena + arena_bytes);
+    p.zmax = fcs::kChunkBytes;
+    p.blob = ds->d_blob;
+    HIPTRY(fcs::launch_fcs(true, p, grid_for(ds, n), st), "launching fcs_kernel<var>");
+    return 0;
+}
+
+int ensure_pipe(DevState *ds, uint64_t bytes, uint64_t frames) {
+    Pipe &pp = ds->pipe;
+    if (!pp.stream) {
+        HIPTRY(hipStreamCreateWithFlags(&pp.stream, hipStreamNonBlocking), "hipStreamCreate");
+        for (int b = 0; b < Pipe::kDepth; b++)
+            HIPTRY(hipEventCreateWithFlags(&pp.done[b], hipEventDisableTiming), "hipEventCreate");
+    }
+    if (bytes > pp.cap_bytes) {
+        for (int b = 0; b < Pipe::kDepth; b++) {
+            if (pp.d_in[b]) hipFree(pp.d_in[b]);
+            if (pp.h_in[b]) hipHostFree(pp.h_in[b]);
+            pp.d_in[b] = nullptr;
+            pp.h_in[b] = nullptr;
+        }
+        pp.cap_bytes = 0;
+        for (int b = 0; b < Pipe::kDepth; b++) {
+            HIPTRY(hipMalloc(&pp.d_in[b], bytes + 64), "hipMalloc(staging)");
+            HIPTRY(hipHostMalloc(&pp.h_in[b], bytes + 64, hipHostMallocDefault), "hipHostMalloc(staging)");
+        }
+        pp.cap_bytes = bytes;
+    }
+    if (frames > pp.cap_frames) {
+        for (int b = 0; b < Pipe::kDepth; b++) {
+            if (pp.d_off[b]) hipFree(pp.d_off[b]);
+            if (pp.d_len[b]) hipFree(pp.d_len[b]);
+            if (pp.d_out[b]) hipFree(pp.d_out[b]);
+            if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
+            if (pp.h_len[b]) hipHostFree(pp.h_len[b]);
+            if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
+            pp.d_off[b] = nullptr; pp.d_len[b] = nullptr; pp.d_out[b] = nullptr;
+            pp.h_off[b] = nullptr; pp.h_len[b] = nullptr; pp.h_out[b] = nullptr;
+        }
+        pp.cap_frames = 0;
+        for (int b = 0; b < Pipe::kDepth; b++) {
+            HIPTRY(hipMalloc(&pp.d_off[b], frames * 8), "hipMalloc(off)");
+            HIPTRY(hipMalloc(&pp.d_len[b], frames * 4), "hipMalloc(len)");
+            HIPTRY(hipMalloc(&pp.d_out[b], frames * 4), "hipMalloc(out)");
+            HIPTRY(hipHostMalloc(&pp.h_off[b], frames * 8, hipHostMallocDefault), "hipHostMalloc(off)");
+            HIPTRY(hipHostMalloc(&pp.h_len[b], frames * 4, hipHostMallocDefault), "hipHostMalloc(len)");
+            HIPTRY(hipHostMalloc(&pp.h_out[b], frames * 4, hipHostMallocDefault), "hipHostMalloc(out)");
+        }
+        pp.cap_frames = frames;
+    }
+    return 0;
+}
+
+bool is_pinned(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
+}
+
+// A chunk of host frames handed to one device: frames [i0, i1) of the caller's arrays.
+struct HostJob {
+    const uint8_t *arena;          // var: arena base; fixed/tx: frame 0
+    uint64_t arena_bytes;
+    const uint64_t *off;           // var only (nullptr: frame i at i*stride)
+    const uint32_t *len;           // var/tx lengths (nullptr: fixed len)
+    uint64_t stride;
+    uint32_t flen;
+    uint32_t *out;                 // crc per frame (nullptr in TX mode)
+    uint8_t *tx_base;              // TX: write FCS after each frame
+    uint64_t i0, i1;
+};
+
+constexpr uint64_t kChunkBytesHost = 128ull << 20;   // per pipeline slot
+constexpr uint64_t kChunkFramesMax = 1ull << 20;
+
+// Runs the chunked H2D -> kernel -> D2H pipeline of one device over frames [i0, i1).
+int run_host_job(DevState *ds, const HostJob &job) {
+    std::lock_guard<std::mutex> lk(ds->pipe_mu);
+    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    int rc = ensure_pipe(ds, kChunkBytesHost + 2 * fcs::kSegBytes, kChunkFramesMax);
+    if (rc) return rc;
+    Pipe &pp = ds->pipe;
+    const bool var = job.off || job.len;
+    const bool src_pinned = is_pinned(job.arena);
+
+    struct Pending { bool live = false; uint64_t i0 = 0, n = 0; } pend[Pipe::kDepth];
+    auto drain = [&](int b) -> int {
+        if (!pend[b].live) return 0;
+        HIPTRY(hipEventSynchronize(pp.done[b]), "hipEventSynchronize");
+        for (uint64_t q = 0; q < pend[b].n; q++) {
+            const uint64_t i = pend[b].i0 + q;
+            const uint32_t c = pp.h_out[b][q];
+            if (job.out) job.out[i] = c;
+            if (job.tx_base) {   // src/linux/ether.c:263 — memcpy of the host-order u32
+                uint8_t *dst = job.tx_base + i * job.stride + job.len[i];
+                std::memcpy(dst, &c, 4);
+            }
+        }
+        pend[b].live = false;
+        return 0;
+    };
+
+    uint64_t i = job.i0;
+    int slot = 0;
+    while (i < job.i1) {
+        const int b = slot % Pipe::kDepth;
+        if ((rc = drain(b))) return rc;
+        // ---- choose the chunk [i, e) and the host byte span it needs ----
+        uint64_t e = i, lo = 0, hi = 0, sum = 0;
+        if (!job.off) {
+            // frame q at arena + q*stride; span [i*stride, (e-1)*stride + len_q)
+            const uint64_t per = std::max<uint64_t>(job.stride, 1);
+            uint64_t cnt = std::min<uint64_t>(std::max<uint64_t>(1, kChunkBytesHost / per), kChunkFramesMax);
+            e = std::min(job.i1, i + cnt);
+            lo = i * job.stride;
+            uint32_t lastlen = job.len ? job.len[e - 1] : job.flen;
+            hi = (e - 1) * job.stride + lastlen;
+            if (job.len)
+                for (uint64_t q = i; q < e; q++) hi = std::max<uint64_t>(hi, q * job.stride + job.len[q]);
+            if (hi - lo > kChunkBytesHost + 2 * fcs::kSegBytes) {   // a single giant frame
+                if (e - i > 1) { e = i + 1; hi = i * job.stride + (job.len ? job.len[i] : job.flen); }
+                else return fail(EINVAL, "frame %llu of %llu bytes exceeds the %llu-byte host chunk",
+                                 (unsigned long long)i, (unsigned long long)(hi - lo),
+                                 (unsigned long long)kChunkBytesHost);
+            }
+        } else {
+            lo = UINT64_MAX;
+            hi = 0;
+            while (e < job.i1 && e - i < kChunkFramesMax) {
+                const uint64_t a = job.off[e], z = a + job.len[e];
+                const uint64_t nlo = std::min(lo, a), nhi = std::max(hi, z);
+                if (e > i && (nhi - nlo > kChunkBytesHost || sum + job.len[e] > kChunkBytesHost)) break;
+                lo = nlo; hi = nhi; sum += job.len[e];
+                e++;
+            }
+            if (hi - lo > kChunkBytesHost + 2 * fcs::kSegBytes && e - i == 1)
+                return fail(EINVAL, "frame %llu of %llu bytes exceeds the %llu-byte host chunk",
+                            (unsigned long long)i, (unsigned long long)job.len[i],
+                            (unsigned long long)kChunkBytesHost);
+        }
+        const uint64_t n = e - i;
+        uint64_t span = hi - lo;
+        const bool gather = job.off && span > kChunkBytesHost;   // sparse: pack frames
+        const uint8_t *src = job.arena + lo;
+        if (gather) {
+            uint64_t w = 0;
+            for (uint64_t q = 0; q < n; q++) {
+                std::memcpy(pp.h_in[b] + w, job.arena + job.off[i + q], job.len[i + q]);
+                pp.h_off[b][q] = w;
+                pp.h_len[b][q] = job.len[i + q];
+                w += job.len[i + q];
+            }
+            span = w;
+            src = pp.h_in[b];
+        } else {
+            if (var) {
+                for (uint64_t q = 0; q < n; q++) {
+                    pp.h_off[b][q] = job.off ? job.off[i + q] - lo : (i + q) * job.stride - lo;
+                    pp.h_len[b][q] = job.len[i + q];
+                }
+            }
+            if (!src_pinned) {
+                std::memcpy(pp.h_in[b], src, span);
+                src = pp.h_in[b];
+            }
+        }
+        HIPTRY(hipMemcpyAsync(pp.d_in[b], src, span, hipMemcpyHostToDevice, pp.stream), "H2D frames");
+        if (var) {
+            HIPTRY(hipMemcpyAsync(pp.d_off[b], pp.h_off[b], n * 8, hipMemcpyHostToDevice, pp.stream), "H2D off");
+            HIPTRY(hipMemcpyAsync(pp.d_len[b], pp.h_len[b], n * 4, hipMemcpyHostToDevice, pp.stream), "H2D len");
+            rc = launch_var(ds, pp.d_in[b], span, pp.d_off[b], pp.d_len[b], pp.d_out[b], n, pp.stream);
+        } else {
+            rc = launch_fixed(ds, pp.d_in[b], job.stride, job.flen, n, pp.d_out[b], pp.stream);
+        }
+        if (rc) return rc;
+        HIPTRY(hipMemcpyAsync(pp.h_out[b], pp.d_out[b], n * 4, hipMemcpyDeviceToHost, pp.stream), "D2H crc");
+        HIPTRY(hipEventRecord(pp.done[b], pp.stream), "hipEventRecord");
+        pend[b].live = true;
+        pend[b].i0 = i;
+        pend[b].n = n;
+        i = e;
+        slot++;
+    }
+    for (int b = 0; b < Pipe::kDepth; b++)
+        if ((rc = drain(b))) return rc;
+    return 0;
+}
+
+int engine_devices(std::vector<DevState *> *out) {
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (g_engine_devs.empty()) {
+            int ndev = 0;
+            hipError_t e = hipGetDeviceCount(&ndev);
+            if (e != hipSuccess || ndev <= 0) return fail(ENODEV, "no HIP device visible (%s)", hipGetErrorString(e));
+            for (int d = 0; d < ndev; d++) g_engine_devs.push_back(d);
+        }
+    }
+    std::vector<int> devs;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        devs = g_engine_devs;
+    }
+    out->clear();
+    for (int d : devs) {
+        DevState *ds = nullptr;
+        int rc = dev_state(d, &ds);
+        if (rc) return rc;
+        out->push_back(ds);
+    }
+    return 0;
+}
+
+// Shard [0, n) over the engine devices (contiguous ranges, byte-balanced when lengths are known).
+int run_host_sharded(HostJob job, uint64_t n) {
+    if (n == 0) return 0;
+    std::vector<DevState *> devs;
+    int rc = engine_devices(&devs);
+    if (rc) return rc;
+    const uint64_t G = std::min<uint64_t>(devs.size(), std::max<uint64_t>(1, n / 1024));
+    std::vector<uint64_t> cut(G + 1, 0);
+    cut[G] = n;
+    if (job.len) {
+        uint64_t tot = 0;
+        for (uint64_t i = 0; i < n; i++) tot += job.len[i];
+        uint64_t acc = 0, g = 1;
+        for (uint64_t i = 0; i < n && g < G; i++) {
+            acc += job.len[i];
+            while (g < G && acc * G >= tot * g) cut[g++] = i + 1;
+        }
+        for (; g < G; g++) cut[g] = n;
+    } else {
+        for (uint64_t g = 1; g < G; g++) cut[g] = n * g / G;
+    }
+    if (G == 1) {
+        job.i0 = 0;
+        job.i1 = n;
+        return run_host_job(devs[0], job);
+    }
+    std::vector<int> rcs(G, 0);
+    std::vector<std::string> errs(G);
+    std::vector<std::thread> th;
+    for (uint64_t g = 0; g < G; g++) {
+        th.emplace_back([&, g] {
+            HostJob jj = job;
+            jj.i0 = cut[g];
+            jj.i1 = cut[g + 1];
+            rcs[g] = jj.i0 < jj.i1 ? run_host_job(devs[g], jj) : 0;
+            errs[g] = g_last_error;
+        });
+    }
+    for (auto &t : th) t.join();
+    for (uint64_t g = 0; g < G; g++)
+        if (rcs[g]) {
+            g_last_error = errs[g];
+            return rcs[g];
+        }
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *fcs_last_error(void) { return g_last_error.c_str(); }
+
+const char *fcs_engine_version(void) {
+    return "nstack-fcs 0.1 gfx950: half-wave/frame, 48B chunks, slice-by-4 LDS x32 replicas, "
+           "v_perm addressing, DPP reduce";
+}
+
+int fcs_engine_init(int ndev) {
+    int total = 0;
+    hipError_t e = hipGetDeviceCount(&total);
+    if (e != hipSuccess || total <= 0) return fail(ENODEV, "no HIP device visible (%s)", hipGetErrorString(e));
+    const int use = (ndev <= 0 || ndev > total) ? total : ndev;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        g_engine_devs.clear();
+        for (int d = 0; d < use; d++) g_engine_devs.push_back(d);
+    }
+    for (int d = 0; d < use; d++) {
+        DevState *ds = nullptr;
+        int rc = dev_state(d, &ds);
+        if (rc) return rc;
+    }
+    return use;
+}
+
+void fcs_engine_fini(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    for (auto &up : g_dev) {
+        if (!up) continue;
+        DevState *ds = up.get();
+        hipSetDevice(ds->dev);
+        Pipe &pp = ds->pipe;
+        for (int b = 0; b < Pipe::kDepth; b++) {
+            if (pp.done[b]) hipEventDestroy(pp.done[b]);
+            if (pp.d_in[b]) hipFree(pp.d_in[b]);
+            if (pp.h_in[b]) hipHostFree(pp.h_in[b]);
+            if (pp.d_off[b]) hipFree(pp.d_off[b]);
+            if (pp.d_len[b]) hipFree(pp.d_len[b]);
+            if (pp.d_out[b]) hipFree(pp.d_out[b]);
+            if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
+            if (pp.h_len[b]) hipHostFree(pp.h_len[b]);
+            if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
+        }
+        if (pp.stream) hipStreamDestroy(pp.stream);
+        if (ds->one_stream) hipStreamDestroy(ds->one_stream);
+        if (ds->one_d) hipFree(ds->one_d);
+        if (ds->one_h) hipHostFree(ds->one_h);
+        if (ds->one_dout) hipFree(ds->one_dout);
+        if (ds->one_hout) hipHostFree(ds->one_hout);
+        if (ds->d_blob) hipFree(ds->d_blob);
+    }
+    g_dev.clear();
+    g_engine_devs.clear();
+    hipSetDevice(cur);
+}
+
+int fcs_engine_device_count(void) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_engine_devs.empty()) return (int)g_engine_devs.size();
+    int total = 0;
+    if (hipGetDeviceCount(&total) != hipSuccess) return 0;
+    return total;
+}
+
+int ether_fcs_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                        uint32_t *out, void *stream) {
+    if (n == 0) return 0;
+    if (!base || !out) return fail(EINVAL, "null pointer");
+    if (n > 1 && stride < len) return fail(EINVAL, "stride %llu < len %u", (unsigned long long)stride, len);
+    DevState *ds = nullptr;
+    int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    return launch_fixed(ds, base, stride, len, n, out, (hipStream_t)stream);
+}
+
+int ether_fcs_batch_dev(const void *arena, uint64_t arena_bytes, const uint64_t *off,
+                        const uint32_t *len, uint32_t *out, uint64_t n, void *stream) {
+    if (n == 0) return 0;
+    if (!arena || !off || !len || !out) return fail(EINVAL, "null pointer");
+    DevState *ds = nullptr;
+    int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    return launch_var(ds, arena, arena_bytes, off, len, out, n, (hipStream_t)stream);
+}
+
+int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
+                         const uint32_t *len, uint32_t *out, uint64_t n) {
+    if (n == 0) return 0;
+    if (!arena || !off || !len || !out) return fail(EINVAL, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i] > arena_bytes || len[i] > arena_bytes - off[i])
+            return fail(EINVAL, "frame %llu [%llu, +%u) outside the %llu-byte arena", (unsigned long long)i,
+                        (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, out, nullptr, 0, n};
+    return run_host_sharded(job, n);
+}
+
+int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                         uint32_t *out) {
+    if (n == 0) return 0;
+    if (!base || !out) return fail(EINVAL, "null pointer");
+    if (n > 1 && stride < len) return fail(EINVAL, "stride %llu < len %u", (unsigned long long)stride, len);
+    HostJob job{(const uint8_t *)base, (n - 1) * stride + len, nullptr, nullptr, n > 1 ? stride : len, len,
+                out, nullptr, 0, n};
+    return run_host_sharded(job, n);
+}
+
+int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n) {
+    if (n == 0) return 0;
+    if (!base || !len) return fail(EINVAL, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if ((uint64_t)len[i] + 4 > stride)
+            return fail(EINVAL, "frame %llu: len %u + FCS does not fit stride %llu", (unsigned long long)i,
+                        len[i], (unsigned long long)stride);
+    HostJob job{(const uint8_t *)base, n * stride, nullptr, len, stride, 0, nullptr, (uint8_t *)base, 0, n};
+    return run_host_sharded(job, n);
+}
+
+// Drop-in for src/ether_fcs.c:4. Synchronous, reentrant (per-device lock around the staging).
+uint32_t ether_fcs(const void *data, size_t bsize) {
+    if (bsize == 0) return 0;   // src/ether_fcs.c: the loop does not run, crc stays 0
+    DevState *ds = nullptr;
+    int dev = 0;
+    int rc = 0;
+    {
+        std::vector<DevState *> devs;
+        rc = engine_devices(&devs);
+        if (!rc) ds = devs[0];
+    }
+    if (rc) {
+        std::fprintf(stderr, "nstack_fcs: ether_fcs: no usable GPU engine: %s\n", g_last_error.c_str());
+        std::abort();
+    }
+    dev = ds->dev;
+    std::lock_guard<std::mutex> lk(ds->one_mu);
+    auto die = [](const char *what, hipError_t e) {
+        std::fprintf(stderr, "nstack_fcs: ether_fcs: %s: %s\n", what, hipGetErrorString(e));
+        std::abort();
+    };
+    int cur = 0;
+    hipError_t e = hipGetDevice(&cur);
+    if (e != hipSuccess) die("hipGetDevice", e);
+    if ((e = hipSetDevice(dev)) != hipSuccess) die("hipSetDevice", e);
+    if (!ds->one_stream) {
+        if ((e = hipStreamCreateWithFlags(&ds->one_stream, hipStreamNonBlocking)) != hipSuccess) die("stream", e);
+        if ((e = hipMalloc(&ds->one_dout, 64)) != hipSuccess) die("hipMalloc", e);
+        if ((e = hipHostMalloc(&ds->one_hout, 64, hipHostMallocDefault)) != hipSuccess) die("hipHostMalloc", e);
+    }
+    if (bsize > ds->one_cap) {
+        if (ds->one_d) hipFree(ds->one_d);
+        if (ds->one_h) hipHostFree(ds->one_h);
+        uint64_t cap = std::max<uint64_t>(4096, bsize + 64);
+        if ((e = hipMalloc(&ds->one_d, cap)) != hipSuccess) die("hipMalloc", e);
+        if ((e = hipHostMalloc(&ds->one_h, cap, hipHostMallocDefault)) != hipSuccess) die("hipHostMalloc", e);
+        ds->one_cap = cap - 64;
+    }
+    std::memcpy(ds->one_h, data, bsize);
+    if ((e = hipMemcpyAsync(ds->one_d, ds->one_h, bsize, hipMemcpyHostToDevice, ds->one_stream)) != hipSuccess)
+        die("H2D", e);
+    rc = launch_fixed(ds, ds->one_d, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);
+    if (rc) {
+        std::fprintf(stderr, "nstack_fcs: ether_fcs: %s\n", g_last_error.c_str());
+        std::abort();
+    }
+    if ((e = hipMemcpyAsync(ds->one_hout, ds->one_dout, 4, hipMemcpyDeviceToHost, ds->one_stream)) != hipSuccess)
+        die("D2H", e);
+    if ((e = hipStreamSynchronize(ds->one_stream)) != hipSuccess) die("sync", e);
+    const uint32_t c = ds->one_hout[0];
+    hipSetDevice(cur);
+    return c;
+}
+
+void *fcs_host_alloc(uint64_t bytes) {
+    void *p = nullptr;
+    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+        fail(ENOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
+        return nullptr;
+    }
+    return p;
+}
+
+void fcs_host_free(void *p) {
+    if (p) hipHostFree(p);
+}
+
+int fcs_fill_splitmix64_dev(void *p, uint64_t bytes, uint64_t seed, uint64_t byte_offset, void *stream) {
+    if (!bytes) return 0;
+    if (!p) return fail(EINVAL, "null pointer");
+    HIPTRY(fcs::launch_fill(p, bytes, seed, byte_offset, (hipStream_t)stream), "launching fill");
+    return 0;
+}
+
+int fcs_read_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream) {
+    if (!p || !sink) return fail(EINVAL, "null pointer");
+    HIPTRY(fcs::launch_read_stream(p, bytes, sink, (hipStream_t)stream), "launching read stream");
+    return 0;
+}
+
+int fcs_timed_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n, uint32_t *out,
+                        void *stream, int reps, float *ms_per_launch) {
+    if (reps <= 0 || !ms_per_launch) return fail(EINVAL, "bad reps/out");
+    hipEvent_t a, b;
+    HIPTRY(hipEventCreate(&a), "hipEventCreate");
+    HIPTRY(hipEventCreate(&b), "hipEventCreate");
+    hipStream_t st = (hipStream_t)stream;
+    HIPTRY(hipEventRecord(a, st), "hipEventRecord");
+    for (int r = 0; r < reps; r++) {
+        int rc = ether_fcs_fixed_dev(base, stride, len, n, out, stream);
+        if (rc) return rc;
+    }
+    HIPTRY(hipEventRecord(b, st), "hipEventRecord");
+    HIPTRY(hipEventSynchronize(b), "hipEventSynchronize");
+    float ms = 0;
+    HIPTRY(hipEventElapsedTime(&ms, a, b), "hipEventElapsedTime");
+    hipEventDestroy(a);
+    hipEventDestroy(b);
+    *ms_per_launch = ms / (float)reps;
+    return 0;
+}
+
+// Introspection for the CPU test-suite: copy the constant table blob the kernel stages into LDS.
+// (Table construction is host code; it checksums no frame data.)
+int fcs_tables_blob(uint32_t *out, uint64_t words) {
+    const std::vector<uint32_t> b = tables().blob();
+    if (!out || words < b.size()) return fail(EINVAL, "need %zu words", b.size());
+    std::memcpy(out, b.data(), b.size() * 4);
+    return (int)b.size();
+}
+
+}  // extern "C"

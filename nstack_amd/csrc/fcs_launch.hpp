@@ -1,0 +1,30 @@
+// fcs_launch.hpp — host-side launchers implemented in fcs_kernel.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace fcs {
+
+struct KParams {
+    uint64_t base;          // fixed: frame 0 start; var: arena start
+    uint64_t stride;        // fixed only
+    const uint64_t *off;    // var only
+    const uint32_t *len;    // var only
+    uint32_t *out;
+    uint64_t n;             // frames
+    uint64_t lo4, hi4;      // readable byte range, dword-rounded (never crosses a page)
+    uint32_t flen;          // fixed: frame length
+    uint32_t fseg;          // fixed: segments per frame
+    uint32_t zmax;          // max leading zero bytes any front lane can see (mask loop bound)
+    const uint32_t *blob;   // constant tables (kBlobWords)
+};
+
+constexpr int kWgThreads = 1024;
+
+hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st);
+hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hipStream_t st);
+hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st);
+hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,
+                           uint64_t n, hipStream_t st);
+
+}  // namespace fcs

@@ -1,0 +1,93 @@
+// fcs_tables.hpp — host-side construction of the constant tables the FCS kernel keeps in LDS.
+//
+// The CRC in src/ether_fcs.c:4-19 is CRC-32/ISO-HDLC: a reflected LFSR over GF(2) with
+// polynomial 0xEDB88320 whose register starts and ends complemented. Writing A_n for the
+// linear operator "advance the register over n zero bytes", appending one 4-byte word w is
+// s' = A_4(s ^ w), and that is what the slice-by-4 tables T3..T0 evaluate. Everything the
+// kernel needs beyond that is an A_n (or its inverse) for a handful of n, tabulated by nibble:
+//   lane tables   L_j = A_{48 j}         j = 0..31   (shift lane j's chunk to the frame end)
+//   jump table    J   = A_{1488}                     (lane's chunk in segment k -> segment k+1)
+//   front init    INV[z] = A_z^{-1}(0xFFFFFFFF)      (register value that, after z leading
+//                                                     zero bytes, equals the all-ones init)
+// These are constants of the algorithm, computed once per process; no frame bytes are ever
+// checksummed on the host (the product has no CPU CRC path).
+#pragma once
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+namespace fcs {
+
+constexpr uint32_t kPoly = 0xEDB88320u;
+constexpr int kChunkBytes = 48;                       // bytes per lane per segment
+constexpr int kGroup = 32;                            // lanes per frame (half wave)
+constexpr int kSegBytes = kChunkBytes * kGroup;       // 1536
+constexpr int kJumpBytes = kSegBytes - kChunkBytes;   // 1488
+
+// LDS layout of the kernel (bytes). Data tables: T_k[b], replica r (= lane & 31) lives at
+//   half(k)*65536 + b*256 + odd(k)*128 + r*4    with T3,T2 in half 0 and T1,T0 in half 1,
+// so the address is one v_perm of {x.byte_k, lane constant} and every ds_read_b32 of a
+// 32-lane group hits 32 distinct banks.
+constexpr uint32_t kLdsData = 0;        // 131072 B
+constexpr uint32_t kLdsLane = 131072;   // 8 nibble tables x 16 entries x 32 lanes x 4 B = 16384
+constexpr uint32_t kLdsJump = 147456;   // 8 x 16 x 4 B = 512
+constexpr uint32_t kLdsInv = 147968;    // 48 x 4 B = 192 (+64 pad)
+constexpr uint32_t kLdsBytes = 148224;
+
+// Global "blob" the kernel copies into LDS at start (un-replicated forms).
+constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
+constexpr uint32_t kBlobLane = 1024;                    // uint32 [8][16][32] (LDS order)
+constexpr uint32_t kBlobJump = kBlobLane + 8 * 16 * 32; // uint32 [8][16]
+constexpr uint32_t kBlobInv = kBlobJump + 8 * 16;       // uint32 [64]
+constexpr uint32_t kBlobWords = kBlobInv + 64;
+
+struct Tables {
+    uint32_t T[4][256];
+    uint8_t top_inv[256];   // index i with (T0[i] >> 24) == byte (unique for a CRC table)
+
+    Tables() {
+        for (uint32_t b = 0; b < 256; b++) {
+            uint32_t r = b;
+            for (int i = 0; i < 8; i++) r = (r >> 1) ^ ((r & 1u) ? kPoly : 0u);
+            T[0][b] = r;
+        }
+        for (int k = 1; k < 4; k++)
+            for (int b = 0; b < 256; b++)
+                T[k][b] = (T[k - 1][b] >> 8) ^ T[0][T[k - 1][b] & 0xFF];
+        for (int b = 0; b < 256; b++) top_inv[T[0][b] >> 24] = (uint8_t)b;
+    }
+    // A_1: one zero byte.
+    uint32_t zstep(uint32_t s) const { return (s >> 8) ^ T[0][s & 0xFF]; }
+    // A_1^{-1}: s = (p >> 8) ^ T0[p & 0xFF]; the top byte of s names p & 0xFF.
+    uint32_t zunstep(uint32_t s) const {
+        uint32_t i = top_inv[s >> 24];
+        return ((s ^ T[0][i]) << 8) | i;
+    }
+    uint32_t shift(uint32_t s, long n) const {
+        for (; n > 0; n--) s = zstep(s);
+        for (; n < 0; n++) s = zunstep(s);
+        return s;
+    }
+    // Nibble table of A_n: entry [t][e] = A_n(e << 4t).
+    void nibble_table(long n, uint32_t out[8][16]) const {
+        for (int t = 0; t < 8; t++)
+            for (int e = 0; e < 16; e++) out[t][e] = shift((uint32_t)e << (4 * t), n);
+    }
+    std::vector<uint32_t> blob() const {
+        std::vector<uint32_t> b(kBlobWords, 0u);
+        for (int k = 0; k < 4; k++) std::memcpy(&b[kBlobSlice + 256 * k], T[k], 1024);
+        uint32_t nt[8][16];
+        for (int j = 0; j < kGroup; j++) {
+            nibble_table((long)kChunkBytes * j, nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobLane + (t * 16 + e) * 32 + j] = nt[t][e];
+        }
+        nibble_table(kJumpBytes, nt);
+        for (int t = 0; t < 8; t++)
+            for (int e = 0; e < 16; e++) b[kBlobJump + t * 16 + e] = nt[t][e];
+        for (int z = 0; z < kChunkBytes; z++) b[kBlobInv + z] = shift(0xFFFFFFFFu, -(long)z);
+        return b;
+    }
+};
+
+}  // namespace fcs

@@ -1,0 +1,217 @@
+/*
+ * oracle/fcs_oracle.c — TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
+ * The product library (nstack_amd/libnstack_fcs.so) contains no CPU CRC path.
+ *
+ * What it restates:
+ *   ether_fcs()  /root/reference/src/ether_fcs.c:4-19
+ *     - a 16-entry nibble table for the reflected CRC-32 polynomial 0xEDB88320 with the
+ *       register complement folded into the table (table[i] = T16[15 - i] ^ 0xF0000000,
+ *       src/ether_fcs.c:7-10), register initialised to 0 (:11), two table steps per byte,
+ *       low nibble first (:13-16), no final XOR (:18).
+ *     The table here is DERIVED from the polynomial at first use instead of being written
+ *     out, and oracle_selfcheck() verifies the derivation against the known answers in
+ *     SURVEY.md §8c ("123456789" -> 0xCBF43926, residue 0x2144DF1C).
+ *   A slice-by-8 variant (oracle_crc32_fast) computes the same function (CRC-32/ISO-HDLC)
+ *   about 10x faster; it is used to check multi-GiB GPU runs, never as the baseline.
+ *
+ * Pinning: tests/test_oracle.py checks both against the golden fixtures in tests/golden/
+ * (generated from the reference's own src/ether_fcs.c compiled by oracle/Makefile into
+ * oracle/_ref/, see tests/golden/make_golden.py) and against zlib.crc32.
+ *
+ * Data generators (shared with the GPU tests / bench so inputs can be re-created on CPU):
+ *   oracle_xorshift64_fill  — the SURVEY §8c/§8d dataset (seed 42, s^=s<<13; s^=s>>7;
+ *                             s^=s<<17; byte = low 8 bits of s after each step).
+ *   oracle_splitmix_fill    — counter-based bytes: 8-byte word w at byte offset 8*w is
+ *                             splitmix64(seed + w) little-endian; matches the device
+ *                             generator fcs_fill_splitmix64 in the product library.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <time.h>
+#include <pthread.h>
+
+#define POLY_REFLECTED 0xEDB88320u
+
+static uint32_t nib_table[16];   /* complement-folded nibble table (src/ether_fcs.c:7-10) */
+static uint32_t slice8[8][256];  /* standard reflected slice-by-8 tables */
+static int tables_ready;
+
+static uint32_t reflected_shift(uint32_t r, int bits)
+{
+    for (int b = 0; b < bits; b++)
+        r = (r >> 1) ^ ((r & 1u) ? POLY_REFLECTED : 0u);
+    return r;
+}
+
+static void build_tables(void)
+{
+    if (tables_ready)
+        return;
+    /* T16[k]: four reflected shift steps of k; folded: table[i] = T16[15-i] ^ 0xF0000000 */
+    for (int i = 0; i < 16; i++)
+        nib_table[i] = reflected_shift((uint32_t)(15 - i), 4) ^ 0xF0000000u;
+    for (int b = 0; b < 256; b++)
+        slice8[0][b] = reflected_shift((uint32_t)b, 8);
+    for (int k = 1; k < 8; k++)
+        for (int b = 0; b < 256; b++)
+            slice8[k][b] = (slice8[k - 1][b] >> 8) ^ slice8[0][slice8[k - 1][b] & 0xFF];
+    tables_ready = 1;
+}
+
+/* Restatement of ether_fcs (src/ether_fcs.c:4-19): register 0, folded table, 2 nibbles/byte. */
+uint32_t oracle_ether_fcs(const void *data, size_t bsize)
+{
+    const uint8_t *p = (const uint8_t *) data;
+    uint32_t r = 0;
+    if (!tables_ready)
+        build_tables();
+    for (size_t i = 0; i < bsize; i++) {
+        r = (r >> 4) ^ nib_table[(r ^ p[i]) & 0x0F];        /* low nibble  (:14) */
+        r = (r >> 4) ^ nib_table[(r ^ (p[i] >> 4)) & 0x0F]; /* high nibble (:15) */
+    }
+    return r;
+}
+
+/* Same function, slice-by-8 over the standard (non-folded) register: ~r in, ~r out. */
+uint32_t oracle_crc32_fast(const void *data, size_t n)
+{
+    const uint8_t *p = (const uint8_t *) data;
+    uint32_t r = 0xFFFFFFFFu;
+    if (!tables_ready)
+        build_tables();
+    while (n && ((uintptr_t) p & 7)) {
+        r = (r >> 8) ^ slice8[0][(r ^ *p++) & 0xFF];
+        n--;
+    }
+    while (n >= 8) {
+        uint32_t lo, hi;
+        memcpy(&lo, p, 4);
+        memcpy(&hi, p + 4, 4);
+        lo ^= r;
+        r = slice8[7][lo & 0xFF] ^ slice8[6][(lo >> 8) & 0xFF] ^
+            slice8[5][(lo >> 16) & 0xFF] ^ slice8[4][lo >> 24] ^
+            slice8[3][hi & 0xFF] ^ slice8[2][(hi >> 8) & 0xFF] ^
+            slice8[1][(hi >> 16) & 0xFF] ^ slice8[0][hi >> 24];
+        p += 8;
+        n -= 8;
+    }
+    while (n--)
+        r = (r >> 8) ^ slice8[0][(r ^ *p++) & 0xFF];
+    return ~r;
+}
+
+/* Batch helpers. fast=0 -> nibble restatement, fast=1 -> slice-by-8. */
+void oracle_fcs_batch(const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                      uint32_t *out, size_t n, int fast)
+{
+    for (size_t i = 0; i < n; i++)
+        out[i] = fast ? oracle_crc32_fast(arena + off[i], len[i])
+                      : oracle_ether_fcs(arena + off[i], len[i]);
+}
+
+struct fixed_job {
+    const uint8_t *base;
+    size_t stride, n;
+    uint32_t len;
+    uint32_t *out;
+    int fast;
+};
+
+static void *fixed_worker(void *arg)
+{
+    struct fixed_job *j = (struct fixed_job *) arg;
+    for (size_t i = 0; i < j->n; i++)
+        j->out[i] = j->fast ? oracle_crc32_fast(j->base + i * j->stride, j->len)
+                            : oracle_ether_fcs(j->base + i * j->stride, j->len);
+    return NULL;
+}
+
+/* Fixed-stride frames, optionally over nthreads host threads (contiguous shards). */
+void oracle_fcs_fixed(const uint8_t *base, size_t stride, uint32_t len, size_t n,
+                      uint32_t *out, int fast, int nthreads)
+{
+    if (!tables_ready)
+        build_tables();
+    if (nthreads <= 1) {
+        struct fixed_job j = {base, stride, n, len, out, fast};
+        fixed_worker(&j);
+        return;
+    }
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    struct fixed_job jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        size_t lo = n * (size_t) t / (size_t) nthreads;
+        size_t hi = n * (size_t)(t + 1) / (size_t) nthreads;
+        jobs[t] = (struct fixed_job){base + lo * stride, stride, hi - lo, len, out + lo, fast};
+        pthread_create(&th[t], NULL, fixed_worker, &jobs[t]);
+    }
+    for (int t = 0; t < nthreads; t++)
+        pthread_join(th[t], NULL);
+}
+
+/* Wall-clock seconds of oracle_fcs_fixed (for bench.py's cpu_baseline leg). */
+double oracle_time_fixed(const uint8_t *base, size_t stride, uint32_t len, size_t n,
+                         uint32_t *out, int fast, int nthreads)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    oracle_fcs_fixed(base, stride, len, n, out, fast, nthreads);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
+/* SURVEY §8c dataset: xorshift64, one output byte per step; *state carries across calls. */
+void oracle_xorshift64_fill(uint8_t *buf, size_t n, uint64_t *state)
+{
+    uint64_t s = *state;
+    for (size_t i = 0; i < n; i++) {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        buf[i] = (uint8_t) s;
+    }
+    *state = s;
+}
+
+static uint64_t splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+/* Bytes [byte_offset, byte_offset + n) of the counter-based stream for `seed`. */
+void oracle_splitmix_fill(uint8_t *buf, size_t n, uint64_t seed, uint64_t byte_offset)
+{
+    for (size_t i = 0; i < n; i++) {
+        uint64_t pos = byte_offset + i;
+        uint64_t w = splitmix64(seed + (pos >> 3));
+        buf[i] = (uint8_t)(w >> (8 * (pos & 7)));
+    }
+}
+
+/* 0 on success; checks the derived tables against SURVEY §8c known answers. */
+int oracle_selfcheck(void)
+{
+    static const char kv[] = "123456789";
+    uint8_t buf[64];
+    if (oracle_ether_fcs(kv, 9) != 0xCBF43926u || oracle_crc32_fast(kv, 9) != 0xCBF43926u)
+        return 1;
+    if (oracle_ether_fcs(kv, 0) != 0)
+        return 2;
+    for (int n = 0; n < 60; n++) {
+        for (int i = 0; i < n; i++)
+            buf[i] = (uint8_t)(i * 37 + 11);
+        uint32_t c = oracle_ether_fcs(buf, (size_t) n);
+        memcpy(buf + n, &c, 4);
+        if (oracle_ether_fcs(buf, (size_t) n + 4) != 0x2144DF1Cu)
+            return 3;
+    }
+    return 0;
+}

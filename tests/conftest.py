@@ -1,0 +1,51 @@
+"""Shared fixtures. Markers: `gpu` = needs an MI355X (run on the GPU box with -m gpu)."""
+import ctypes
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs a real MI355X (gfx950) GPU")
+
+
+def _build_oracle():
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"], check=True)
+    return so
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    """The CPU restatement of src/ether_fcs.c (test infrastructure only)."""
+    L = ctypes.CDLL(_build_oracle())
+    u64, u32, vp, i32 = ctypes.c_uint64, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_int
+    L.oracle_ether_fcs.restype = u32
+    L.oracle_ether_fcs.argtypes = [vp, ctypes.c_size_t]
+    L.oracle_crc32_fast.restype = u32
+    L.oracle_crc32_fast.argtypes = [vp, ctypes.c_size_t]
+    L.oracle_fcs_batch.argtypes = [vp, vp, vp, vp, ctypes.c_size_t, i32]
+    L.oracle_fcs_fixed.argtypes = [vp, ctypes.c_size_t, u32, ctypes.c_size_t, vp, i32, i32]
+    L.oracle_time_fixed.restype = ctypes.c_double
+    L.oracle_time_fixed.argtypes = [vp, ctypes.c_size_t, u32, ctypes.c_size_t, vp, i32, i32]
+    L.oracle_xorshift64_fill.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(u64)]
+    L.oracle_splitmix_fill.argtypes = [vp, ctypes.c_size_t, u64, u64]
+    L.oracle_selfcheck.restype = i32
+    return L
+
+
+@pytest.fixture(scope="session")
+def golden():
+    with open(os.path.join(GOLDEN, "vectors.json")) as f:
+        vec = json.load(f)
+    with open(os.path.join(GOLDEN, vec["arena"]), "rb") as f:
+        arena = f.read()
+    with open(os.path.join(GOLDEN, "kat.json")) as f:
+        kat = json.load(f)
+    return {"vectors": vec, "arena": arena, "kat": kat}

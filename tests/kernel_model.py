@@ -1,0 +1,119 @@
+"""Bit-level CPU model of the gfx950 FCS kernel's arithmetic (TEST INFRASTRUCTURE ONLY).
+
+It replays, per half-wave, exactly what nstack_amd/csrc/fcs_kernel.hip does — the LDS image the
+workgroup builds from the table blob, v_perm_b32 address formation, the slice-by-4 chain, the
+front-lane INV injection and masking, the segment jump, the per-lane shift and the XOR reduce —
+so table or layout mistakes show up on the CPU before any GPU time is spent. It is checked
+against the oracle (tests/test_kernel_model.py); it is never used to produce product results.
+"""
+import numpy as np
+
+CHUNK, GROUP = 48, 32
+SEG = CHUNK * GROUP
+LDS_LANE, LDS_JUMP, LDS_INV, LDS_BYTES = 131072, 147456, 147968, 148224
+BLOB_SLICE, BLOB_LANE = 0, 1024
+BLOB_JUMP = BLOB_LANE + 8 * 16 * 32
+BLOB_INV = BLOB_JUMP + 8 * 16
+
+
+def v_perm(s0, s1, sel):
+    data = ((s0 & 0xFFFFFFFF) << 32) | (s1 & 0xFFFFFFFF)
+    out = 0
+    for i in range(4):
+        b = (sel >> (8 * i)) & 0xFF
+        if b >= 13:
+            v = 0xFF
+        elif b == 12:
+            v = 0
+        elif b < 8:
+            v = (data >> (8 * b)) & 0xFF
+        else:
+            raise ValueError("sign-extension selectors unused")
+        out |= v << (8 * i)
+    return out
+
+
+def build_lds(blob):
+    lds = np.zeros(LDS_BYTES // 4, dtype=np.uint32)
+    for i in range(8192):
+        h, b, odd = i >> 12, (i >> 4) & 255, (i >> 3) & 1
+        k = (2 if odd else 3) if h == 0 else (0 if odd else 1)
+        lds[i * 4:i * 4 + 4] = blob[BLOB_SLICE + 256 * k + b]
+    n = BLOB_INV + 48 - BLOB_LANE
+    lds[LDS_LANE // 4:LDS_LANE // 4 + n] = blob[BLOB_LANE:BLOB_LANE + n]
+    return lds
+
+
+def rd(lds, addr):
+    assert addr % 4 == 0 and 0 <= addr < LDS_BYTES
+    return int(lds[addr // 4])
+
+
+def step4(lds, x, j):
+    base0, base1 = j * 4, 0x10000 | (j * 4)
+    a0 = v_perm(x, base0, 0x0C020400)
+    a1 = v_perm(x, base0, 0x0C020500)
+    a2 = v_perm(x, base1, 0x0C020600)
+    a3 = v_perm(x, base1, 0x0C020700)
+    return rd(lds, a0) ^ rd(lds, a1 + 128) ^ rd(lds, a2) ^ rd(lds, a3 + 128)
+
+
+def lane_shift(lds, s, j):
+    lanebase = LDS_LANE | (j * 4)
+    r = 0
+    for t in range(8):
+        sh = (s >> (4 * t - 7)) if 4 * t >= 7 else ((s << (7 - 4 * t)) & 0xFFFFFFFF)
+        r ^= rd(lds, ((sh & 0x780) | lanebase) + t * 2048)
+    return r
+
+
+def jump(lds, s):
+    r = 0
+    for t in range(8):
+        sh = (s >> (4 * t - 2)) if 4 * t >= 2 else ((s << 2) & 0xFFFFFFFF)
+        r ^= rd(lds, ((sh & 0x3C) | LDS_JUMP) + t * 64)
+    return r
+
+
+def alignbyte(hi, lo, r):
+    return ((((hi << 32) | lo) >> (8 * (r & 3))) & 0xFFFFFFFF)
+
+
+def model_frame(lds, mem: bytes, S: int, L: int):
+    """FCS of mem[S:S+L] computed the kernel's way. mem is the whole readable arena."""
+    E = S + L
+    m = (L + SEG - 1) // SEG if L else 1
+    state = [0] * GROUP
+    lo4, hi4 = 0, (len(mem) + 3) & ~3
+    padded = mem + b"\0" * 8
+    for k in range(m):
+        for j in range(GROUP):
+            cend = E - SEG * (m - 1 - k) - CHUNK * j
+            cstart = cend - CHUNK
+            z = (S - cstart) if k == 0 else -1
+            zr = max(-1, min(CHUNK, z))
+            r = cstart & 3
+            d = [0] * 13
+            if zr < CHUNK:
+                a = cstart & ~3
+                for q in range(13 if r else 12):
+                    ad = a + 4 * q
+                    if ad >= lo4 and ad + 4 <= hi4:
+                        d[q] = int.from_bytes(padded[ad:ad + 4], "little")
+            w = [alignbyte(d[i + 1], d[i], r) for i in range(12)]
+            if k == 0:
+                for i in range(12):
+                    t = max(0, min(4, zr - 4 * i))
+                    w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
+                iv = rd(lds, LDS_INV + 4 * max(0, min(47, zr)))
+                x0 = iv if 0 <= zr < CHUNK else 0
+            else:
+                x0 = jump(lds, state[j])
+            st = x0
+            for i in range(12):
+                st = step4(lds, st ^ w[i], j)
+            state[j] = st
+    v = 0
+    for j in range(GROUP):
+        v ^= lane_shift(lds, state[j], j)
+    return (~v & 0xFFFFFFFF) if L else 0

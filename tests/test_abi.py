@@ -1,0 +1,75 @@
+"""The C-ABI boundary: the product library loads, exports exactly what include/nstack_fcs.h
+declares, and (without a GPU) refuses to compute instead of falling back to the CPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+import nstack_amd as na
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "nstack_fcs.h")
+
+
+def _declared():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src)) - {"defined"})
+
+
+def test_header_declares_python_exports():
+    assert sorted(na.EXPORTS) == _declared()
+
+
+def test_library_exports_every_declared_symbol():
+    lib = na.load()
+    out = subprocess.run(["nm", "-D", "--defined-only", na.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (\w+)", out))
+    for sym in _declared():
+        assert sym in exported, sym
+        assert getattr(lib, sym) is not None
+
+
+def test_dropin_symbol_signature_matches_reference_prototype():
+    # src/nstack_ether.h:80: uint32_t ether_fcs(const void *data, size_t bsize);
+    src = open(HEADER).read()
+    assert re.search(r"uint32_t\s+ether_fcs\s*\(\s*const void \*data,\s*size_t bsize\s*\)\s*;", src)
+
+
+def test_no_cpu_crc_in_product():
+    """The product .so must not contain a CPU CRC table (no silent fallback path)."""
+    data = open(na.LIB_PATH, "rb").read()
+    # T0[1] of the reflected table, little-endian; it appears only if a CPU table were embedded.
+    assert (0x77073096).to_bytes(4, "little") not in data
+
+
+def test_code_object_is_gfx950():
+    out = subprocess.run(["/opt/rocm/lib/llvm/bin/llvm-objdump", "--offloading", na.LIB_PATH],
+                         capture_output=True, text=True, cwd="/tmp")
+    if out.returncode != 0:
+        out = subprocess.run(["strings", na.LIB_PATH], capture_output=True, text=True)
+    assert "gfx950" in out.stdout
+
+
+def _gpu_visible():
+    return os.path.exists("/dev/kfd")
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")
+def test_fails_loudly_without_gpu():
+    lib = na.load()
+    rc = lib.ether_fcs_fixed_dev(ctypes.c_void_p(64), 1518, 1518, 1, ctypes.c_void_p(64), None)
+    assert rc == -19  # -ENODEV
+    with pytest.raises(na.FcsError):
+        na.engine_init(0)
+    assert lib.ether_fcs_fixed_dev(None, 1518, 1518, 1, None, None) == -22  # -EINVAL first
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")
+def test_dropin_aborts_without_gpu():
+    code = "import nstack_amd as na; na.ether_fcs(b'123456789')"
+    p = subprocess.run(["python", "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert p.returncode != 0
+    assert "no usable GPU engine" in p.stderr

@@ -1,0 +1,309 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bit-exact is the only bar (integer CRC). Sizes here finish in seconds on the oracle; the
+BASELINE-size run (64 M x 1518 B) is checked through size-independent properties: sampled frames
+against the oracle, shard consistency (two half launches == one launch), determinism, and the
+CRC residue of every frame written in TX mode.
+"""
+import ctypes
+import os
+import random
+import struct
+import threading
+import zlib
+
+import numpy as np
+import pytest
+
+import nstack_amd as na
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    na.load()
+    return torch.device("cuda:0")
+
+
+def to_dev(arr: np.ndarray, dev):
+    return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
+
+
+def oracle_fixed(oracle, host: np.ndarray, stride, L, n, fast=1):
+    out = np.empty(n, dtype=np.uint32)
+    oracle.oracle_fcs_fixed(host.ctypes.data, stride, L, n, out.ctypes.data, fast, 16)
+    return out
+
+
+def oracle_var(oracle, arena: np.ndarray, off, ln, fast=1):
+    out = np.empty(len(off), dtype=np.uint32)
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    ln = np.ascontiguousarray(ln, dtype=np.uint32)
+    oracle.oracle_fcs_batch(arena.ctypes.data, off.ctypes.data, ln.ctypes.data, out.ctypes.data, len(off), fast)
+    return out
+
+
+def run_var(dev, arena_np: np.ndarray, off, ln):
+    arena = to_dev(arena_np, dev)
+    o = to_dev(np.asarray(off, dtype=np.uint64).view(np.int64), dev)
+    l_ = to_dev(np.asarray(ln, dtype=np.uint32).view(np.int32), dev)
+    out = torch.empty(len(off), dtype=torch.int32, device=dev)
+    na.batch_dev(arena, arena_np.nbytes, o, l_, out, len(off))
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+def run_fixed(dev, base_t, stride, L, n):
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    na.fixed_dev(base_t, stride, L, n, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+# ---------------------------------------------------------------- fixtures (golden, KAT)
+def test_golden_vectors_var(dev, golden):
+    arena = np.frombuffer(golden["arena"], dtype=np.uint8).copy()
+    fr = golden["vectors"]["frames"]
+    got = run_var(dev, arena, [f["off"] for f in fr], [f["len"] for f in fr])
+    exp = np.array([f["crc"] for f in fr], dtype=np.uint32)
+    assert np.array_equal(got, exp)
+
+
+def test_golden_vectors_fixed_one_by_one(dev, golden):
+    arena = np.frombuffer(golden["arena"], dtype=np.uint8).copy()
+    a = to_dev(arena, dev)
+    for f in golden["vectors"]["frames"][::7]:
+        got = run_fixed(dev, a.data_ptr() + f["off"], max(f["len"], 1), f["len"], 1)
+        assert int(got[0]) == f["crc"], f
+
+
+def test_known_answers(dev, golden):
+    for case in golden["kat"]["cases"]:
+        b = bytes.fromhex(case["hex"]) if case["hex"] is not None else bytes([case["fill"]]) * case["len"]
+        arr = np.frombuffer(b + b"\0" * 8, dtype=np.uint8).copy()
+        got = run_var(dev, arr, [0], [len(b)])
+        assert int(got[0]) == case["crc"], case["name"]
+
+
+def test_dropin_ether_fcs(dev, golden):
+    assert na.ether_fcs(b"123456789") == 0xCBF43926
+    assert na.ether_fcs(b"") == 0
+    arena = golden["arena"]
+    for f in golden["vectors"]["frames"][::11]:
+        assert na.ether_fcs(arena[f["off"]:f["off"] + f["len"]]) == f["crc"]
+
+
+# ---------------------------------------------------------------- edge lengths / alignment
+EDGE = [0, 1, 3, 4, 59, 60, 61, 63, 64, 65, 69, 70, 71, 575, 576, 577, 1487, 1488, 1489,
+        1513, 1514, 1515, 1516, 1517, 1518, 1535, 1536, 1537, 3071, 3072, 3073, 8999, 9000]
+
+
+@pytest.mark.parametrize("L", EDGE)
+def test_fixed_edge_lengths_all_alignments(dev, oracle, L):
+    n = 4099
+    for stride in sorted({max(L, 1), L + 1, L + 2, L + 3, ((L + 63) // 64) * 64 or 64}):
+        host = np.random.default_rng(L * 7 + stride).integers(0, 256, n * stride + 8, dtype=np.uint8)
+        d = to_dev(host, dev)
+        for lead in (0, 1, 2, 3):
+            nn = n - 1
+            got = run_fixed(dev, d.data_ptr() + lead, stride, L, nn)
+            exp = oracle_fixed(oracle, host[lead:], stride, L, nn)
+            assert np.array_equal(got, exp), (L, stride, lead, int(np.argmax(got != exp)))
+
+
+def test_frames_touching_allocation_edges(dev, oracle):
+    """Frame 0 at the very start and the last frame ending at the very end of the buffer."""
+    for L in (1, 5, 70, 1517, 1518, 9000):
+        n = 33
+        host = np.random.default_rng(L).integers(0, 256, n * L, dtype=np.uint8)
+        d = to_dev(host, dev)
+        got = run_fixed(dev, d, L, L, n)
+        assert np.array_equal(got, oracle_fixed(oracle, host, L, L, n))
+        got = run_var(dev, host, [i * L for i in range(n)], [L] * n)
+        assert np.array_equal(got, oracle_fixed(oracle, host, L, L, n))
+
+
+# ---------------------------------------------------------------- variable length
+def test_random_lengths_random_offsets(dev, oracle):
+    rng = np.random.default_rng(5)
+    n = 20000
+    ln = rng.integers(0, 9019, n).astype(np.uint32)
+    ln[rng.random(n) < 0.05] = 0
+    size = int(ln.sum()) + 4 * n + 64
+    arena = rng.integers(0, 256, size, dtype=np.uint8)
+    off = rng.integers(0, size - 9019, n).astype(np.uint64)  # overlapping, unordered
+    got = run_var(dev, arena, off, ln)
+    assert np.array_equal(got, oracle_var(oracle, arena, off, ln))
+
+
+def imix(n, seed):
+    counts = [n * 7 // 12, n * 4 // 12]
+    counts.append(n - sum(counts))
+    ln = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), counts)
+    np.random.default_rng(seed).shuffle(ln)
+    return ln
+
+
+def test_imix_packed(dev, oracle):
+    ln = imix(120000, 3)
+    off = np.zeros(len(ln), dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    size = int(off[-1] + ln[-1])
+    arena = np.random.default_rng(4).integers(0, 256, size, dtype=np.uint8)
+    got = run_var(dev, arena, off, ln)
+    assert np.array_equal(got, oracle_var(oracle, arena, off, ln))
+
+
+def test_jumbo(dev, oracle):
+    n, L = 4096, 9000
+    host = np.random.default_rng(6).integers(0, 256, n * L, dtype=np.uint8)
+    d = to_dev(host, dev)
+    assert np.array_equal(run_fixed(dev, d, L, L, n), oracle_fixed(oracle, host, L, L, n))
+
+
+def test_long_frames(dev, oracle):
+    for L in (65536, 100003, 1 << 20):
+        n = 7
+        host = np.random.default_rng(L).integers(0, 256, n * L + 3, dtype=np.uint8)
+        d = to_dev(host, dev)
+        got = run_fixed(dev, d.data_ptr() + 3, L, L, n)
+        assert np.array_equal(got, oracle_fixed(oracle, host[3:], L, L, n))
+
+
+# ---------------------------------------------------------------- SURVEY §8c dataset
+def test_survey_xorshift_digest(dev, oracle, golden):
+    dg = golden["vectors"]["xorshift_1m_1518"]
+    n, L = dg["frames"], dg["len"]
+    host = np.empty(n * L, dtype=np.uint8)
+    st = ctypes.c_uint64(dg["seed"])
+    oracle.oracle_xorshift64_fill(host.ctypes.data, host.size, ctypes.byref(st))
+    got = run_fixed(dev, to_dev(host, dev), L, L, n)
+    assert int(np.bitwise_xor.reduce(got)) == dg["xor"] == 0x600A585E
+    assert int(got.astype(np.uint64).sum()) == dg["sum64"]
+    assert int(got[0]) == dg["first"] and int(got[-1]) == dg["last"]
+
+
+# ---------------------------------------------------------------- device generator
+def test_device_generator_matches_oracle(dev, oracle):
+    for off, nb in ((0, 4096), (5, 1000), (13, 77), (1 << 33, 513)):
+        t = torch.zeros(nb + 16, dtype=torch.uint8, device=dev)
+        na.fill_splitmix_dev(t.data_ptr() + 3, nb, 99, off)
+        torch.cuda.synchronize()
+        h = np.empty(nb, dtype=np.uint8)
+        oracle.oracle_splitmix_fill(h.ctypes.data, nb, 99, off)
+        got = t.cpu().numpy()
+        assert np.array_equal(got[3:3 + nb], h)
+        assert not got[:3].any() and not got[3 + nb:].any()
+
+
+# ---------------------------------------------------------------- BASELINE size (properties)
+def test_baseline_size_properties(dev, oracle):
+    """64 M x 1518 B (94.9 GiB) in one launch: sampled frames == oracle, two half launches ==
+    one launch (shard consistency), and a second launch is bit-identical (determinism)."""
+    free, _ = torch.cuda.mem_get_info()
+    n, L = 64 << 20, 1518
+    if free < n * L + (4 << 30):
+        pytest.skip("not enough HBM")
+    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, n * L, 2026, 0)
+    a = run_fixed(dev, arena, L, L, n)
+    h = n // 2
+    b0 = run_fixed(dev, arena, L, L, h)
+    b1 = run_fixed(dev, arena.data_ptr() + h * L, L, L, n - h)
+    assert np.array_equal(a, np.concatenate([b0, b1]))
+    assert np.array_equal(a, run_fixed(dev, arena, L, L, n))
+    rng = np.random.default_rng(1)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 3000), [0, 1, n - 2, n - 1]]))
+    buf = np.empty(L, dtype=np.uint8)
+    for i in idx:
+        oracle.oracle_splitmix_fill(buf.ctypes.data, L, 2026, int(i) * L)
+        assert int(a[i]) == oracle.oracle_crc32_fast(buf.ctypes.data, L), int(i)
+    del arena
+    torch.cuda.empty_cache()
+
+
+# ---------------------------------------------------------------- host-side entry points
+def test_fixed_host_and_batch_host(dev, oracle):
+    n, L = 300000, 1518
+    host = np.random.default_rng(8).integers(0, 256, n * L, dtype=np.uint8)
+    out = np.zeros(n, dtype=np.uint32)
+    na.fixed_host(host, L, L, n, out)
+    assert np.array_equal(out, oracle_fixed(oracle, host, L, L, n))
+    ln = imix(200000, 9)
+    off = np.zeros(len(ln), dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    arena = np.random.default_rng(10).integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    out2 = np.zeros(len(ln), dtype=np.uint32)
+    na.batch_host(arena, arena.nbytes, off, ln, out2, len(ln))
+    assert np.array_equal(out2, oracle_var(oracle, arena, off, ln))
+
+
+def test_tx_mode_matches_ether_send_layout(dev, oracle):
+    """ether_send (src/linux/ether.c:222-263): frame = hdr + payload + zero pad, FCS over
+    frame_size-4 bytes stored little-endian at the end. Batched TX must produce byte-identical
+    frames; every frame then satisfies the CRC residue 0x2144DF1C."""
+    rng = random.Random(12)
+    stride = 1518
+    payloads = [rng.randrange(0, 1501) for _ in range(5000)]
+    frames = np.zeros((len(payloads), stride), dtype=np.uint8)
+    covered = np.zeros(len(payloads), dtype=np.uint32)
+    expected = []
+    for i, bsize in enumerate(payloads):
+        frame_size = 14 + max(bsize, 60 - 4) + 4          # :222-224
+        hdr = bytes(rng.randrange(256) for _ in range(12)) + struct.pack(">H", 0x0800)
+        body = bytes(rng.randrange(256) for _ in range(bsize))
+        f = hdr + body + b"\0" * (frame_size - 14 - bsize)  # :261 zero pad before the FCS
+        c = zlib.crc32(f[:frame_size - 4])
+        assert c == oracle.oracle_ether_fcs(f, frame_size - 4)
+        expected.append(f[:frame_size - 4] + struct.pack("<I", c))  # :262-263
+        frames[i, :frame_size - 4] = np.frombuffer(f[:frame_size - 4], dtype=np.uint8)
+        covered[i] = frame_size - 4
+    na.tx_host(frames, stride, covered, len(payloads))
+    for i in range(len(payloads)):
+        fs = int(covered[i]) + 4
+        assert frames[i, :fs].tobytes() == expected[i]
+        assert oracle.oracle_ether_fcs(frames[i].ctypes.data, fs) == 0x2144DF1C
+
+
+def test_concurrent_callers(dev, oracle):
+    """ether_fcs is called from 3-4 threads in the reference."""
+    errs = []
+    rng = np.random.default_rng(13)
+    data = rng.integers(0, 256, 64 * 1024, dtype=np.uint8)
+
+    def worker(t):
+        try:
+            r = random.Random(t)
+            for _ in range(200):
+                a = r.randrange(0, 60000)
+                L = r.randrange(0, 1519)
+                b = data[a:a + L].tobytes()
+                if na.ether_fcs(b) != zlib.crc32(b):
+                    errs.append((t, a, L))
+            out = np.zeros(1000, dtype=np.uint32)
+            na.fixed_host(data, 60, 60, 1000, out)
+            if not np.array_equal(out, oracle_fixed(oracle, data, 60, 60, 1000)):
+                errs.append((t, "batch"))
+        except Exception as e:  # pragma: no cover
+            errs.append(repr(e))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(4)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs[:5]
+
+
+def test_bad_arguments_are_rejected(dev):
+    lib = na.load()
+    assert lib.ether_fcs_fixed_dev(None, 1, 1, 1, None, None) == -22
+    t = torch.zeros(64, dtype=torch.uint8, device=dev)
+    assert lib.ether_fcs_fixed_dev(ctypes.c_void_p(t.data_ptr()), 10, 20, 2, ctypes.c_void_p(t.data_ptr()), None) == -22
+    assert lib.ether_fcs_fixed_dev(ctypes.c_void_p(t.data_ptr()), 10, 20, 0, ctypes.c_void_p(t.data_ptr()), None) == 0
