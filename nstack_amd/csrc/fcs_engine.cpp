@@ -135,10 +135,13 @@ inline uint64_t ceil4(uint64_t x) { return (x + 3) & ~3ull; }
 
 uint32_t segments(uint32_t len) { return len ? (len + fcs::kSegBytes - 1) / fcs::kSegBytes : 1u; }
 
-// Leading zero bytes of the front lane of segment 0 for a frame of length len.
-uint32_t front_zeros(uint32_t len) {
-    if (!len) return 0;
+// Bound for the kernel's front-masking loop (words 0 .. ceil(zmax/4)-1 get masked): the leading
+// zero bytes of the front lane of segment 0, or the whole chunk (48) when segment 0 leaves lanes
+// with no frame bytes at all (those lanes' loads are not zero-filled and must be masked entirely).
+uint32_t mask_bound(uint32_t len) {
+    if (!len) return fcs::kChunkBytes;
     const uint32_t l0 = len - fcs::kSegBytes * (segments(len) - 1);
+    if (l0 <= fcs::kSegBytes - fcs::kChunkBytes) return fcs::kChunkBytes;
     return fcs::kChunkBytes * ((l0 + fcs::kChunkBytes - 1) / fcs::kChunkBytes) - l0;
 }
 
@@ -158,7 +161,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.hi4 = ceil4((uint64_t)base + (n - 1) * stride + len);
     p.flen = len;
     p.fseg = segments(len);
-    p.zmax = front_zeros(len);
+    p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
     HIPTRY(fcs::launch_fcs(false, p, grid_for(ds, n), st), "launching fcs_kernel<fixed>");
     return 0;

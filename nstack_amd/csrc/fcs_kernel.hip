@@ -115,38 +115,139 @@ __device__ __forceinline__ Item frame_item(const KParams &p, uint64_t f) {
     return it;
 }
 
-// Load lane j's chunk of segment k: 13 dwords from floor4(chunk start). zr = bytes between the
-// chunk start and the frame start (segment 0 only; < 0: chunk fully inside the frame).
-__device__ __forceinline__ void load_chunk(const KParams &p, const Item &it, uint32_t k, int j,
-                                           bool act, uint32_t (&d)[13], int &zr, uint32_t &r) {
+// Raw loads of one lane chunk (issued early, consumed one item later) and what is needed to
+// interpret them. Loads are unconditional and always inside [lo4, hi4): lanes with nothing to load
+// read lo4, and a window that starts before lo4 (front lane of a frame at the very start of the
+// arena) is clamped per 16-byte group and repaired after the data has landed (fixup_edge).
+struct Chunk {
+    u32x4a4 x0, x1, x2;
+    uint32_t x3;
+    int zr;          // bytes from chunk start to frame start (segment 0), -1 inside, 48 = no data
+    uint32_t r;      // chunk start & 3 (realignment)
+    int delta0;      // dwords group 0 was shifted by the low clamp (0 = not clamped)
+    int delta1, delta2;
+};
+
+__device__ __forceinline__ uint64_t clamp64(uint64_t x, uint64_t lo, uint64_t hi) {
+    return x < lo ? lo : (x > hi ? hi : x);
+}
+
+template <bool TINY>
+__device__ __forceinline__ void issue_chunk(const KParams &p, const Item &it, uint32_t k, int j,
+                                            bool act, Chunk &c) {
     const int64_t cend = (int64_t)it.end - (int64_t)kSegBytes * (int64_t)(it.m - 1 - k) -
                          (int64_t)kChunkBytes * j;
     const int64_t cstart = cend - kChunkBytes;
     const int64_t z = (k == 0) ? ((int64_t)(it.end - it.len) - cstart) : -1;
-    zr = z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
-    r = (uint32_t)cstart & 3u;
-#pragma unroll
-    for (int q = 0; q < 13; q++) d[q] = 0;
-    if (!act || zr >= kChunkBytes) return;
-    const uint64_t a = (uint64_t)cstart & ~3ull;
-    const uint64_t lim = a + (r ? 52 : 48);
-    if (a >= p.lo4 && lim <= p.hi4) {
-        const u32x4a4 x0 = gload<u32x4a4>(a), x1 = gload<u32x4a4>(a + 16), x2 = gload<u32x4a4>(a + 32);
-        d[0] = x0.x; d[1] = x0.y; d[2] = x0.z; d[3] = x0.w;
-        d[4] = x1.x; d[5] = x1.y; d[6] = x1.z; d[7] = x1.w;
-        d[8] = x2.x; d[9] = x2.y; d[10] = x2.z; d[11] = x2.w;
-        if (r) d[12] = gload<uint32_t>(a + 48);
-    } else {
-        // Arena edge (first/last frames only): per-dword guarded loads, never outside [lo4, hi4).
+    c.zr = z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
+    c.r = (uint32_t)cstart & 3u;
+    const bool need = act && c.zr < kChunkBytes;
+    const uint64_t a = need ? ((uint64_t)cstart & ~3ull) : p.lo4;
+    if (TINY) {
+        // Arena shorter than 64 B (host-selected variant): per-dword guarded loads.
+        uint32_t d[13];
 #pragma unroll
         for (int q = 0; q < 13; q++) {
             const uint64_t ad = a + 4 * q;
-            if (ad >= p.lo4 && ad + 4 <= p.hi4) d[q] = gload<uint32_t>(ad);
+            d[q] = (need && ad >= p.lo4 && ad + 4 <= p.hi4) ? gload<uint32_t>(ad) : 0u;
         }
+        c.x0 = u32x4a4{d[0], d[1], d[2], d[3]};
+        c.x1 = u32x4a4{d[4], d[5], d[6], d[7]};
+        c.x2 = u32x4a4{d[8], d[9], d[10], d[11]};
+        c.x3 = d[12];
+        c.delta0 = c.delta1 = c.delta2 = 0;
+        return;
     }
+    const uint64_t lo = p.lo4, hi16 = p.hi4 - 16, hi4 = p.hi4 - 4;
+    const uint64_t g0 = clamp64(a, lo, hi16), g1 = clamp64(a + 16, lo, hi16), g2 = clamp64(a + 32, lo, hi16);
+    c.delta0 = (int)((g0 - a) >> 2);
+    c.delta1 = (int)((g1 - (a + 16)) >> 2);
+    c.delta2 = (int)((g2 - (a + 32)) >> 2);
+    c.x0 = gload<u32x4a4>(g0);
+    c.x1 = gload<u32x4a4>(g1);
+    c.x2 = gload<u32x4a4>(g2);
+    c.x3 = gload<uint32_t>(clamp64(a + 48, lo, hi4));
 }
 
-template <bool VAR>
+// Undo the low clamp of one 16-byte group: true dword q = loaded dword q - delta (q >= delta);
+// dwords q < delta lie before the arena start, hence before the frame start, and get masked.
+__device__ __forceinline__ void unshift_group(uint32_t *g, int delta) {
+    const uint32_t a = g[0], b = g[1], c = g[2], d = g[3];
+    g[1] = delta == 1 ? a : (delta >= 2 ? a : b);
+    g[2] = delta == 1 ? b : (delta == 2 ? a : (delta >= 3 ? a : c));
+    g[3] = delta == 1 ? c : (delta == 2 ? b : (delta == 3 ? a : (delta >= 4 ? a : d)));
+}
+
+template <bool VAR, bool TINY>
+struct Lane {
+    const KParams &p;
+    const uint8_t *lds;
+    int j;
+    uint32_t base0, base1, lanebase;
+    uint64_t H;
+
+    struct Pos {
+        uint64_t f;
+        uint32_t k;
+        bool act;
+        Item it;
+    };
+
+    __device__ __forceinline__ Pos next(const Pos &c) const {
+        Pos n = c;
+        n.k = c.k + 1;
+        if (n.k >= c.it.m) {
+            n.f = c.f + H;
+            n.k = 0;
+        }
+        n.act = c.act && n.f < p.n;
+        if (n.act && n.k == 0) n.it = frame_item<VAR>(p, n.f);
+        return n;
+    }
+
+    // Consume one chunk: realign, mask, run the slice-by-4 chain, finish the frame if last.
+    __device__ __forceinline__ void process(const Pos &c, const Chunk &ch, uint32_t &s) const {
+        uint32_t d[13] = {ch.x0.x, ch.x0.y, ch.x0.z, ch.x0.w, ch.x1.x, ch.x1.y, ch.x1.z,
+                          ch.x1.w, ch.x2.x, ch.x2.y, ch.x2.z, ch.x2.w, ch.x3};
+        if (__any(ch.delta0 | ch.delta1 | ch.delta2)) {   // arena start only; wave-uniform branch
+            unshift_group(d + 0, ch.delta0);
+            unshift_group(d + 4, ch.delta1);
+            unshift_group(d + 8, ch.delta2);
+        }
+        uint32_t w[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ch.r);
+        uint32_t x0;
+        if (c.k == 0) {
+#pragma unroll
+            for (int i = 0; i < 12; i++) {
+                if (4 * i < (int)p.zmax) {   // uniform bound: skip words no front lane can mask
+                    int t = ch.zr - 4 * i;
+                    t = t < 0 ? 0 : (t > 4 ? 4 : t);
+                    w[i] &= (uint32_t)(0xFFFFFFFFull << (8 * t));
+                }
+            }
+            const int zi = ch.zr < 0 ? 0 : (ch.zr > 47 ? 47 : ch.zr);
+            const uint32_t iv = lds_rd(lds, kLdsInv + 4u * (uint32_t)zi);
+            x0 = (ch.zr >= 0 && ch.zr < kChunkBytes) ? iv : 0u;
+        } else {
+            x0 = jump(lds, s);
+        }
+        uint32_t st = x0;
+#pragma unroll
+        for (int i = 0; i < 12; i++) st = step4(lds, st ^ w[i], base0, base1);
+        s = st;
+
+        const bool last = c.act && (c.k + 1 == c.it.m);
+        if (__any(last)) {
+            uint32_t v = last ? lane_shift(lds, s, lanebase) : 0u;
+            v = half_xor(v);
+            if (last && j == 31) p.out[c.f] = c.it.len ? ~v : 0u;
+        }
+    }
+};
+
+template <bool VAR, bool TINY>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
 
@@ -172,77 +273,27 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
 
     const int lane = threadIdx.x & 63;
     const int j = lane & 31;
-    const uint32_t base0 = (uint32_t)j * 4u;
-    const uint32_t base1 = 0x10000u | ((uint32_t)j * 4u);
-    const uint32_t lanebase = kLdsLane | ((uint32_t)j * 4u);
+    Lane<VAR, TINY> L{p, lds, j, (uint32_t)j * 4u, 0x10000u | ((uint32_t)j * 4u), kLdsLane | ((uint32_t)j * 4u),
+                (uint64_t)gridDim.x * kHalvesPerWg};
 
-    const uint64_t H = (uint64_t)gridDim.x * kHalvesPerWg;
-    uint64_t f = ((uint64_t)blockIdx.x * kHalvesPerWg) + (threadIdx.x >> 5);
-    uint32_t k = 0;
-    bool act = f < p.n;
-    Item cur = act ? frame_item<VAR>(p, f) : Item{0, 0, 1};
-    uint32_t d[13];
-    int zr;
-    uint32_t r;
-    load_chunk(p, cur, 0, j, act, d, zr, r);
+    typename Lane<VAR, TINY>::Pos A, B;
+    A.f = ((uint64_t)blockIdx.x * kHalvesPerWg) + (threadIdx.x >> 5);
+    A.k = 0;
+    A.act = A.f < p.n;
+    A.it = A.act ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
+    Chunk CA, CB;
+    issue_chunk<TINY>(p, A.it, A.k, j, A.act, CA);
     uint32_t s = 0;
 
-    while (__any(act)) {
-        // ---- prefetch the next item (next segment, or next frame's first segment) ----
-        uint64_t f2 = f;
-        uint32_t k2 = k + 1;
-        Item nx = cur;
-        if (k2 >= cur.m) {
-            f2 = f + H;
-            k2 = 0;
-        }
-        const bool act2 = act && f2 < p.n;
-        if (act2 && k2 == 0) nx = frame_item<VAR>(p, f2);
-        uint32_t d2[13];
-        int zr2;
-        uint32_t r2;
-        load_chunk(p, nx, k2, j, act2, d2, zr2, r2);
-
-        // ---- process the current item ----
-        uint32_t w[12];
-#pragma unroll
-        for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
-        uint32_t x0;
-        if (k == 0) {
-#pragma unroll
-            for (int i = 0; i < 12; i++) {
-                if (4 * i < (int)p.zmax) {   // uniform bound: skip words no front lane can mask
-                    int t = zr - 4 * i;
-                    t = t < 0 ? 0 : (t > 4 ? 4 : t);
-                    w[i] &= (uint32_t)(0xFFFFFFFFull << (8 * t));
-                }
-            }
-            const uint32_t iv = lds_rd(lds, kLdsInv + 4u * (uint32_t)(zr < 0 ? 0 : (zr > 47 ? 47 : zr)));
-            x0 = (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
-        } else {
-            x0 = jump(lds, s);
-        }
-        uint32_t st = x0;
-#pragma unroll
-        for (int i = 0; i < 12; i++) st = step4(lds, st ^ w[i], base0, base1);
-        s = st;
-
-        const bool last = act && (k + 1 == cur.m);
-        if (__any(last)) {
-            uint32_t v = last ? lane_shift(lds, s, lanebase) : 0u;
-            v = half_xor(v);
-            if (last && j == 31) p.out[f] = cur.len ? ~v : 0u;
-        }
-
-        // ---- advance ----
-        f = f2;
-        k = k2;
-        cur = nx;
-        act = act2;
-        zr = zr2;
-        r = r2;
-#pragma unroll
-        for (int q = 0; q < 13; q++) d[q] = d2[q];
+    // Two items in flight per lane: process one while the other's loads are outstanding.
+    while (__any(A.act)) {
+        B = L.next(A);
+        issue_chunk<TINY>(p, B.it, B.k, j, B.act, CB);
+        L.process(A, CA, s);
+        if (!__any(B.act)) break;
+        A = L.next(B);
+        issue_chunk<TINY>(p, A.it, A.k, j, A.act, CA);
+        L.process(B, CB, s);
     }
 }
 
@@ -318,10 +369,15 @@ __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t s
 
 // ---- host-side launchers (the engine TU never names the kernels) ----
 hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st) {
-    if (var)
-        hipLaunchKernelGGL(fcs_kernel<true>, dim3(grid), dim3(kWgThreads), 0, st, p);
+    const bool tiny = p.hi4 - p.lo4 < 64;
+    if (var && tiny)
+        hipLaunchKernelGGL((fcs_kernel<true, true>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    else if (var)
+        hipLaunchKernelGGL((fcs_kernel<true, false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    else if (tiny)
+        hipLaunchKernelGGL((fcs_kernel<false, true>), dim3(grid), dim3(kWgThreads), 0, st, p);
     else
-        hipLaunchKernelGGL(fcs_kernel<false>, dim3(grid), dim3(kWgThreads), 0, st, p);
+        hipLaunchKernelGGL((fcs_kernel<false, false>), dim3(grid), dim3(kWgThreads), 0, st, p);
     return hipGetLastError();
 }
 

@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""Profiling driver: R launches of the fixed-length FCS kernel over F x L frames (HBM-resident).
+Used under rocprofv3 (kernel trace / PMC passes); prints per-launch time from HIP events."""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frames", type=int, default=64 << 20)
+    ap.add_argument("--len", type=int, default=1518)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--var", action="store_true", help="use the variable-length entry point")
+    a = ap.parse_args()
+    import torch
+    import nstack_amd as na
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    n, L = a.frames, a.len
+    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, n * L, 7, 0)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    if a.var:
+        off = torch.arange(n, dtype=torch.int64, device=dev) * L
+        ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    st = torch.cuda.current_stream()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for r in range(a.reps + 1):
+        if r == 1:
+            e0.record(st)
+        if a.var:
+            na.batch_dev(arena, n * L, off, ln, out, n, st)
+        else:
+            na.fixed_dev(arena, L, L, n, out, st)
+    e1.record(st)
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / a.reps
+    print(f"frames={n} len={L} var={a.var} ms/launch={ms:.4f} GB/s={n * L / ms / 1e6:.1f}")
+
+
+if __name__ == "__main__":
+    main()
