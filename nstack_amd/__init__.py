@@ -13,7 +13,7 @@ import errno
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnstack_fcs.so")
+LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fcs.so")
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",

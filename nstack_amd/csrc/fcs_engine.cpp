@@ -146,7 +146,8 @@ uint32_t mask_bound(uint32_t len) {
 }
 
 int grid_for(const DevState *ds, uint64_t n) {
-    const uint64_t want = (n + 31) / 32;   // 32 half-wave frame slots per workgroup
+    const uint64_t slots = fcs::kWgThreads / fcs::kGroup;   // frame slots per workgroup
+    const uint64_t want = (n + slots - 1) / slots;
     return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ds->cus, want));
 }
 
@@ -446,8 +447,8 @@ extern "C" {
 const char *fcs_last_error(void) { return g_last_error.c_str(); }
 
 const char *fcs_engine_version(void) {
-    return "nstack-fcs 0.1 gfx950: half-wave/frame, 48B chunks, slice-by-4 LDS x32 replicas, "
-           "v_perm addressing, DPP reduce";
+    return "nstack-fcs 0.2 gfx950: quarter-wave/frame, 96B lane chunks as 2 chains, slice-by-4 "
+           "LDS x32 replicas, v_perm addressing, DPP reduce";
 }
 
 int fcs_engine_init(int ndev) {

@@ -4,42 +4,35 @@
 // one launch over many independent frames. Result per frame is bit-identical to ether_fcs().
 //
 // Work decomposition:
-//   * one HALF-WAVE (32 lanes) per frame; lane j owns the 48-byte chunk that ends 48*j bytes
-//     before the frame end, so a 32-lane group covers one 1536-byte "segment"; longer frames
-//     are walked segment by segment, front to back (jumbo 9000 B = 6 segments);
-//   * each lane loads its chunk with 3 x global_load_dwordx4 + 1 dword from a 4-byte aligned
-//     address (measured: this layout streams HBM at the same rate as a fully coalesced read),
-//     re-aligns it to the frame end with v_alignbyte_b32 and zeroes bytes before the frame start;
-//   * the lane runs a slice-by-4 CRC over its 12 words: 4 ds_read_b32 per word from byte tables
-//     replicated 32x in LDS (replica = lane & 31 -> every 32-lane LDS access is bank-conflict
-//     free), addressed by a single v_perm_b32 per lookup;
-//   * the frame's initial all-ones register is injected as the front lane's start value
-//     INV[z] = A_z^{-1}(~0) (z = zero bytes in front of the frame start), so no length-dependent
-//     constant is needed; across segments a lane's register jumps over the other lanes' bytes
-//     with J = A_1488;
-//   * at the frame end lane j shifts its register by 48*j zero bytes (per-lane nibble tables,
-//     bank = lane), the 32 registers are XOR-reduced with DPP, and lane 31 stores ~crc.
-// No MFMA: this is a byte-stream codec bounded by HBM read bandwidth (roofline: DESIGN.md §4).
+//   * one QUARTER-WAVE (16 lanes) per frame; lane j owns the 96-byte chunk that ends 96*j bytes
+//     before the frame end, so 16 lanes cover one 1536-byte "segment"; longer frames are walked
+//     segment by segment, front to back (jumbo 9000 B = 6 segments); a wave works on 4 frames;
+//   * each lane loads its chunk with 6 x global_load_dwordx4 + 1 dword from a 4-byte aligned
+//     address (this layout streams HBM at the rate of a coalesced read: tools/microbench), two
+//     chunks in flight per lane; the words are re-aligned to the frame end with v_alignbyte_b32
+//     and the bytes in front of the frame start are zeroed;
+//   * the lane runs its 24 words as two independent 12-word slice-by-4 chains (ILP 2): per word
+//     4 ds_read_b32 from byte tables replicated 32x in LDS (replica = lane & 31 -> every 32-lane
+//     LDS access is bank-conflict free), each address formed by ONE v_perm_b32; the first chain
+//     is shifted over the second chain's 48 bytes with H = A_48 (nibble tables) and XORed in;
+//   * the frame's all-ones initial register is injected as the front lane's start value
+//     INV[z] = A_z^{-1}(~0) (z = zero bytes in front of the frame start); across segments a
+//     lane's register jumps over the other lanes' bytes with J = A_1440;
+//   * at the frame end lane j shifts its register by 96*j zero bytes (per-lane nibble tables,
+//     bank = lane), the 16 registers are XOR-reduced with 4 DPP steps and lane 15 stores ~crc.
+// No MFMA: a byte-stream codec bounded by HBM read bandwidth (roofline: DESIGN.md §4).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-#include "fcs_tables.hpp"
 #include "fcs_launch.hpp"
+#include "fcs_tables.hpp"
 
 namespace fcs {
 
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kHalvesPerWg = kWgThreads / 32;   // 16 waves; LDS (145 KiB) admits one WG per CU
-
-
-
-struct Item {
-    uint64_t end;   // byte address one past the frame's last byte
-    uint32_t len;
-    uint32_t m;     // segments
-};
+constexpr int kSlotsPerWg = kWgThreads / kGroup;   // 64 frame slots; LDS (145 KiB) -> 1 WG per CU
 
 // Loads through address space 1 (global): flat loads would also count on lgkmcnt and make every
 // LDS wait drain the prefetched chunk loads.
@@ -60,44 +53,56 @@ __device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32
     const uint32_t a1 = __builtin_amdgcn_perm(x, base0, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, base1, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, base1, 0x0C020700u);
+#ifdef FCS_ABL_NOLDS   // measurement-only build: same VALU shape, LDS reads replaced
+    return (a0 * 0x9E3779B1u) ^ (a1 >> 3) ^ (a2 << 5) ^ a3;
+#else
     const uint32_t t3 = lds_rd(lds, a0);
     const uint32_t t2 = lds_rd(lds, a1 + 128);
     const uint32_t t1 = lds_rd(lds, a2);
     const uint32_t t0 = lds_rd(lds, a3 + 128);
-    return t3 ^ t2 ^ t1 ^ t0;
+    return (t3 ^ t2) ^ (t1 ^ t0);
+#endif
 }
 
-// A_{48 j}(s): lane j's own nibble tables (entry e of table t at kLdsLane + t*2048 + e*128 + j*4).
+// A_{96 j}(s): this lane's own nibble tables (entry e of table t at kLdsLane + t*2048 + e*128 +
+// (lane & 31)*4; the slot holds the table of lane & 15).
 __device__ __forceinline__ uint32_t lane_shift(const uint8_t *lds, uint32_t s, uint32_t lanebase) {
-    uint32_t r = 0;
+    uint32_t r[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         const uint32_t sh = (4 * t >= 7) ? (s >> (4 * t - 7)) : (s << (7 - 4 * t));
-        r ^= lds_rd(lds, ((sh & 0x780u) | lanebase) + t * 2048);
+        r[t] = lds_rd(lds, ((sh & 0x780u) | lanebase) + t * 2048);
     }
-    return r;
+    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
 }
 
-// A_1488(s): one shared table set (entry e of table t at kLdsJump + t*64 + e*4).
-__device__ __forceinline__ uint32_t jump(const uint8_t *lds, uint32_t s) {
-    uint32_t r = 0;
+// A_n(s) for one n shared by all lanes (J = A_1440 at kLdsJump, H = A_48 at kLdsHalf):
+// entry e of nibble table t at REGION + t*64 + e*4; 16 entries span 16 banks -> conflict free.
+template <uint32_t REGION>
+__device__ __forceinline__ uint32_t uniform_shift(const uint8_t *lds, uint32_t s) {
+    uint32_t r[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
-        r ^= lds_rd(lds, ((sh & 0x3Cu) | kLdsJump) + t * 64);
+        r[t] = lds_rd(lds, ((sh & 0x3Cu) | REGION) + t * 64);
     }
-    return r;
+    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
 }
 
-// XOR over the 32 lanes of each half wave; the full value lands in lanes 16..31 / 48..63.
-__device__ __forceinline__ uint32_t half_xor(uint32_t v) {
+// XOR over each 16-lane row (one frame); every lane of the row ends with the row's XOR.
+__device__ __forceinline__ uint32_t row_xor(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast15 -> rows 1,3
     return v;
 }
+
+struct Item {
+    uint64_t end;   // byte address one past the frame's last byte
+    uint32_t len;
+    uint32_t m;     // segments
+};
 
 template <bool VAR>
 __device__ __forceinline__ Item frame_item(const KParams &p, uint64_t f) {
@@ -115,76 +120,83 @@ __device__ __forceinline__ Item frame_item(const KParams &p, uint64_t f) {
     return it;
 }
 
-// Raw loads of one lane chunk (issued early, consumed one item later) and what is needed to
-// interpret them. Loads are unconditional and always inside [lo4, hi4): lanes with nothing to load
-// read lo4, and a window that starts before lo4 (front lane of a frame at the very start of the
-// arena) is clamped per 16-byte group and repaired after the data has landed (fixup_edge).
+// Raw loads of one lane chunk (issued one item ahead of their use) and what is needed to
+// interpret them. Loads are unconditional and stay inside [lo4, hi4): lanes with nothing to load
+// read lo4; a window that starts before lo4 (front lane of a frame at the very start of the
+// arena) is moved up to lo4 in a wave-uniform branch and shifted back after the data has landed
+// (process()).
 struct Chunk {
-    u32x4a4 x0, x1, x2;
-    uint32_t x3;
-    int zr;          // bytes from chunk start to frame start (segment 0), -1 inside, 48 = no data
-    uint32_t r;      // chunk start & 3 (realignment)
-    int delta0;      // dwords group 0 was shifted by the low clamp (0 = not clamped)
-    int delta1, delta2;
+    u32x4a4 x[6];
+    uint32_t x6;
+    int zr;        // bytes from chunk start to frame start (segment 0); -1 inside; 96 = no data
+    uint32_t r;    // chunk start & 3 (realignment)
+    int dlead;     // dwords the load window was moved up to stay >= lo4 (0 = not moved)
 };
 
-__device__ __forceinline__ uint64_t clamp64(uint64_t x, uint64_t lo, uint64_t hi) {
-    return x < lo ? lo : (x > hi ? hi : x);
-}
-
-template <bool TINY>
+template <bool VAR, bool TINY, bool SINGLE>
 __device__ __forceinline__ void issue_chunk(const KParams &p, const Item &it, uint32_t k, int j,
                                             bool act, Chunk &c) {
-    const int64_t cend = (int64_t)it.end - (int64_t)kSegBytes * (int64_t)(it.m - 1 - k) -
-                         (int64_t)kChunkBytes * j;
-    const int64_t cstart = cend - kChunkBytes;
-    const int64_t z = (k == 0) ? ((int64_t)(it.end - it.len) - cstart) : -1;
-    c.zr = z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
+    int64_t cstart;
+    if (SINGLE) {   // fixed length, one segment: zr does not depend on the frame
+        cstart = (int64_t)it.end - (int64_t)kChunkBytes * (j + 1);
+        const int z = kChunkBytes * (j + 1) - (int)p.flen;
+        c.zr = z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : z);
+    } else {
+        cstart = (int64_t)it.end - (int64_t)kSegBytes * (int64_t)(it.m - 1 - k) -
+                 (int64_t)kChunkBytes * (j + 1);
+        const int64_t z = (k == 0) ? ((int64_t)(it.end - it.len) - cstart) : -1;
+        c.zr = z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
+    }
     c.r = (uint32_t)cstart & 3u;
     const bool need = act && c.zr < kChunkBytes;
     const uint64_t a = need ? ((uint64_t)cstart & ~3ull) : p.lo4;
+    c.dlead = 0;
     if (TINY) {
-        // Arena shorter than 64 B (host-selected variant): per-dword guarded loads.
-        uint32_t d[13];
+        // Arena shorter than 192 B (host-selected variant): per-dword guarded loads.
+        uint32_t d[kChunkWords + 1];
 #pragma unroll
-        for (int q = 0; q < 13; q++) {
+        for (int q = 0; q <= kChunkWords; q++) {
             const uint64_t ad = a + 4 * q;
             d[q] = (need && ad >= p.lo4 && ad + 4 <= p.hi4) ? gload<uint32_t>(ad) : 0u;
         }
-        c.x0 = u32x4a4{d[0], d[1], d[2], d[3]};
-        c.x1 = u32x4a4{d[4], d[5], d[6], d[7]};
-        c.x2 = u32x4a4{d[8], d[9], d[10], d[11]};
-        c.x3 = d[12];
-        c.delta0 = c.delta1 = c.delta2 = 0;
+#pragma unroll
+        for (int g = 0; g < 6; g++) c.x[g] = u32x4a4{d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
+        c.x6 = d[kChunkWords];
         return;
     }
-    const uint64_t lo = p.lo4, hi16 = p.hi4 - 16, hi4 = p.hi4 - 4;
-    const uint64_t g0 = clamp64(a, lo, hi16), g1 = clamp64(a + 16, lo, hi16), g2 = clamp64(a + 32, lo, hi16);
-    c.delta0 = (int)((g0 - a) >> 2);
-    c.delta1 = (int)((g1 - (a + 16)) >> 2);
-    c.delta2 = (int)((g2 - (a + 32)) >> 2);
-    c.x0 = gload<u32x4a4>(g0);
-    c.x1 = gload<u32x4a4>(g1);
-    c.x2 = gload<u32x4a4>(g2);
-    c.x3 = gload<uint32_t>(clamp64(a + 48, lo, hi4));
+    // High side in bounds by construction: a + 96 <= chunk end <= hi4; the 25th dword (needed
+    // only when r != 0) ends at ceil4(chunk end) <= hi4; when r == 0 dword 23 is re-read instead.
+    // Low side: a window starting before lo4 (front lane of a frame at the arena start) is moved
+    // up to lo4 as a whole; process() shifts the dwords back by dlead (wave-uniform, rare branch).
+    uint64_t ab = a;
+    if (__any(a < p.lo4)) {
+        c.dlead = a < p.lo4 ? (int)((p.lo4 - a) >> 2) : 0;
+        ab = a < p.lo4 ? p.lo4 : a;
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(ab + 16 * q);
+    c.x6 = gload<uint32_t>(ab + ((c.r || c.dlead) ? 96 : 92));
 }
 
-// Undo the low clamp of one 16-byte group: true dword q = loaded dword q - delta (q >= delta);
-// dwords q < delta lie before the arena start, hence before the frame start, and get masked.
-__device__ __forceinline__ void unshift_group(uint32_t *g, int delta) {
-    const uint32_t a = g[0], b = g[1], c = g[2], d = g[3];
-    g[1] = delta == 1 ? a : (delta >= 2 ? a : b);
-    g[2] = delta == 1 ? b : (delta == 2 ? a : (delta >= 3 ? a : c));
-    g[3] = delta == 1 ? c : (delta == 2 ? b : (delta == 3 ? a : (delta >= 4 ? a : d)));
+// Undo the window move of issue_chunk: true dword q = loaded dword q - dlead (q >= dlead); dwords
+// q < dlead lie before the arena start, hence before the frame start, and get masked anyway.
+template <int N>
+__device__ __forceinline__ void shift_up(uint32_t (&d)[N], int dlead) {
+#pragma unroll
+    for (int b = 16; b >= 1; b >>= 1) {
+        const bool take = (dlead & b) != 0;
+#pragma unroll
+        for (int q = N - 1; q >= 0; q--) d[q] = take ? (q >= b ? d[q - b] : 0u) : d[q];
+    }
 }
 
-template <bool VAR, bool TINY>
+template <bool VAR, bool TINY, bool SINGLE>
 struct Lane {
     const KParams &p;
     const uint8_t *lds;
-    int j;
+    int j;            // lane within the frame's 16
     uint32_t base0, base1, lanebase;
-    uint64_t H;
+    uint64_t Q;       // frame slots in the grid
 
     struct Pos {
         uint64_t f;
@@ -195,59 +207,85 @@ struct Lane {
 
     __device__ __forceinline__ Pos next(const Pos &c) const {
         Pos n = c;
-        n.k = c.k + 1;
-        if (n.k >= c.it.m) {
-            n.f = c.f + H;
+        if (SINGLE) {
+            n.f = c.f + Q;
             n.k = 0;
+        } else {
+            n.k = c.k + 1;
+            if (n.k >= c.it.m) {
+                n.f = c.f + Q;
+                n.k = 0;
+            }
         }
         n.act = c.act && n.f < p.n;
-        if (n.act && n.k == 0) n.it = frame_item<VAR>(p, n.f);
+        if (SINGLE || (n.act && n.k == 0)) n.it = frame_item<VAR>(p, n.f);
         return n;
     }
 
-    // Consume one chunk: realign, mask, run the slice-by-4 chain, finish the frame if last.
+    // Consume one chunk: realign, mask, run the two chains, finish the frame if last.
     __device__ __forceinline__ void process(const Pos &c, const Chunk &ch, uint32_t &s) const {
-        uint32_t d[13] = {ch.x0.x, ch.x0.y, ch.x0.z, ch.x0.w, ch.x1.x, ch.x1.y, ch.x1.z,
-                          ch.x1.w, ch.x2.x, ch.x2.y, ch.x2.z, ch.x2.w, ch.x3};
-        if (__any(ch.delta0 | ch.delta1 | ch.delta2)) {   // arena start only; wave-uniform branch
-            unshift_group(d + 0, ch.delta0);
-            unshift_group(d + 4, ch.delta1);
-            unshift_group(d + 8, ch.delta2);
+        uint32_t d[kChunkWords + 1];
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            d[4 * q] = ch.x[q].x;
+            d[4 * q + 1] = ch.x[q].y;
+            d[4 * q + 2] = ch.x[q].z;
+            d[4 * q + 3] = ch.x[q].w;
         }
-        uint32_t w[12];
+        d[kChunkWords] = ch.x6;
+        if (!TINY && __any(ch.dlead)) shift_up(d, ch.dlead);   // arena start only; uniform
+        uint32_t w[kChunkWords];
 #pragma unroll
-        for (int i = 0; i < 12; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ch.r);
+        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ch.r);
+#ifdef FCS_ABL_NOCOMPUTE   // measurement-only build: loads + realign
+        {
+            uint32_t acc = 0;
+#pragma unroll
+            for (int i = 0; i < kChunkWords; i++) acc ^= w[i];
+            s ^= acc;
+            if (c.act && j == 15 && s == 0x12345678u) p.out[c.f] = s;
+            return;
+        }
+#endif
         uint32_t x0;
-        if (c.k == 0) {
+        if (SINGLE || c.k == 0) {
 #pragma unroll
-            for (int i = 0; i < 12; i++) {
-                if (4 * i < (int)p.zmax) {   // uniform bound: skip words no front lane can mask
+            for (int i = 0; i < kChunkWords; i++) {
+                if (4 * i < (int)p.zmax) {   // uniform bound: words no front lane can mask are skipped
                     int t = ch.zr - 4 * i;
                     t = t < 0 ? 0 : (t > 4 ? 4 : t);
                     w[i] &= (uint32_t)(0xFFFFFFFFull << (8 * t));
                 }
             }
-            const int zi = ch.zr < 0 ? 0 : (ch.zr > 47 ? 47 : ch.zr);
+            const int zi = ch.zr < 0 ? 0 : (ch.zr > kChunkBytes - 1 ? kChunkBytes - 1 : ch.zr);
             const uint32_t iv = lds_rd(lds, kLdsInv + 4u * (uint32_t)zi);
             x0 = (ch.zr >= 0 && ch.zr < kChunkBytes) ? iv : 0u;
         } else {
-            x0 = jump(lds, s);
+            x0 = uniform_shift<kLdsJump>(lds, s);
         }
-        uint32_t st = x0;
+        // Two independent 12-word chains (ILP 2 on the LDS latency), joined by H = A_48.
+        uint32_t sa = x0, sb = 0;
 #pragma unroll
-        for (int i = 0; i < 12; i++) st = step4(lds, st ^ w[i], base0, base1);
-        s = st;
+        for (int i = 0; i < kChunkWords / 2; i++) {
+            sa = step4(lds, sa ^ w[i], base0, base1);
+            sb = step4(lds, sb ^ w[kChunkWords / 2 + i], base0, base1);
+        }
+        s = uniform_shift<kLdsHalf>(lds, sa) ^ sb;
 
-        const bool last = c.act && (c.k + 1 == c.it.m);
+        const bool last = c.act && (SINGLE || c.k + 1 == c.it.m);
+#ifdef FCS_ABL_NOFINAL   // measurement-only build: no lane shift / reduction
+        if (last && j == 15) p.out[c.f] = s;
+        return;
+#endif
         if (__any(last)) {
             uint32_t v = last ? lane_shift(lds, s, lanebase) : 0u;
-            v = half_xor(v);
-            if (last && j == 31) p.out[c.f] = c.it.len ? ~v : 0u;
+            v = row_xor(v);
+            if (last && j == 15) p.out[c.f] = c.it.len ? ~v : 0u;
         }
     }
 };
 
-template <bool VAR, bool TINY>
+template <bool VAR, bool TINY, bool SINGLE>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
 
@@ -267,32 +305,33 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
         }
         const uint32_t *src = p.blob + kBlobLane;
         uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
-        for (int i = tid; i < (int)(kBlobInv + 48 - kBlobLane); i += kWgThreads) dst[i] = src[i];
+        for (int i = tid; i < (int)(kBlobWords - kBlobLane); i += kWgThreads) dst[i] = src[i];
         __syncthreads();
     }
 
     const int lane = threadIdx.x & 63;
-    const int j = lane & 31;
-    Lane<VAR, TINY> L{p, lds, j, (uint32_t)j * 4u, 0x10000u | ((uint32_t)j * 4u), kLdsLane | ((uint32_t)j * 4u),
-                (uint64_t)gridDim.x * kHalvesPerWg};
+    const int j = lane & (kGroup - 1);
+    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
+    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4,
+                              (uint64_t)gridDim.x * kSlotsPerWg};
 
-    typename Lane<VAR, TINY>::Pos A, B;
-    A.f = ((uint64_t)blockIdx.x * kHalvesPerWg) + (threadIdx.x >> 5);
+    typename Lane<VAR, TINY, SINGLE>::Pos A, B;
+    A.f = ((uint64_t)blockIdx.x * kSlotsPerWg) + (threadIdx.x / kGroup);
     A.k = 0;
     A.act = A.f < p.n;
-    A.it = A.act ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
+    A.it = (SINGLE || A.act) ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
     Chunk CA, CB;
-    issue_chunk<TINY>(p, A.it, A.k, j, A.act, CA);
+    issue_chunk<VAR, TINY, SINGLE>(p, A.it, A.k, j, A.act, CA);
     uint32_t s = 0;
 
     // Two items in flight per lane: process one while the other's loads are outstanding.
     while (__any(A.act)) {
         B = L.next(A);
-        issue_chunk<TINY>(p, B.it, B.k, j, B.act, CB);
+        issue_chunk<VAR, TINY, SINGLE>(p, B.it, B.k, j, B.act, CB);
         L.process(A, CA, s);
         if (!__any(B.act)) break;
         A = L.next(B);
-        issue_chunk<TINY>(p, A.it, A.k, j, A.act, CA);
+        issue_chunk<VAR, TINY, SINGLE>(p, A.it, A.k, j, A.act, CA);
         L.process(B, CB, s);
     }
 }
@@ -307,7 +346,6 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
 
 __global__ __launch_bounds__(256) void fill_splitmix_kernel(uint8_t *p, uint64_t bytes,
                                                             uint64_t seed, uint64_t off) {
-    // Aligned body: 8-byte words of the stream that fall fully inside [off, off+bytes).
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t nth = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t head = (8 - (off & 7)) & 7;   // bytes before the first aligned stream word
@@ -369,15 +407,21 @@ __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t s
 
 // ---- host-side launchers (the engine TU never names the kernels) ----
 hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st) {
-    const bool tiny = p.hi4 - p.lo4 < 64;
-    if (var && tiny)
-        hipLaunchKernelGGL((fcs_kernel<true, true>), dim3(grid), dim3(kWgThreads), 0, st, p);
-    else if (var)
-        hipLaunchKernelGGL((fcs_kernel<true, false>), dim3(grid), dim3(kWgThreads), 0, st, p);
-    else if (tiny)
-        hipLaunchKernelGGL((fcs_kernel<false, true>), dim3(grid), dim3(kWgThreads), 0, st, p);
-    else
-        hipLaunchKernelGGL((fcs_kernel<false, false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    const bool tiny = p.hi4 - p.lo4 < 2 * kChunkBytes;
+    const bool single = !var && p.fseg == 1;
+#define FCS_LAUNCH(V, T, S) \
+    hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kWgThreads), 0, st, p)
+    if (var) {
+        if (tiny) FCS_LAUNCH(true, true, false);
+        else FCS_LAUNCH(true, false, false);
+    } else if (tiny) {
+        if (single) FCS_LAUNCH(false, true, true);
+        else FCS_LAUNCH(false, true, false);
+    } else {
+        if (single) FCS_LAUNCH(false, false, true);
+        else FCS_LAUNCH(false, false, false);
+    }
+#undef FCS_LAUNCH
     return hipGetLastError();
 }
 

@@ -5,8 +5,12 @@
 // linear operator "advance the register over n zero bytes", appending one 4-byte word w is
 // s' = A_4(s ^ w), and that is what the slice-by-4 tables T3..T0 evaluate. Everything the
 // kernel needs beyond that is an A_n (or its inverse) for a handful of n, tabulated by nibble:
-//   lane tables   L_j = A_{48 j}         j = 0..31   (shift lane j's chunk to the frame end)
-//   jump table    J   = A_{1488}                     (lane's chunk in segment k -> segment k+1)
+//   lane tables   L_j = A_{96 j}         j = 0..15   (shift lane j's chunk to the frame end)
+//   jump table    J   = A_{1440}                     (lane's chunk in segment k -> segment k+1)
+//   half combine  H   = A_48                         (a lane runs its 24 words as two
+//                                                     independent 12-word chains; the first
+//                                                     chain's register is shifted over the
+//                                                     second half's 48 bytes)
 //   front init    INV[z] = A_z^{-1}(0xFFFFFFFF)      (register value that, after z leading
 //                                                     zero bytes, equals the all-ones init)
 // These are constants of the algorithm, computed once per process; no frame bytes are ever
@@ -19,27 +23,32 @@
 namespace fcs {
 
 constexpr uint32_t kPoly = 0xEDB88320u;
-constexpr int kChunkBytes = 48;                       // bytes per lane per segment
-constexpr int kGroup = 32;                            // lanes per frame (half wave)
+constexpr int kChunkBytes = 96;                       // bytes per lane per segment
+constexpr int kChunkWords = kChunkBytes / 4;          // 24
+constexpr int kGroup = 16;                            // lanes per frame (quarter wave)
 constexpr int kSegBytes = kChunkBytes * kGroup;       // 1536
-constexpr int kJumpBytes = kSegBytes - kChunkBytes;   // 1488
+constexpr int kJumpBytes = kSegBytes - kChunkBytes;   // 1440
 
 // LDS layout of the kernel (bytes). Data tables: T_k[b], replica r (= lane & 31) lives at
 //   half(k)*65536 + b*256 + odd(k)*128 + r*4    with T3,T2 in half 0 and T1,T0 in half 1,
 // so the address is one v_perm of {x.byte_k, lane constant} and every ds_read_b32 of a
-// 32-lane group hits 32 distinct banks.
+// 32-lane group hits 32 distinct banks. Lane tables are stored per lane & 31 (bank = lane) with
+// the content of lane & 15, so two frames in one 32-lane group never conflict.
 constexpr uint32_t kLdsData = 0;        // 131072 B
-constexpr uint32_t kLdsLane = 131072;   // 8 nibble tables x 16 entries x 32 lanes x 4 B = 16384
-constexpr uint32_t kLdsJump = 147456;   // 8 x 16 x 4 B = 512
-constexpr uint32_t kLdsInv = 147968;    // 48 x 4 B = 192 (+64 pad)
-constexpr uint32_t kLdsBytes = 148224;
+constexpr uint32_t kLdsLane = 131072;   // 8 nibble tables x 16 entries x 32 slots x 4 B = 16384
+constexpr uint32_t kLdsJump = 147456;   // 8 x 16 x 4 B = 512 (A_1440)
+constexpr uint32_t kLdsHalf = 147968;   // 8 x 16 x 4 B = 512 (A_48)
+constexpr uint32_t kLdsInv = 148480;    // 96 x 4 B = 384
+constexpr uint32_t kLdsBytes = 148864;
 
-// Global "blob" the kernel copies into LDS at start (un-replicated forms).
+// Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
-constexpr uint32_t kBlobLane = 1024;                    // uint32 [8][16][32] (LDS order)
+constexpr uint32_t kBlobLane = 1024;                    // uint32 [8][16][32]
 constexpr uint32_t kBlobJump = kBlobLane + 8 * 16 * 32; // uint32 [8][16]
-constexpr uint32_t kBlobInv = kBlobJump + 8 * 16;       // uint32 [64]
-constexpr uint32_t kBlobWords = kBlobInv + 64;
+constexpr uint32_t kBlobHalf = kBlobJump + 8 * 16;      // uint32 [8][16]
+constexpr uint32_t kBlobInv = kBlobHalf + 8 * 16;       // uint32 [96]
+constexpr uint32_t kBlobWords = kBlobInv + kChunkBytes;
+static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 
 struct Tables {
     uint32_t T[4][256];
@@ -77,14 +86,17 @@ struct Tables {
         std::vector<uint32_t> b(kBlobWords, 0u);
         for (int k = 0; k < 4; k++) std::memcpy(&b[kBlobSlice + 256 * k], T[k], 1024);
         uint32_t nt[8][16];
-        for (int j = 0; j < kGroup; j++) {
-            nibble_table((long)kChunkBytes * j, nt);
+        for (int slot = 0; slot < 32; slot++) {
+            nibble_table((long)kChunkBytes * (slot % kGroup), nt);
             for (int t = 0; t < 8; t++)
-                for (int e = 0; e < 16; e++) b[kBlobLane + (t * 16 + e) * 32 + j] = nt[t][e];
+                for (int e = 0; e < 16; e++) b[kBlobLane + (t * 16 + e) * 32 + slot] = nt[t][e];
         }
         nibble_table(kJumpBytes, nt);
         for (int t = 0; t < 8; t++)
             for (int e = 0; e < 16; e++) b[kBlobJump + t * 16 + e] = nt[t][e];
+        nibble_table(kChunkBytes / 2, nt);
+        for (int t = 0; t < 8; t++)
+            for (int e = 0; e < 16; e++) b[kBlobHalf + t * 16 + e] = nt[t][e];
         for (int z = 0; z < kChunkBytes; z++) b[kBlobInv + z] = shift(0xFFFFFFFFu, -(long)z);
         return b;
     }

@@ -8,12 +8,14 @@ against the oracle (tests/test_kernel_model.py); it is never used to produce pro
 """
 import numpy as np
 
-CHUNK, GROUP = 48, 32
+CHUNK, GROUP = 96, 16
 SEG = CHUNK * GROUP
-LDS_LANE, LDS_JUMP, LDS_INV, LDS_BYTES = 131072, 147456, 147968, 148224
+LDS_LANE, LDS_JUMP, LDS_HALF, LDS_INV, LDS_BYTES = 131072, 147456, 147968, 148480, 148864
 BLOB_SLICE, BLOB_LANE = 0, 1024
 BLOB_JUMP = BLOB_LANE + 8 * 16 * 32
-BLOB_INV = BLOB_JUMP + 8 * 16
+BLOB_HALF = BLOB_JUMP + 8 * 16
+BLOB_INV = BLOB_HALF + 8 * 16
+BLOB_WORDS = BLOB_INV + CHUNK
 
 
 def v_perm(s0, s1, sel):
@@ -39,7 +41,7 @@ def build_lds(blob):
         h, b, odd = i >> 12, (i >> 4) & 255, (i >> 3) & 1
         k = (2 if odd else 3) if h == 0 else (0 if odd else 1)
         lds[i * 4:i * 4 + 4] = blob[BLOB_SLICE + 256 * k + b]
-    n = BLOB_INV + 48 - BLOB_LANE
+    n = BLOB_WORDS - BLOB_LANE
     lds[LDS_LANE // 4:LDS_LANE // 4 + n] = blob[BLOB_LANE:BLOB_LANE + n]
     return lds
 
@@ -67,12 +69,16 @@ def lane_shift(lds, s, j):
     return r
 
 
-def jump(lds, s):
+def uniform_shift(lds, s, region):
     r = 0
     for t in range(8):
         sh = (s >> (4 * t - 2)) if 4 * t >= 2 else ((s << 2) & 0xFFFFFFFF)
-        r ^= rd(lds, ((sh & 0x3C) | LDS_JUMP) + t * 64)
+        r ^= rd(lds, ((sh & 0x3C) | region) + t * 64)
     return r
+
+
+def jump(lds, s):
+    return uniform_shift(lds, s, LDS_JUMP)
 
 
 def alignbyte(hi, lo, r):
@@ -93,26 +99,28 @@ def model_frame(lds, mem: bytes, S: int, L: int):
             z = (S - cstart) if k == 0 else -1
             zr = max(-1, min(CHUNK, z))
             r = cstart & 3
-            d = [0] * 13
+            W = CHUNK // 4
+            d = [0] * (W + 1)
             if zr < CHUNK:
                 a = cstart & ~3
-                for q in range(13 if r else 12):
+                for q in range(W + 1 if r else W):
                     ad = a + 4 * q
                     if ad >= lo4 and ad + 4 <= hi4:
                         d[q] = int.from_bytes(padded[ad:ad + 4], "little")
-            w = [alignbyte(d[i + 1], d[i], r) for i in range(12)]
+            w = [alignbyte(d[i + 1], d[i], r) for i in range(W)]
             if k == 0:
-                for i in range(12):
+                for i in range(W):
                     t = max(0, min(4, zr - 4 * i))
                     w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
-                iv = rd(lds, LDS_INV + 4 * max(0, min(47, zr)))
+                iv = rd(lds, LDS_INV + 4 * max(0, min(CHUNK - 1, zr)))
                 x0 = iv if 0 <= zr < CHUNK else 0
             else:
                 x0 = jump(lds, state[j])
-            st = x0
-            for i in range(12):
-                st = step4(lds, st ^ w[i], j)
-            state[j] = st
+            sa, sb = x0, 0
+            for i in range(W // 2):
+                sa = step4(lds, sa ^ w[i], j)
+                sb = step4(lds, sb ^ w[W // 2 + i], j)
+            state[j] = uniform_shift(lds, sa, LDS_HALF) ^ sb
     v = 0
     for j in range(GROUP):
         v ^= lane_shift(lds, state[j], j)
