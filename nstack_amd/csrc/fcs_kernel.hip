@@ -11,13 +11,13 @@
 //     address (this layout streams HBM at the rate of a coalesced read: tools/microbench), two
 //     chunks in flight per lane; the words are re-aligned to the frame end with v_alignbyte_b32
 //     and the bytes in front of the frame start are zeroed;
-//   * the lane runs its 24 words as two independent 12-word slice-by-4 chains (ILP 2): per word
+//   * the lane runs its 24 words as four independent 6-word slice-by-4 chains (ILP 4): per word
 //     4 ds_read_b32 from byte tables replicated 32x in LDS (replica = lane & 31 -> every 32-lane
-//     LDS access is bank-conflict free), each address formed by ONE v_perm_b32; the first chain
-//     is shifted over the second chain's 48 bytes with H = A_48 (nibble tables) and XORed in;
+//     LDS access is bank-conflict free), each address formed by ONE v_perm_b32; the chains are
+//     merged as A_48(A_24(a) ^ b) ^ (A_24(c) ^ d) with nibble tables;
 //   * the frame's all-ones initial register is injected as the front lane's start value
 //     INV[z] = A_z^{-1}(~0) (z = zero bytes in front of the frame start); across segments a
-//     lane's register jumps over the other lanes' bytes with J = A_1440;
+//     lane accumulates S = A_1536(S) ^ segment value, so consecutive items stay independent;
 //   * at the frame end lane j shifts its register by 96*j zero bytes (per-lane nibble tables,
 //     bank = lane), the 16 registers are XOR-reduced with 4 DPP steps and lane 15 stores ~crc.
 // No MFMA: a byte-stream codec bounded by HBM read bandwidth (roofline: DESIGN.md §4).
@@ -33,6 +33,10 @@ typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kSlotsPerWg = kWgThreads / kGroup;   // 64 frame slots; LDS (145 KiB) -> 1 WG per CU
+constexpr int kSingleMaskWords = 8;                // SINGLE variant: front-lane masks for words < 8
+#ifndef FCS_CHAINS
+#define FCS_CHAINS 2                               // independent chains per lane (2 or 4)
+#endif
 
 // Loads through address space 1 (global): flat loads would also count on lgkmcnt and make every
 // LDS wait drain the prefetched chunk loads.
@@ -41,27 +45,38 @@ __device__ __forceinline__ T gload(uint64_t addr) {
     return *reinterpret_cast<const __attribute__((address_space(1))) T *>(addr);
 }
 
+// a ^ b ^ c in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96.
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
 __device__ __forceinline__ uint32_t lds_rd(const uint8_t *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
 
-// One 4-byte step: A_4(x) = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3].
+// One 4-byte step with the next word folded in: returns A_4(x) ^ wn, where
+// A_4(x) = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3] -> 4 v_perm + 4 ds_read + 2 v_bitop3.
 // base0 = r*4 (half 0: T3 at +0, T2 at +128), base1 = 0x10000 | r*4 (half 1: T1, T0).
-__device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32_t base0,
+__device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32_t wn, uint32_t base0,
                                           uint32_t base1) {
     const uint32_t a0 = __builtin_amdgcn_perm(x, base0, 0x0C020400u);
     const uint32_t a1 = __builtin_amdgcn_perm(x, base0, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, base1, 0x0C020600u);
     const uint32_t a3 = __builtin_amdgcn_perm(x, base1, 0x0C020700u);
-#ifdef FCS_ABL_NOLDS   // measurement-only build: same VALU shape, LDS reads replaced
-    return (a0 * 0x9E3779B1u) ^ (a1 >> 3) ^ (a2 << 5) ^ a3;
+#if defined(FCS_ABL_NOLDS)   // measurement-only build: LDS reads replaced by cheap VALU
+    return xor3(a0 ^ (a1 >> 3), (a2 << 5) ^ (a3 >> 1), wn);
 #else
     const uint32_t t3 = lds_rd(lds, a0);
     const uint32_t t2 = lds_rd(lds, a1 + 128);
     const uint32_t t1 = lds_rd(lds, a2);
     const uint32_t t0 = lds_rd(lds, a3 + 128);
-    return (t3 ^ t2) ^ (t1 ^ t0);
+    return xor3(xor3(t3, t2, t1), t0, wn);
 #endif
+}
+
+// XOR of 8 table values and one extra input: 4 v_bitop3.
+__device__ __forceinline__ uint32_t xor9(const uint32_t (&r)[8], uint32_t extra) {
+    return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), xor3(r[6], r[7], extra));
 }
 
 // A_{96 j}(s): this lane's own nibble tables (entry e of table t at kLdsLane + t*2048 + e*128 +
@@ -73,20 +88,21 @@ __device__ __forceinline__ uint32_t lane_shift(const uint8_t *lds, uint32_t s, u
         const uint32_t sh = (4 * t >= 7) ? (s >> (4 * t - 7)) : (s << (7 - 4 * t));
         r[t] = lds_rd(lds, ((sh & 0x780u) | lanebase) + t * 2048);
     }
-    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
+    return xor9(r, 0u);
 }
 
-// A_n(s) for one n shared by all lanes (J = A_1440 at kLdsJump, H = A_48 at kLdsHalf):
+// A_n(s) for one n shared by all lanes (J = A_1536, H48 = A_48, H24 = A_24):
 // entry e of nibble table t at REGION + t*64 + e*4; 16 entries span 16 banks -> conflict free.
+// Returns A_n(s) ^ extra.
 template <uint32_t REGION>
-__device__ __forceinline__ uint32_t uniform_shift(const uint8_t *lds, uint32_t s) {
+__device__ __forceinline__ uint32_t uniform_shift(const uint8_t *lds, uint32_t s, uint32_t extra) {
     uint32_t r[8];
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
         r[t] = lds_rd(lds, ((sh & 0x3Cu) | REGION) + t * 64);
     }
-    return ((r[0] ^ r[1]) ^ (r[2] ^ r[3])) ^ ((r[4] ^ r[5]) ^ (r[6] ^ r[7]));
+    return xor9(r, extra);
 }
 
 // XOR over each 16-lane row (one frame); every lane of the row ends with the row's XOR.
@@ -173,6 +189,21 @@ __device__ __forceinline__ void issue_chunk(const KParams &p, const Item &it, ui
         c.dlead = a < p.lo4 ? (int)((p.lo4 - a) >> 2) : 0;
         ab = a < p.lo4 ? p.lo4 : a;
     }
+#ifdef FCS_ABL_COALESCED   // measurement-only build: same bytes per quarter, coalesced 256-B rows
+    {
+        // quarter's segment start, 16-B aligned, clamped to the arena: every read stays in
+        // [lo16, sb + 1536) with sb + 1536 <= frame end (or lo16 + 1536 for idle/edge lanes).
+        const uint64_t seg0 = (uint64_t)cstart + (uint64_t)kChunkBytes * (j + 1) - kSegBytes;
+        const uint64_t lo16 = (p.lo4 + 15) & ~15ull;
+        uint64_t sb = seg0 & ~15ull;
+        sb = (need && sb >= lo16) ? sb : lo16;
+        const uint64_t cb = sb + 16 * (uint64_t)j;
+#pragma unroll
+        for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(cb + 256 * q);
+        c.x6 = gload<uint32_t>(cb + 4);
+        return;
+    }
+#endif
 #pragma unroll
     for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(ab + 16 * q);
     c.x6 = gload<uint32_t>(ab + ((c.r || c.dlead) ? 96 : 92));
@@ -247,11 +278,14 @@ struct Lane {
             return;
         }
 #endif
-        uint32_t x0;
-        if (SINGLE || c.k == 0) {
+        uint32_t x0 = 0;
+        const bool first = SINGLE || c.k == 0;
+        if (first) {
 #pragma unroll
             for (int i = 0; i < kChunkWords; i++) {
-                if (4 * i < (int)p.zmax) {   // uniform bound: words no front lane can mask are skipped
+                // uniform bound: words no front lane can mask are skipped. SINGLE launches only when
+                // zmax <= 32 (host), so at most 8 loop-invariant masks stay live in registers.
+                if ((!SINGLE || i < kSingleMaskWords) && 4 * i < (int)p.zmax) {
                     int t = ch.zr - 4 * i;
                     t = t < 0 ? 0 : (t > 4 ? 4 : t);
                     w[i] &= (uint32_t)(0xFFFFFFFFull << (8 * t));
@@ -260,17 +294,31 @@ struct Lane {
             const int zi = ch.zr < 0 ? 0 : (ch.zr > kChunkBytes - 1 ? kChunkBytes - 1 : ch.zr);
             const uint32_t iv = lds_rd(lds, kLdsInv + 4u * (uint32_t)zi);
             x0 = (ch.zr >= 0 && ch.zr < kChunkBytes) ? iv : 0u;
-        } else {
-            x0 = uniform_shift<kLdsJump>(lds, s);
         }
-        // Two independent 12-word chains (ILP 2 on the LDS latency), joined by H = A_48.
-        uint32_t sa = x0, sb = 0;
+#if FCS_CHAINS == 2
+        // Two independent 12-word chains, merged with A_48.
+        uint32_t xa = x0 ^ w[0], xb = w[12];
 #pragma unroll
-        for (int i = 0; i < kChunkWords / 2; i++) {
-            sa = step4(lds, sa ^ w[i], base0, base1);
-            sb = step4(lds, sb ^ w[kChunkWords / 2 + i], base0, base1);
+        for (int i = 0; i < 12; i++) {
+            xa = step4(lds, xa, i < 11 ? w[i + 1] : 0u, base0, base1);
+            xb = step4(lds, xb, i < 11 ? w[13 + i] : 0u, base0, base1);
         }
-        s = uniform_shift<kLdsHalf>(lds, sa) ^ sb;
+        const uint32_t r = uniform_shift<kLdsH48>(lds, xa, xb);
+#else
+        // Four independent 6-word chains (ILP 4 on the LDS/VALU latency), merged as a tree.
+        uint32_t xa = x0 ^ w[0], xb = w[6], xc = w[12], xd = w[18];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            xa = step4(lds, xa, i < 5 ? w[i + 1] : 0u, base0, base1);
+            xb = step4(lds, xb, i < 5 ? w[7 + i] : 0u, base0, base1);
+            xc = step4(lds, xc, i < 5 ? w[13 + i] : 0u, base0, base1);
+            xd = step4(lds, xd, i < 5 ? w[19 + i] : 0u, base0, base1);
+        }
+        const uint32_t ab = uniform_shift<kLdsH24>(lds, xa, xb);
+        const uint32_t cd = uniform_shift<kLdsH24>(lds, xc, xd);
+        const uint32_t r = uniform_shift<kLdsH48>(lds, ab, cd);
+#endif
+        s = first ? r : uniform_shift<kLdsJump>(lds, s, r);
 
         const bool last = c.act && (SINGLE || c.k + 1 == c.it.m);
 #ifdef FCS_ABL_NOFINAL   // measurement-only build: no lane shift / reduction
@@ -324,6 +372,10 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
     issue_chunk<VAR, TINY, SINGLE>(p, A.it, A.k, j, A.act, CA);
     uint32_t s = 0;
 
+#ifndef FCS_PREFETCH_DEPTH
+#define FCS_PREFETCH_DEPTH 2
+#endif
+#if FCS_PREFETCH_DEPTH == 2
     // Two items in flight per lane: process one while the other's loads are outstanding.
     while (__any(A.act)) {
         B = L.next(A);
@@ -334,6 +386,27 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
         issue_chunk<VAR, TINY, SINGLE>(p, A.it, A.k, j, A.act, CA);
         L.process(B, CB, s);
     }
+#else
+    // Three chunk buffers: while one item is processed the next two have their loads in flight.
+    typename Lane<VAR, TINY, SINGLE>::Pos C;
+    Chunk CC;
+    B = L.next(A);
+    issue_chunk<VAR, TINY, SINGLE>(p, B.it, B.k, j, B.act, CB);
+    for (;;) {
+        if (!__any(A.act)) break;
+        C = L.next(B);
+        issue_chunk<VAR, TINY, SINGLE>(p, C.it, C.k, j, C.act, CC);
+        L.process(A, CA, s);
+        if (!__any(B.act)) break;
+        A = L.next(C);
+        issue_chunk<VAR, TINY, SINGLE>(p, A.it, A.k, j, A.act, CA);
+        L.process(B, CB, s);
+        if (!__any(C.act)) break;
+        B = L.next(A);
+        issue_chunk<VAR, TINY, SINGLE>(p, B.it, B.k, j, B.act, CB);
+        L.process(C, CC, s);
+    }
+#endif
 }
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
@@ -408,7 +481,11 @@ __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t s
 // ---- host-side launchers (the engine TU never names the kernels) ----
 hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st) {
     const bool tiny = p.hi4 - p.lo4 < 2 * kChunkBytes;
-    const bool single = !var && p.fseg == 1;
+#ifdef FCS_NO_SINGLE   // measurement-only build
+    const bool single = false;
+#else
+    const bool single = !var && p.fseg == 1 && p.zmax <= 4 * kSingleMaskWords;
+#endif
 #define FCS_LAUNCH(V, T, S) \
     hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kWgThreads), 0, st, p)
     if (var) {

@@ -6,11 +6,13 @@
 // s' = A_4(s ^ w), and that is what the slice-by-4 tables T3..T0 evaluate. Everything the
 // kernel needs beyond that is an A_n (or its inverse) for a handful of n, tabulated by nibble:
 //   lane tables   L_j = A_{96 j}         j = 0..15   (shift lane j's chunk to the frame end)
-//   jump table    J   = A_{1440}                     (lane's chunk in segment k -> segment k+1)
-//   half combine  H   = A_48                         (a lane runs its 24 words as two
-//                                                     independent 12-word chains; the first
-//                                                     chain's register is shifted over the
-//                                                     second half's 48 bytes)
+//   segment shift J   = A_{1536}                     (a lane's register accumulated over
+//                                                     segment k is advanced by one segment
+//                                                     before segment k+1's value is XORed in)
+//   chain combine H48 = A_48, H24 = A_24             (a lane runs its 24 words as four
+//                                                     independent 6-word chains and merges
+//                                                     them as a tree: A_48(A_24(a)^b) ^
+//                                                     (A_24(c)^d))
 //   front init    INV[z] = A_z^{-1}(0xFFFFFFFF)      (register value that, after z leading
 //                                                     zero bytes, equals the all-ones init)
 // These are constants of the algorithm, computed once per process; no frame bytes are ever
@@ -27,7 +29,7 @@ constexpr int kChunkBytes = 96;                       // bytes per lane per segm
 constexpr int kChunkWords = kChunkBytes / 4;          // 24
 constexpr int kGroup = 16;                            // lanes per frame (quarter wave)
 constexpr int kSegBytes = kChunkBytes * kGroup;       // 1536
-constexpr int kJumpBytes = kSegBytes - kChunkBytes;   // 1440
+constexpr int kJumpBytes = kSegBytes;                 // 1536 (segment accumulation)
 
 // LDS layout of the kernel (bytes). Data tables: T_k[b], replica r (= lane & 31) lives at
 //   half(k)*65536 + b*256 + odd(k)*128 + r*4    with T3,T2 in half 0 and T1,T0 in half 1,
@@ -36,17 +38,19 @@ constexpr int kJumpBytes = kSegBytes - kChunkBytes;   // 1440
 // the content of lane & 15, so two frames in one 32-lane group never conflict.
 constexpr uint32_t kLdsData = 0;        // 131072 B
 constexpr uint32_t kLdsLane = 131072;   // 8 nibble tables x 16 entries x 32 slots x 4 B = 16384
-constexpr uint32_t kLdsJump = 147456;   // 8 x 16 x 4 B = 512 (A_1440)
-constexpr uint32_t kLdsHalf = 147968;   // 8 x 16 x 4 B = 512 (A_48)
-constexpr uint32_t kLdsInv = 148480;    // 96 x 4 B = 384
-constexpr uint32_t kLdsBytes = 148864;
+constexpr uint32_t kLdsJump = 147456;   // 8 x 16 x 4 B = 512 (A_1536)
+constexpr uint32_t kLdsH48 = 147968;    // 8 x 16 x 4 B = 512 (A_48)
+constexpr uint32_t kLdsH24 = 148480;    // 8 x 16 x 4 B = 512 (A_24)
+constexpr uint32_t kLdsInv = 148992;    // 96 x 4 B = 384
+constexpr uint32_t kLdsBytes = 149376;
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
 constexpr uint32_t kBlobLane = 1024;                    // uint32 [8][16][32]
 constexpr uint32_t kBlobJump = kBlobLane + 8 * 16 * 32; // uint32 [8][16]
-constexpr uint32_t kBlobHalf = kBlobJump + 8 * 16;      // uint32 [8][16]
-constexpr uint32_t kBlobInv = kBlobHalf + 8 * 16;       // uint32 [96]
+constexpr uint32_t kBlobH48 = kBlobJump + 8 * 16;       // uint32 [8][16]
+constexpr uint32_t kBlobH24 = kBlobH48 + 8 * 16;        // uint32 [8][16]
+constexpr uint32_t kBlobInv = kBlobH24 + 8 * 16;        // uint32 [96]
 constexpr uint32_t kBlobWords = kBlobInv + kChunkBytes;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 
@@ -94,9 +98,12 @@ struct Tables {
         nibble_table(kJumpBytes, nt);
         for (int t = 0; t < 8; t++)
             for (int e = 0; e < 16; e++) b[kBlobJump + t * 16 + e] = nt[t][e];
-        nibble_table(kChunkBytes / 2, nt);
+        nibble_table(48, nt);
         for (int t = 0; t < 8; t++)
-            for (int e = 0; e < 16; e++) b[kBlobHalf + t * 16 + e] = nt[t][e];
+            for (int e = 0; e < 16; e++) b[kBlobH48 + t * 16 + e] = nt[t][e];
+        nibble_table(24, nt);
+        for (int t = 0; t < 8; t++)
+            for (int e = 0; e < 16; e++) b[kBlobH24 + t * 16 + e] = nt[t][e];
         for (int z = 0; z < kChunkBytes; z++) b[kBlobInv + z] = shift(0xFFFFFFFFu, -(long)z);
         return b;
     }

@@ -10,11 +10,12 @@ import numpy as np
 
 CHUNK, GROUP = 96, 16
 SEG = CHUNK * GROUP
-LDS_LANE, LDS_JUMP, LDS_HALF, LDS_INV, LDS_BYTES = 131072, 147456, 147968, 148480, 148864
+LDS_LANE, LDS_JUMP, LDS_H48, LDS_H24, LDS_INV, LDS_BYTES = 131072, 147456, 147968, 148480, 148992, 149376
 BLOB_SLICE, BLOB_LANE = 0, 1024
 BLOB_JUMP = BLOB_LANE + 8 * 16 * 32
-BLOB_HALF = BLOB_JUMP + 8 * 16
-BLOB_INV = BLOB_HALF + 8 * 16
+BLOB_H48 = BLOB_JUMP + 8 * 16
+BLOB_H24 = BLOB_H48 + 8 * 16
+BLOB_INV = BLOB_H24 + 8 * 16
 BLOB_WORDS = BLOB_INV + CHUNK
 
 
@@ -115,12 +116,18 @@ def model_frame(lds, mem: bytes, S: int, L: int):
                 iv = rd(lds, LDS_INV + 4 * max(0, min(CHUNK - 1, zr)))
                 x0 = iv if 0 <= zr < CHUNK else 0
             else:
-                x0 = jump(lds, state[j])
-            sa, sb = x0, 0
-            for i in range(W // 2):
+                x0 = 0
+            q = W // 4
+            sa, sb, sc, sd = x0, 0, 0, 0
+            for i in range(q):
                 sa = step4(lds, sa ^ w[i], j)
-                sb = step4(lds, sb ^ w[W // 2 + i], j)
-            state[j] = uniform_shift(lds, sa, LDS_HALF) ^ sb
+                sb = step4(lds, sb ^ w[q + i], j)
+                sc = step4(lds, sc ^ w[2 * q + i], j)
+                sd = step4(lds, sd ^ w[3 * q + i], j)
+            ab = uniform_shift(lds, sa, LDS_H24) ^ sb
+            cd = uniform_shift(lds, sc, LDS_H24) ^ sd
+            r = uniform_shift(lds, ab, LDS_H48) ^ cd
+            state[j] = r if k == 0 else (jump(lds, state[j]) ^ r)
     v = 0
     for j in range(GROUP):
         v ^= lane_shift(lds, state[j], j)

@@ -1,0 +1,61 @@
+#!/usr/bin/env python3
+"""In-process A/B timing of FCS kernel variants (measurement tool, not product code).
+
+    python tools/ab.py [--frames F] [--len L] [--rounds R] lib1.so lib2.so ...
+
+Every library is a full build of the engine (tools/variants.sh); all are loaded into ONE process
+and launched round-robin on the same HBM-resident frames, so clock/device differences cancel
+(cdna_hip_programming.md §5.4 rule 24). Prints median / min ms per launch and GB/s per variant,
+and checks every variant's CRCs against the first one's.
+"""
+import argparse
+import ctypes
+import os
+import statistics
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--frames", type=int, default=64 << 20)
+    ap.add_argument("--len", type=int, default=1518)
+    ap.add_argument("--rounds", type=int, default=6)
+    ap.add_argument("--reps", type=int, default=3)
+    a = ap.parse_args()
+    import torch
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda:0")
+    n, L = a.frames, a.len
+    libs = []
+    for p in a.libs:
+        lib = ctypes.CDLL(os.path.abspath(p))
+        lib.ether_fcs_fixed_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
+                                            ctypes.c_void_p, ctypes.c_void_p]
+        lib.fcs_fill_splitmix64_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_void_p]
+        libs.append(lib)
+    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    libs[0].fcs_fill_splitmix64_dev(arena.data_ptr(), n * L, 11, 0, None)
+    outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
+    st = torch.cuda.current_stream()
+    times = [[] for _ in libs]
+    for r in range(a.rounds + 1):
+        for i, lib in enumerate(libs):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(st)
+            for _ in range(a.reps):
+                rc = lib.ether_fcs_fixed_dev(arena.data_ptr(), L, L, n, outs[i].data_ptr(), st.cuda_stream)
+                assert rc == 0, rc
+            e1.record(st)
+            torch.cuda.synchronize()
+            if r:
+                times[i].append(e0.elapsed_time(e1) / a.reps)
+    for i, p in enumerate(a.libs):
+        med, mn = statistics.median(times[i]), min(times[i])
+        same = bool(torch.equal(outs[i], outs[0]))
+        print(f"{os.path.basename(p):28s} median {med:8.3f} ms  min {mn:8.3f} ms  "
+              f"{n * L / med / 1e6:8.1f} GB/s  same_as_first={same}")
+
+
+if __name__ == "__main__":
+    main()
