@@ -1,0 +1,99 @@
+"""N > 1 path on CPU: two ranks over gloo (127.0.0.1) run bench.py's sharding and timing logic.
+
+Frames shard embarrassingly: each rank owns a contiguous slice of one global
+counter-based frame stream, computes its CRCs (here with the oracle — test infrastructure; on
+the GPU box the same ranges go to the HIP kernel), and the job reports all ranks' bytes over the
+max rank time. Checks: the ranges partition the frame space; the gathered per-rank CRCs equal a
+single-process pass over all frames (shard consistency); the MAX all-reduce and aggregate()
+arithmetic; no collective touches frame data.
+"""
+import ctypes
+import os
+import socket
+import sys
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+TOTAL, L, SEED = 3001, 1518, 77
+
+
+def _oracle():
+    o = ctypes.CDLL(os.path.join(ROOT, "oracle", "_build", "liboracle.so"))
+    o.oracle_splitmix_fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64, ctypes.c_uint64]
+    o.oracle_fcs_fixed.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t,
+                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+    return o
+
+
+def _crcs(o, lo, hi):
+    n = hi - lo
+    buf = np.empty(max(n, 1) * L, dtype=np.uint8)
+    o.oracle_splitmix_fill(buf.ctypes.data, n * L, SEED, lo * L)
+    out = np.zeros(max(n, 1), dtype=np.uint32)
+    if n:
+        o.oracle_fcs_fixed(buf.ctypes.data, L, L, n, out.ctypes.data, 1, 1)
+    return out[:n]
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o = _oracle()
+    lo, hi = bench.shard_range(TOTAL, world, rank)
+    dist.barrier()
+    crc = _crcs(o, lo, hi)
+    elapsed = torch.tensor([0.5 + rank], dtype=torch.float64)   # synthetic per-rank times
+    dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    sizes = [None] * world
+    dist.all_gather_object(sizes, (lo, hi, crc.tolist()))
+    dist.barrier()
+    if rank == 0:
+        q.put((sizes, float(elapsed.item())))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("world", [2])
+def test_two_rank_sharding_matches_single_pass(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    sizes, tmax = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # ranges partition [0, TOTAL) contiguously
+    assert sizes[0][0] == 0 and sizes[-1][1] == TOTAL
+    for a, b in zip(sizes, sizes[1:]):
+        assert a[1] == b[0]
+    gathered = np.concatenate([np.array(s[2], dtype=np.uint32) for s in sizes])
+    assert np.array_equal(gathered, _crcs(_oracle(), 0, TOTAL))
+    assert tmax == 0.5 + (world - 1)
+    value, t = bench.aggregate([(s[1] - s[0]) * L for s in sizes], [0.5, 1.5])
+    assert t == 1.5 and value == TOTAL * L / 1.5
+
+
+def test_shard_ranges_cover_eight_gpus():
+    total = 512 << 20   # BASELINE configs[4]
+    r = [bench.shard_range(total, 8, k) for k in range(8)]
+    assert r[0][0] == 0 and r[-1][1] == total
+    assert all(hi - lo == 64 << 20 for lo, hi in r)
