@@ -333,29 +333,31 @@ struct Lane {
     }
 };
 
+// Stage the constant tables into LDS (once per workgroup; grids are persistent).
+__device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
+    const int tid = threadIdx.x;
+    // data: 8192 x 16 B; each b128 store = 4 replicas of one entry
+    for (int i = tid; i < 8192; i += kWgThreads) {
+        const int h = i >> 12;            // 64 KiB half
+        const int b = (i >> 4) & 255;     // entry
+        const int odd = (i >> 3) & 1;     // +128 slot
+        // half 0: T3 (+0), T2 (+128); half 1: T1 (+0), T0 (+128)
+        const int k = h == 0 ? (odd ? 2 : 3) : (odd ? 0 : 1);
+        const uint32_t v = p.blob[kBlobSlice + 256 * k + b];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
+    }
+    const uint32_t *src = p.blob + kBlobLane;
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
+    for (int i = tid; i < (int)(kBlobWords - kBlobLane); i += kWgThreads) dst[i] = src[i];
+    __syncthreads();
+}
+
 template <bool VAR, bool TINY, bool SINGLE>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
 
-    // ---- stage the tables into LDS (once per workgroup; the grid is persistent) ----
-    {
-        const int tid = threadIdx.x;
-        // data: 8192 x 16 B; each b128 store = 4 replicas of one entry
-        for (int i = tid; i < 8192; i += kWgThreads) {
-            const int h = i >> 12;            // 64 KiB half
-            const int b = (i >> 4) & 255;     // entry
-            const int odd = (i >> 3) & 1;     // +128 slot
-            // half 0: T3 (+0), T2 (+128); half 1: T1 (+0), T0 (+128)
-            const int k = h == 0 ? (odd ? 2 : 3) : (odd ? 0 : 1);
-            const uint32_t v = p.blob[kBlobSlice + 256 * k + b];
-            u32x4 vv = {v, v, v, v};
-            *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
-        }
-        const uint32_t *src = p.blob + kBlobLane;
-        uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
-        for (int i = tid; i < (int)(kBlobWords - kBlobLane); i += kWgThreads) dst[i] = src[i];
-        __syncthreads();
-    }
+    stage_tables(p, lds);
 
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
@@ -407,6 +409,314 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
         L.process(C, CC, s);
     }
 #endif
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Fixed length, one segment, at most 32 leading garbage bytes in the front lane (host-selected:
+// 1504 <= len <= 1536, which covers the 1518-B benchmark frames). The generic kernel's work per
+// item, strength-reduced: the frame end advances by a constant, the per-lane chunk offset, front
+// masks and INV start value are loop invariants, and only a wave's first item can touch the
+// arena start, so the edge repair is peeled out of the loop.
+// ---------------------------------------------------------------------------------------------
+struct Raw {
+    u32x4a4 x[6];
+    uint32_t x6;
+};
+
+struct SingleLane {
+    const uint8_t *lds;
+    int j;
+    uint32_t base0, base1, lanebase, x0, zmax;
+    uint32_t m[kSingleMaskWords];
+
+    template <bool EDGE>
+    __device__ __forceinline__ void process(const Raw &c, uint32_t r, int dlead, bool act,
+                                            uint32_t *outp) const {
+        uint32_t d[kChunkWords + 1];
+#pragma unroll
+        for (int q = 0; q < 6; q++) {
+            d[4 * q] = c.x[q].x;
+            d[4 * q + 1] = c.x[q].y;
+            d[4 * q + 2] = c.x[q].z;
+            d[4 * q + 3] = c.x[q].w;
+        }
+        d[kChunkWords] = c.x6;
+        if (EDGE && __any(dlead)) shift_up(d, dlead);
+        uint32_t w[kChunkWords];
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#pragma unroll
+        for (int i = 0; i < kSingleMaskWords; i++)
+            if (4 * i < (int)zmax) w[i] &= m[i];
+        uint32_t xa = x0 ^ w[0], xb = w[12];
+#pragma unroll
+        for (int i = 0; i < 12; i++) {
+            xa = step4(lds, xa, i < 11 ? w[i + 1] : 0u, base0, base1);
+            xb = step4(lds, xb, i < 11 ? w[13 + i] : 0u, base0, base1);
+        }
+        uint32_t v = lane_shift(lds, uniform_shift<kLdsH48>(lds, xa, xb), lanebase);
+        v = row_xor(v);
+        if (act && j == 15) *outp = ~v;
+    }
+};
+
+__device__ __forceinline__ void issue_raw(uint64_t a, uint32_t r, Raw &c) {
+#pragma unroll
+    for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(a + 16 * q);
+    c.x6 = gload<uint32_t>(a + (r ? 96 : 92));   // 25th dword only matters when r != 0
+}
+
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    stage_tables(p, lds);
+
+    const int lane = threadIdx.x & 63;
+    const int j = lane & (kGroup - 1);
+    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
+    SingleLane S;
+    S.lds = lds;
+    S.j = j;
+    S.base0 = r4;
+    S.base1 = 0x10000u | r4;
+    S.lanebase = kLdsLane | r4;
+    S.zmax = p.zmax;
+    const uint32_t loff = (uint32_t)kChunkBytes * (uint32_t)(j + 1);   // chunk start = end - loff
+    {
+        int zr = (int)loff - (int)p.flen;
+        zr = zr < -1 ? -1 : (zr > kChunkBytes ? kChunkBytes : zr);
+#pragma unroll
+        for (int i = 0; i < kSingleMaskWords; i++) {
+            int t = zr - 4 * i;
+            t = t < 0 ? 0 : (t > 4 ? 4 : t);
+            S.m[i] = (uint32_t)(0xFFFFFFFFull << (8 * t));
+        }
+        const uint32_t iv = lds_rd(lds, kLdsInv + 4u * (uint32_t)(zr < 0 ? 0 : (zr > kChunkBytes - 1 ? kChunkBytes - 1 : zr)));
+        S.x0 = (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
+    }
+
+    const uint64_t Q = (uint64_t)gridDim.x * kSlotsPerWg;
+    const uint64_t f0 = (uint64_t)blockIdx.x * kSlotsPerWg + threadIdx.x / kGroup;
+    int rem = f0 < p.n ? (int)((p.n - 1 - f0) / Q) + 1 : 0;   // items left for this frame slot
+    uint64_t end = p.base + f0 * p.stride + p.flen;
+    const uint64_t dend = Q * p.stride;
+    uint32_t *outp = p.out + f0;
+
+    // ---- first item: the only one that can start before the arena (frame 0's front lane) ----
+    Raw A, B;
+    int dlead = 0;
+    uint32_t rA = (uint32_t)end & 3u;
+    {
+        const uint64_t a = rem > 0 ? ((end - loff) & ~3ull) : p.lo4;
+        uint64_t ab = a;
+        if (__any(a < p.lo4)) {
+            dlead = a < p.lo4 ? (int)((p.lo4 - a) >> 2) : 0;
+            ab = a < p.lo4 ? p.lo4 : a;
+        }
+#pragma unroll
+        for (int q = 0; q < 6; q++) A.x[q] = gload<u32x4a4>(ab + 16 * q);
+        A.x6 = gload<uint32_t>(ab + ((rA || dlead) ? 96 : 92));
+    }
+    uint64_t endB = end + dend;
+    uint32_t rB = (uint32_t)endB & 3u;
+    issue_raw(rem > 1 ? ((endB - loff) & ~3ull) : p.lo4, rB, B);
+    S.process<true>(A, rA, dlead, rem > 0, outp);
+    rem -= 1;
+    end = endB;
+    outp += Q;
+
+    // ---- steady state: two items in flight per lane ----
+    while (__any(rem > 0)) {
+        const uint64_t endA = end + dend;
+        rA = (uint32_t)endA & 3u;
+        issue_raw(rem > 1 ? ((endA - loff) & ~3ull) : p.lo4, rA, A);
+        S.process<false>(B, rB, 0, rem > 0, outp);
+        rem -= 1;
+        end = endA;
+        outp += Q;
+        if (!__any(rem > 0)) break;
+        endB = end + dend;
+        rB = (uint32_t)endB & 3u;
+        issue_raw(rem > 1 ? ((endB - loff) & ~3ull) : p.lo4, rB, B);
+        S.process<false>(A, rA, 0, rem > 0, outp);
+        rem -= 1;
+        end = endB;
+        outp += Q;
+    }
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Variable-length frames (IMIX-shaped batches): windowed class scheduling.
+// A wave owns windows of 64 consecutive frames (frame i of a window <-> lane i for metadata).
+// The window's frames are split by length into classes that use lanes differently:
+//   small  (len <= 96):  the owning lane alone processes the frame as one chunk (chunk 0, no
+//                        lane shift, no reduction);
+//   medium (len <= 768): 8 lanes per frame (chunk c <- lane & 7), 8 frames per item; lanes 8..15
+//                        of a row used the lane tables of chunks 8..15, fixed by one A_{-768};
+//   big    (len > 768):  16 lanes per frame (as the fixed kernels), 4 frames per item,
+//                        1536-B segments accumulated with A_1536.
+// All classes read the same ~64 frames of the arena close together in time (L2-local).
+// ---------------------------------------------------------------------------------------------
+template <bool TINY>
+__device__ __forceinline__ void issue_any(const KParams &p, int64_t cstart, bool need, Chunk &c) {
+    c.r = (uint32_t)cstart & 3u;
+    const uint64_t a = need ? ((uint64_t)cstart & ~3ull) : p.lo4;
+    c.dlead = 0;
+    if (TINY) {
+        uint32_t d[kChunkWords + 1];
+#pragma unroll
+        for (int q = 0; q <= kChunkWords; q++) {
+            const uint64_t ad = a + 4 * q;
+            d[q] = (need && ad >= p.lo4 && ad + 4 <= p.hi4) ? gload<uint32_t>(ad) : 0u;
+        }
+#pragma unroll
+        for (int g = 0; g < 6; g++) c.x[g] = u32x4a4{d[4 * g], d[4 * g + 1], d[4 * g + 2], d[4 * g + 3]};
+        c.x6 = d[kChunkWords];
+        return;
+    }
+    uint64_t ab = a;
+    if (__any(a < p.lo4)) {
+        c.dlead = a < p.lo4 ? (int)((p.lo4 - a) >> 2) : 0;
+        ab = a < p.lo4 ? p.lo4 : a;
+    }
+#pragma unroll
+    for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(ab + 16 * q);
+    c.x6 = gload<uint32_t>(ab + ((c.r || c.dlead) ? 96 : 92));
+}
+
+// Register value of one chunk (realigned, bytes before the frame start masked, x0 injected),
+// before the lane shift: A_48(chain(words 0..11)) ^ chain(words 12..23).
+template <bool TINY>
+__device__ __forceinline__ uint32_t chunk_value(const uint8_t *lds, const Chunk &c, int zr, uint32_t x0,
+                                                uint32_t base0, uint32_t base1) {
+    uint32_t d[kChunkWords + 1];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        d[4 * q] = c.x[q].x;
+        d[4 * q + 1] = c.x[q].y;
+        d[4 * q + 2] = c.x[q].z;
+        d[4 * q + 3] = c.x[q].w;
+    }
+    d[kChunkWords] = c.x6;
+    if (!TINY && __any(c.dlead)) shift_up(d, c.dlead);
+    uint32_t w[kChunkWords];
+#pragma unroll
+    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], c.r);
+    if (__any(zr > 0)) {
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) {
+            int t = zr - 4 * i;
+            t = t < 0 ? 0 : (t > 4 ? 4 : t);
+            w[i] &= (uint32_t)(0xFFFFFFFFull << (8 * t));
+        }
+    }
+    uint32_t xa = x0 ^ w[0], xb = w[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+        xa = step4(lds, xa, i < 11 ? w[i + 1] : 0u, base0, base1);
+        xb = step4(lds, xb, i < 11 ? w[13 + i] : 0u, base0, base1);
+    }
+    return uniform_shift<kLdsH48>(lds, xa, xb);
+}
+
+__device__ __forceinline__ uint32_t inv_start(const uint8_t *lds, int zr) {
+    const int zi = zr < 0 ? 0 : (zr > kChunkBytes - 1 ? kChunkBytes - 1 : zr);
+    const uint32_t iv = lds_rd(lds, kLdsInv + 4u * (uint32_t)zi);
+    return (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
+}
+
+__device__ __forceinline__ int clamp_zr(int64_t z) {
+    return z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
+}
+
+template <bool TINY>
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    stage_tables(p, lds);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int j = lane & (kGroup - 1);
+    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
+    const uint32_t base0 = r4, base1 = 0x10000u | r4, lanebase = kLdsLane | r4;
+    uint8_t *lists = lds + kLdsWave + wave * kLdsWaveBytes;   // [0,64): medium, [64,128): big
+    const uint64_t GW = (uint64_t)gridDim.x * (kWgThreads / 64);
+
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kWgThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
+        // ---- window metadata: lane i <-> frame w0 + i ----
+        const uint64_t f = w0 + lane;
+        const bool act = f < p.n;
+        const uint32_t L = act ? p.len[f] : 0u;
+        const uint64_t E = act ? p.base + p.off[f] + L : p.lo4;
+        const bool small = act && L <= (uint32_t)kChunkBytes;
+        const bool med = act && !small && L <= 8u * kChunkBytes;
+        const bool big = act && L > 8u * kChunkBytes;
+        const uint64_t mmask = __ballot(med), bmask = __ballot(big);
+        const uint32_t nm = (uint32_t)__popcll(mmask), nb = (uint32_t)__popcll(bmask);
+        const uint32_t rm = __builtin_amdgcn_mbcnt_hi((uint32_t)(mmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mmask, 0u));
+        const uint32_t rb = __builtin_amdgcn_mbcnt_hi((uint32_t)(bmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bmask, 0u));
+        if (med) lists[rm] = (uint8_t)lane;
+        if (big) lists[64 + rb] = (uint8_t)lane;
+        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
+
+        // ---- small frames: each in its own lane ----
+        if (__any(small)) {
+            const int zr = small ? (int)(kChunkBytes - L) : kChunkBytes;
+            Chunk c;
+            issue_any<TINY>(p, (int64_t)E - kChunkBytes, small && L > 0, c);
+            const uint32_t v = chunk_value<TINY>(lds, c, zr, small ? inv_start(lds, zr) : 0u, base0, base1);
+            if (small) p.out[f] = L ? ~v : 0u;
+        }
+
+        // ---- medium frames: 8 lanes each, 8 per item ----
+        for (uint32_t t = 0; t < nm; t += 8) {
+            const uint32_t rank = t + (uint32_t)(lane >> 3);
+            const bool valid = rank < nm;
+            const int src = valid ? (int)lists[rank] : 0;
+            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+            const uint32_t Lg = (uint32_t)__shfl((int)L, src);
+            const int c8 = lane & 7;
+            const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (c8 + 1);
+            const int zr = clamp_zr((int64_t)(Eg - Lg) - cstart);
+            Chunk c;
+            issue_any<TINY>(p, cstart, valid && zr < kChunkBytes, c);
+            uint32_t v = chunk_value<TINY>(lds, c, valid ? zr : kChunkBytes, valid ? inv_start(lds, zr) : 0u,
+                                           base0, base1);
+            v = lane_shift(lds, v, lanebase);
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // half_mirror
+            const uint32_t fixed = uniform_shift<kLdsM768>(lds, v, 0u);
+            v = (j >= 8) ? fixed : v;
+            if (valid && c8 == 7) p.out[w0 + (uint32_t)src] = Lg ? ~v : 0u;
+        }
+
+        // ---- big frames: 16 lanes each, 4 per item, segment by segment ----
+        for (uint32_t t = 0; t < nb; t += 4) {
+            const uint32_t rank = t + (uint32_t)(lane >> 4);
+            const bool valid = rank < nb;
+            const int src = valid ? (int)lists[64 + rank] : 0;
+            const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+            const uint32_t Lq = (uint32_t)__shfl((int)L, src);
+            const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
+            uint32_t s = 0;
+            for (uint32_t k = 0; __any(k < m); k++) {
+                const bool on = k < m;
+                const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - k) -
+                                       (int64_t)kChunkBytes * (j + 1);
+                const int zr = (on && k == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
+                Chunk c;
+                issue_any<TINY>(p, cstart, on && zr < kChunkBytes, c);
+                const uint32_t r = chunk_value<TINY>(lds, c, zr, (on && k == 0) ? inv_start(lds, zr) : 0u,
+                                                     base0, base1);
+                s = on ? (k == 0 ? r : uniform_shift<kLdsJump>(lds, s, r)) : s;
+            }
+            uint32_t v = lane_shift(lds, s, lanebase);
+            v = row_xor(v);
+            if (valid && j == 15) p.out[w0 + (uint32_t)src] = Lq ? ~v : 0u;
+        }
+    }
 }
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
@@ -489,14 +799,24 @@ hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st) {
 #define FCS_LAUNCH(V, T, S) \
     hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kWgThreads), 0, st, p)
     if (var) {
+#ifdef FCS_OLD_VAR   // measurement-only build: the frame-per-quarter variable-length kernel
         if (tiny) FCS_LAUNCH(true, true, false);
         else FCS_LAUNCH(true, false, false);
+#else
+        if (tiny) hipLaunchKernelGGL((fcs_var_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
+        else hipLaunchKernelGGL((fcs_var_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+#endif
     } else if (tiny) {
         if (single) FCS_LAUNCH(false, true, true);
         else FCS_LAUNCH(false, true, false);
+    } else if (single) {
+#ifdef FCS_OLD_SINGLE   // measurement-only build: generic kernel's SINGLE instantiation
+        FCS_LAUNCH(false, false, true);
+#else
+        hipLaunchKernelGGL(fcs_single_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
+#endif
     } else {
-        if (single) FCS_LAUNCH(false, false, true);
-        else FCS_LAUNCH(false, false, false);
+        FCS_LAUNCH(false, false, false);
     }
 #undef FCS_LAUNCH
     return hipGetLastError();

@@ -15,6 +15,8 @@
 //                                                     (A_24(c)^d))
 //   front init    INV[z] = A_z^{-1}(0xFFFFFFFF)      (register value that, after z leading
 //                                                     zero bytes, equals the all-ones init)
+//   half-row fix  M   = A_{-768}                     (8-lane groups in lanes 8..15 of a row
+//                                                     used the lane tables of lanes 8..15)
 // These are constants of the algorithm, computed once per process; no frame bytes are ever
 // checksummed on the host (the product has no CPU CRC path).
 #pragma once
@@ -42,7 +44,10 @@ constexpr uint32_t kLdsJump = 147456;   // 8 x 16 x 4 B = 512 (A_1536)
 constexpr uint32_t kLdsH48 = 147968;    // 8 x 16 x 4 B = 512 (A_48)
 constexpr uint32_t kLdsH24 = 148480;    // 8 x 16 x 4 B = 512 (A_24)
 constexpr uint32_t kLdsInv = 148992;    // 96 x 4 B = 384
-constexpr uint32_t kLdsBytes = 149376;
+constexpr uint32_t kLdsM768 = 149376;   // 8 x 16 x 4 B = 512 (A_{-768})
+constexpr uint32_t kLdsWave = 149888;   // per-wave scratch for the variable-length kernel
+constexpr uint32_t kLdsWaveBytes = 128; //   (two 64-entry frame lists per wave)
+constexpr uint32_t kLdsBytes = kLdsWave + 16 * kLdsWaveBytes;   // 151936
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
@@ -51,8 +56,10 @@ constexpr uint32_t kBlobJump = kBlobLane + 8 * 16 * 32; // uint32 [8][16]
 constexpr uint32_t kBlobH48 = kBlobJump + 8 * 16;       // uint32 [8][16]
 constexpr uint32_t kBlobH24 = kBlobH48 + 8 * 16;        // uint32 [8][16]
 constexpr uint32_t kBlobInv = kBlobH24 + 8 * 16;        // uint32 [96]
-constexpr uint32_t kBlobWords = kBlobInv + kChunkBytes;
+constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
+constexpr uint32_t kBlobWords = kBlobM768 + 8 * 16;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
+static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
 struct Tables {
     uint32_t T[4][256];
@@ -105,6 +112,9 @@ struct Tables {
         for (int t = 0; t < 8; t++)
             for (int e = 0; e < 16; e++) b[kBlobH24 + t * 16 + e] = nt[t][e];
         for (int z = 0; z < kChunkBytes; z++) b[kBlobInv + z] = shift(0xFFFFFFFFu, -(long)z);
+        nibble_table(-768, nt);
+        for (int t = 0; t < 8; t++)
+            for (int e = 0; e < 16; e++) b[kBlobM768 + t * 16 + e] = nt[t][e];
         return b;
     }
 };
