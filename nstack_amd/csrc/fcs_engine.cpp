@@ -151,6 +151,8 @@ int grid_for(const DevState *ds, uint64_t n) {
     return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ds->cus, want));
 }
 
+uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
+
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
                  uint32_t *out, hipStream_t st) {
     fcs::KParams p{};
@@ -164,6 +166,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.fseg = segments(len);
     p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
+    p.dbg = g_dbg;
     HIPTRY(fcs::launch_fcs(false, p, grid_for(ds, n), st), "launching fcs_kernel<fixed>");
     return 0;
 }
@@ -643,6 +646,11 @@ int fcs_read_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *str
     HIPTRY(fcs::launch_read_stream(p, bytes, sink, (hipStream_t)stream), "launching read stream");
     return 0;
 }
+
+#ifdef FCS_STAMPS
+// Diagnostic stamp sink for FCS_STAMPS measurement builds (tools/stamps.py); not in product builds.
+extern "C" int fcs_debug_set_sink(void *p) { g_dbg = (uint64_t *)p; return 0; }
+#endif
 
 int fcs_timed_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n, uint32_t *out,
                         void *stream, int reps, float *ms_per_launch) {

@@ -424,7 +424,12 @@ struct Raw {
     uint32_t x6;
 };
 
+__device__ __forceinline__ uint64_t stamp() {
+    return __builtin_amdgcn_s_memtime();
+}
+
 struct SingleLane {
+    uint64_t *dbg;
     const uint8_t *lds;
     int j;
     uint32_t base0, base1, lanebase, x0, zmax;
@@ -443,21 +448,50 @@ struct SingleLane {
         }
         d[kChunkWords] = c.x6;
         if (EDGE && __any(dlead)) shift_up(d, dlead);
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts0 = stamp();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         uint32_t w[kChunkWords];
 #pragma unroll
         for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
 #pragma unroll
         for (int i = 0; i < kSingleMaskWords; i++)
             if (4 * i < (int)zmax) w[i] &= m[i];
+#ifdef FCS_SINGLE_ONE_CHAIN   // one 24-word chain: no A_48 merge (8 fewer LDS reads per item)
+        uint32_t xa = x0 ^ w[0];
+#pragma unroll
+        for (int i = 0; i < 24; i++) xa = step4(lds, xa, i < 23 ? w[i + 1] : 0u, base0, base1);
+        uint32_t v = lane_shift(lds, xa, lanebase);
+#else
         uint32_t xa = x0 ^ w[0], xb = w[12];
 #pragma unroll
         for (int i = 0; i < 12; i++) {
             xa = step4(lds, xa, i < 11 ? w[i + 1] : 0u, base0, base1);
             xb = step4(lds, xb, i < 11 ? w[13 + i] : 0u, base0, base1);
         }
+#ifdef FCS_STAMPS
+        asm volatile("" ::"v"(xa), "v"(xb));
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts1 = stamp();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         uint32_t v = lane_shift(lds, uniform_shift<kLdsH48>(lds, xa, xb), lanebase);
+#endif
         v = row_xor(v);
         if (act && j == 15) *outp = ~v;
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts2 = stamp();
+        if (dbg != nullptr && (threadIdx.x & 63) == 0) {
+            const uint32_t wv = blockIdx.x * (kWgThreads / 64) + (threadIdx.x >> 6);
+            atomicAdd((unsigned long long *)&dbg[wv * 4 + 0], (unsigned long long)(ts1 - ts0));
+            atomicAdd((unsigned long long *)&dbg[wv * 4 + 1], (unsigned long long)(ts2 - ts0));
+            atomicAdd((unsigned long long *)&dbg[wv * 4 + 2], 1ull);
+            atomicAdd((unsigned long long *)&dbg[wv * 4 + 3], (unsigned long long)ts2);
+        }
+#endif
     }
 };
 
@@ -475,6 +509,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
     SingleLane S;
+    S.dbg = p.dbg;
     S.lds = lds;
     S.j = j;
     S.base0 = r4;

@@ -17,6 +17,7 @@ struct KParams {
     uint32_t fseg;          // fixed: segments per frame
     uint32_t zmax;          // max leading zero bytes any front lane can see (mask loop bound)
     const uint32_t *blob;   // constant tables (kBlobWords)
+    uint64_t *dbg;          // diagnostic stamp sink (FCS_STAMPS builds only; null otherwise)
 };
 
 constexpr int kWgThreads = 1024;

@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--len", type=int, default=1518)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--imix", action="store_true",
+                    help="variable-length path: --frames IMIX frames (7:4:1 of 64/576/1518, shuffled)")
     a = ap.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -31,11 +33,23 @@ def main():
         lib = ctypes.CDLL(os.path.abspath(p))
         lib.ether_fcs_fixed_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint64,
                                             ctypes.c_void_p, ctypes.c_void_p]
+        lib.ether_fcs_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         lib.fcs_fill_splitmix64_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_void_p]
         libs.append(lib)
-    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
-    libs[0].fcs_fill_splitmix64_dev(arena.data_ptr(), n * L, 11, 0, None)
+    if a.imix:
+        import numpy as np
+        rng = np.random.default_rng(7)
+        ln_np = rng.choice(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.uint32), n)
+        ln = torch.from_numpy(ln_np.view(np.int32)).to(dev)
+        off = torch.zeros(n, dtype=torch.int64, device=dev)
+        off[1:] = torch.cumsum(ln[:-1].to(torch.int64), 0)
+        total = int(off[-1].item()) + int(ln_np[-1])
+    else:
+        total = n * L
+    arena = torch.empty(total, dtype=torch.uint8, device=dev)
+    libs[0].fcs_fill_splitmix64_dev(arena.data_ptr(), total, 11, 0, None)
     outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
     st = torch.cuda.current_stream()
     times = [[] for _ in libs]
@@ -44,7 +58,11 @@ def main():
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record(st)
             for _ in range(a.reps):
-                rc = lib.ether_fcs_fixed_dev(arena.data_ptr(), L, L, n, outs[i].data_ptr(), st.cuda_stream)
+                if a.imix:
+                    rc = lib.ether_fcs_batch_dev(arena.data_ptr(), total, off.data_ptr(), ln.data_ptr(),
+                                                 outs[i].data_ptr(), n, st.cuda_stream)
+                else:
+                    rc = lib.ether_fcs_fixed_dev(arena.data_ptr(), L, L, n, outs[i].data_ptr(), st.cuda_stream)
                 assert rc == 0, rc
             e1.record(st)
             torch.cuda.synchronize()
@@ -54,7 +72,7 @@ def main():
         med, mn = statistics.median(times[i]), min(times[i])
         same = bool(torch.equal(outs[i], outs[0]))
         print(f"{os.path.basename(p):28s} median {med:8.3f} ms  min {mn:8.3f} ms  "
-              f"{n * L / med / 1e6:8.1f} GB/s  same_as_first={same}")
+              f"{total / med / 1e6:8.1f} GB/s  same_as_first={same}")
 
 
 if __name__ == "__main__":
