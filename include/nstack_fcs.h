@@ -52,7 +52,7 @@ int fcs_engine_init(int ndev);
 void fcs_engine_fini(void);
 int fcs_engine_device_count(void);
 const char *fcs_last_error(void);
-/* Engine/kernel description string, e.g. "fcs-hip gfx950 slice4-lds32 chunk48 group32". */
+/* Engine/kernel description string (kernel geometry and table layout). */
 const char *fcs_engine_version(void);
 
 /* ---- device-resident batches (pointers in HBM of the current device) ---- */
@@ -74,6 +74,21 @@ int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64
  * first len[i] bytes is written little-endian at base[i*stride + len[i] .. +4). Requires
  * len[i] + 4 <= stride. Frames are modified in place in host memory. */
 int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n);
+
+/* ---- RX verification (new behaviour: the reference's ether_receive,
+ *      src/linux/ether.c:180-212, checks no FCS) ----
+ * Frames here INCLUDE their 4-byte FCS trailer (len[i] = covered bytes + 4). A frame checks iff
+ * ether_fcs(frame, len) == 0x2144DF1C, the CRC-32 residue, which holds exactly when the trailer
+ * is the little-endian FCS of the bytes before it, as ether_send (src/linux/ether.c:262-263)
+ * writes it. ok[i] = 1 / 0; frames shorter than 4 bytes never check.
+ * Device forms: ok[] and *bad (u64) are device memory; *bad is zeroed on the stream, then set to
+ * the number of failing frames. Host form: returns that number (>= 0) or -errno. */
+int ether_fcs_verify_dev(const void *arena, uint64_t arena_bytes, const uint64_t *off,
+                         const uint32_t *len, uint8_t *ok, uint64_t *bad, uint64_t n, void *stream);
+int ether_fcs_verify_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                               uint8_t *ok, uint64_t *bad, void *stream);
+int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
+                              const uint32_t *len, uint8_t *ok, uint64_t n);
 
 /* ---- pinned host memory for zero-copy-staging callers (optional) ---- */
 void *fcs_host_alloc(uint64_t bytes);

@@ -16,14 +16,15 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fcs.so")
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
-           "batch_host", "tx_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
+           "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
            "tables_blob", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
     "fcs_last_error", "fcs_engine_version", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
-    "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "fcs_host_alloc",
+    "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_verify_dev",
+    "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
     "fcs_tables_blob",
 ]
@@ -61,6 +62,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "ether_fcs_batch_host": (i32, [vp, u64, vp, vp, vp, u64]),
         "ether_fcs_fixed_host": (i32, [vp, u64, u32, u64, vp]),
         "ether_fcs_tx_host": (i32, [vp, u64, vp, u64]),
+        "ether_fcs_verify_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
+        "ether_fcs_verify_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, vp]),
+        "ether_fcs_verify_host": (c.c_int64, [vp, u64, vp, vp, vp, u64]),
         "fcs_host_alloc": (vp, [u64]),
         "fcs_host_free": (None, [vp]),
         "fcs_fill_splitmix64_dev": (i32, [vp, u64, u64, u64, vp]),
@@ -154,6 +158,23 @@ def batch_host(arena, arena_bytes: int, off, length, out, n: int) -> None:
 
 def tx_host(base, stride: int, length, n: int) -> None:
     _check(load().ether_fcs_tx_host(_ptr(base), stride, _ptr(length), n), "ether_fcs_tx_host")
+
+
+def verify_dev(arena, arena_bytes: int, off, length, ok, bad, n: int, stream=None) -> None:
+    """RX check of frames that carry their FCS trailer: ok[i] (u8), *bad (u64) on the device."""
+    _check(load().ether_fcs_verify_dev(_ptr(arena), arena_bytes, _ptr(off), _ptr(length), _ptr(ok),
+                                       _ptr(bad), n, _stream(stream)), "ether_fcs_verify_dev")
+
+
+def verify_fixed_dev(base, stride: int, length: int, n: int, ok, bad, stream=None) -> None:
+    _check(load().ether_fcs_verify_fixed_dev(_ptr(base), stride, length, n, _ptr(ok), _ptr(bad),
+                                             _stream(stream)), "ether_fcs_verify_fixed_dev")
+
+
+def verify_host(arena, arena_bytes: int, off, length, ok, n: int) -> int:
+    """Host form: fills ok[i] and returns the number of frames that fail the check."""
+    return _check(load().ether_fcs_verify_host(_ptr(arena), arena_bytes, _ptr(off), _ptr(length),
+                                               _ptr(ok), n), "ether_fcs_verify_host")
 
 
 def fill_splitmix_dev(ptr, nbytes: int, seed: int, byte_offset: int = 0, stream=None) -> None:

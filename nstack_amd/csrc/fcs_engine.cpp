@@ -154,8 +154,10 @@ int grid_for(const DevState *ds, uint64_t n) {
 uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
 
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
-                 uint32_t *out, hipStream_t st) {
+                 uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
     fcs::KParams p{};
+    p.ok = ok;
+    p.bad = bad;
     p.base = (uint64_t)base;
     p.stride = stride;
     p.out = out;
@@ -172,8 +174,11 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
 }
 
 int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint64_t *off,
-               const uint32_t *len, uint32_t *out, uint64_t n, hipStream_t st) {
+               const uint32_t *len, uint32_t *out, uint64_t n, hipStream_t st, uint8_t *ok = nullptr,
+               unsigned long long *bad = nullptr) {
     fcs::KParams p{};
+    p.ok = ok;
+    p.bad = bad;
     p.base = (uint64_t)arena;
     p.off = off;
     p.len = len;
@@ -253,7 +258,11 @@ struct HostJob {
     uint32_t *out;                 // crc per frame (nullptr in TX mode)
     uint8_t *tx_base;              // TX: write FCS after each frame
     uint64_t i0, i1;
+    uint8_t *ok;                   // verify: ok[i] = frame i (FCS trailer included) checks
+    std::atomic<uint64_t> *bad;    //   ... count of frames that do not
 };
+
+constexpr uint32_t kResidue = 0x2144DF1Cu;   // ether_fcs(frame || LE32(ether_fcs(frame)))
 
 constexpr uint64_t kChunkBytesHost = 128ull << 20;   // per pipeline slot
 constexpr uint64_t kChunkFramesMax = 1ull << 20;
@@ -276,6 +285,10 @@ int run_host_job(DevState *ds, const HostJob &job) {
             const uint64_t i = pend[b].i0 + q;
             const uint32_t c = pp.h_out[b][q];
             if (job.out) job.out[i] = c;
+            if (job.ok) {
+                job.ok[i] = c == kResidue;
+                if (c != kResidue) job.bad->fetch_add(1, std::memory_order_relaxed);
+            }
             if (job.tx_base) {   // src/linux/ether.c:263 — memcpy of the host-order u32
                 uint8_t *dst = job.tx_base + i * job.stride + job.len[i];
                 std::memcpy(dst, &c, 4);
@@ -542,7 +555,7 @@ int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t
         if (off[i] > arena_bytes || len[i] > arena_bytes - off[i])
             return fail(EINVAL, "frame %llu [%llu, +%u) outside the %llu-byte arena", (unsigned long long)i,
                         (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
-    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, out, nullptr, 0, n};
+    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, out, nullptr, 0, n, nullptr, nullptr};
     return run_host_sharded(job, n);
 }
 
@@ -552,7 +565,7 @@ int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64
     if (!base || !out) return fail(EINVAL, "null pointer");
     if (n > 1 && stride < len) return fail(EINVAL, "stride %llu < len %u", (unsigned long long)stride, len);
     HostJob job{(const uint8_t *)base, (n - 1) * stride + len, nullptr, nullptr, n > 1 ? stride : len, len,
-                out, nullptr, 0, n};
+                out, nullptr, 0, n, nullptr, nullptr};
     return run_host_sharded(job, n);
 }
 
@@ -563,8 +576,50 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
         if ((uint64_t)len[i] + 4 > stride)
             return fail(EINVAL, "frame %llu: len %u + FCS does not fit stride %llu", (unsigned long long)i,
                         len[i], (unsigned long long)stride);
-    HostJob job{(const uint8_t *)base, n * stride, nullptr, len, stride, 0, nullptr, (uint8_t *)base, 0, n};
+    HostJob job{(const uint8_t *)base, n * stride, nullptr, len, stride, 0, nullptr, (uint8_t *)base, 0, n,
+                nullptr, nullptr};
     return run_host_sharded(job, n);
+}
+
+// ---- RX verification: frames that carry their FCS trailer ----
+int ether_fcs_verify_dev(const void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
+                         uint8_t *ok, uint64_t *bad, uint64_t n, void *stream) {
+    if (!bad) return fail(EINVAL, "null pointer");
+    HIPTRY(hipMemsetAsync(bad, 0, 8, (hipStream_t)stream), "zeroing bad count");
+    if (n == 0) return 0;
+    if (!arena || !off || !len || !ok) return fail(EINVAL, "null pointer");
+    DevState *ds = nullptr;
+    int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    return launch_var(ds, arena, arena_bytes, off, len, nullptr, n, (hipStream_t)stream, ok,
+                      (unsigned long long *)bad);
+}
+
+int ether_fcs_verify_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n, uint8_t *ok,
+                               uint64_t *bad, void *stream) {
+    if (!bad) return fail(EINVAL, "null pointer");
+    HIPTRY(hipMemsetAsync(bad, 0, 8, (hipStream_t)stream), "zeroing bad count");
+    if (n == 0) return 0;
+    if (!base || !ok) return fail(EINVAL, "null pointer");
+    if (n > 1 && stride < len) return fail(EINVAL, "stride %llu < len %u", (unsigned long long)stride, len);
+    DevState *ds = nullptr;
+    int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    return launch_fixed(ds, base, stride, len, n, nullptr, (hipStream_t)stream, ok, (unsigned long long *)bad);
+}
+
+int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
+                              uint8_t *ok, uint64_t n) {
+    if (n == 0) return 0;
+    if (!arena || !off || !len || !ok) return fail(EINVAL, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i] > arena_bytes || len[i] > arena_bytes - off[i])
+            return fail(EINVAL, "frame %llu [%llu, +%u) outside the %llu-byte arena", (unsigned long long)i,
+                        (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    std::atomic<uint64_t> bad{0};
+    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, nullptr, nullptr, 0, n, ok, &bad};
+    const int rc = run_host_sharded(job, n);
+    return rc ? rc : (int64_t)bad.load();
 }
 
 // Drop-in for src/ether_fcs.c:4. Synchronous, reentrant (per-device lock around the staging).

@@ -141,6 +141,24 @@ __device__ __forceinline__ Item frame_item(const KParams &p, uint64_t f) {
 // read lo4; a window that starts before lo4 (front lane of a frame at the very start of the
 // arena) is moved up to lo4 in a wave-uniform branch and shifted back after the data has landed
 // (process()).
+// CRC residue: ether_fcs(frame || LE32(ether_fcs(frame))) for every frame.
+constexpr uint32_t kResidue = 0x2144DF1Cu;
+
+// Result store for one frame per lane with st set; called by the whole wave (convergent).
+// FCS mode: out[i] = FCS. Verify mode (ok != null; frames carry their FCS trailer): ok[i] = 1 iff
+// the FCS over the whole frame equals the residue; non-matching frames are counted into *bad with
+// one atomic per wave. Both may be requested together.
+__device__ __forceinline__ void emit(uint32_t *out, uint8_t *ok, unsigned long long *bad, bool st, uint64_t i,
+                                     uint32_t fcs) {
+    if (out != nullptr && st) out[i] = fcs;
+    if (ok != nullptr) {
+        const bool good = fcs == kResidue;
+        if (st) ok[i] = good ? 1 : 0;
+        const uint64_t m = __ballot(st && !good);
+        if (m != 0 && (threadIdx.x & 63) == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
+    }
+}
+
 struct Chunk {
     u32x4a4 x[6];
     uint32_t x6;
@@ -328,7 +346,7 @@ struct Lane {
         if (__any(last)) {
             uint32_t v = last ? lane_shift(lds, s, lanebase) : 0u;
             v = row_xor(v);
-            if (last && j == 15) p.out[c.f] = c.it.len ? ~v : 0u;
+            emit(p.out, p.ok, p.bad, last && j == 15, c.f, c.it.len ? ~v : 0u);
         }
     }
 };
@@ -430,14 +448,16 @@ __device__ __forceinline__ uint64_t stamp() {
 
 struct SingleLane {
     uint64_t *dbg;
+    uint32_t *out;
+    uint8_t *ok;
+    unsigned long long *bad;
     const uint8_t *lds;
     int j;
     uint32_t base0, base1, lanebase, x0, zmax;
     uint32_t m[kSingleMaskWords];
 
     template <bool EDGE>
-    __device__ __forceinline__ void process(const Raw &c, uint32_t r, int dlead, bool act,
-                                            uint32_t *outp) const {
+    __device__ __forceinline__ void process(const Raw &c, uint32_t r, int dlead, bool act, uint64_t fi) const {
         uint32_t d[kChunkWords + 1];
 #pragma unroll
         for (int q = 0; q < 6; q++) {
@@ -480,7 +500,7 @@ struct SingleLane {
         uint32_t v = lane_shift(lds, uniform_shift<kLdsH48>(lds, xa, xb), lanebase);
 #endif
         v = row_xor(v);
-        if (act && j == 15) *outp = ~v;
+        emit(out, ok, bad, act && j == 15, fi, ~v);
 #ifdef FCS_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts2 = stamp();
@@ -510,6 +530,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
     SingleLane S;
     S.dbg = p.dbg;
+    S.out = p.out;
+    S.ok = p.ok;
+    S.bad = p.bad;
     S.lds = lds;
     S.j = j;
     S.base0 = r4;
@@ -535,7 +558,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
     int rem = f0 < p.n ? (int)((p.n - 1 - f0) / Q) + 1 : 0;   // items left for this frame slot
     uint64_t end = p.base + f0 * p.stride + p.flen;
     const uint64_t dend = Q * p.stride;
-    uint32_t *outp = p.out + f0;
+    uint64_t fi = f0;   // frame index of the item being processed
 
     // ---- first item: the only one that can start before the arena (frame 0's front lane) ----
     Raw A, B;
@@ -555,28 +578,28 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
     uint64_t endB = end + dend;
     uint32_t rB = (uint32_t)endB & 3u;
     issue_raw(rem > 1 ? ((endB - loff) & ~3ull) : p.lo4, rB, B);
-    S.process<true>(A, rA, dlead, rem > 0, outp);
+    S.process<true>(A, rA, dlead, rem > 0, fi);
     rem -= 1;
     end = endB;
-    outp += Q;
+    fi += Q;
 
     // ---- steady state: two items in flight per lane ----
     while (__any(rem > 0)) {
         const uint64_t endA = end + dend;
         rA = (uint32_t)endA & 3u;
         issue_raw(rem > 1 ? ((endA - loff) & ~3ull) : p.lo4, rA, A);
-        S.process<false>(B, rB, 0, rem > 0, outp);
+        S.process<false>(B, rB, 0, rem > 0, fi);
         rem -= 1;
         end = endA;
-        outp += Q;
+        fi += Q;
         if (!__any(rem > 0)) break;
         endB = end + dend;
         rB = (uint32_t)endB & 3u;
         issue_raw(rem > 1 ? ((endB - loff) & ~3ull) : p.lo4, rB, B);
-        S.process<false>(A, rA, 0, rem > 0, outp);
+        S.process<false>(A, rA, 0, rem > 0, fi);
         rem -= 1;
         end = endB;
-        outp += Q;
+        fi += Q;
     }
 }
 
@@ -701,7 +724,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
             Chunk c;
             issue_any<TINY>(p, (int64_t)E - kChunkBytes, small && L > 0, c);
             const uint32_t v = chunk_value<TINY>(lds, c, zr, small ? inv_start(lds, zr) : 0u, base0, base1);
-            if (small) p.out[f] = L ? ~v : 0u;
+            emit(p.out, p.ok, p.bad, small, f, L ? ~v : 0u);
         }
 
         // ---- medium frames: 8 lanes each, 8 per item ----
@@ -724,7 +747,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // half_mirror
             const uint32_t fixed = uniform_shift<kLdsM768>(lds, v, 0u);
             v = (j >= 8) ? fixed : v;
-            if (valid && c8 == 7) p.out[w0 + (uint32_t)src] = Lg ? ~v : 0u;
+            emit(p.out, p.ok, p.bad, valid && c8 == 7, w0 + (uint32_t)src, Lg ? ~v : 0u);
         }
 
         // ---- big frames: 16 lanes each, 4 per item, segment by segment ----
@@ -749,7 +772,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
             }
             uint32_t v = lane_shift(lds, s, lanebase);
             v = row_xor(v);
-            if (valid && j == 15) p.out[w0 + (uint32_t)src] = Lq ? ~v : 0u;
+            emit(p.out, p.ok, p.bad, valid && j == 15, w0 + (uint32_t)src, Lq ? ~v : 0u);
         }
     }
 }

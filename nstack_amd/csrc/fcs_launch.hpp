@@ -18,6 +18,8 @@ struct KParams {
     uint32_t zmax;          // max leading zero bytes any front lane can see (mask loop bound)
     const uint32_t *blob;   // constant tables (kBlobWords)
     uint64_t *dbg;          // diagnostic stamp sink (FCS_STAMPS builds only; null otherwise)
+    uint8_t *ok;            // verify mode: ok[i] = 1 iff frame i (FCS trailer included) checks
+    unsigned long long *bad;//   ... and *bad += number of frames that do not (else both null)
 };
 
 constexpr int kWgThreads = 1024;

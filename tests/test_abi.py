@@ -65,6 +65,15 @@ def test_fails_loudly_without_gpu():
     with pytest.raises(na.FcsError):
         na.engine_init(0)
     assert lib.ether_fcs_fixed_dev(None, 1518, 1518, 1, None, None) == -22  # -EINVAL first
+    # RX verification has no CPU path either
+    import numpy as np
+    arena = np.zeros(128, dtype=np.uint8)
+    off = np.zeros(1, dtype=np.uint64)
+    ln = np.full(1, 74, dtype=np.uint32)
+    ok = np.zeros(1, dtype=np.uint8)
+    assert lib.ether_fcs_verify_host(arena.ctypes.data, 128, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, 1) == -19
+    with pytest.raises(na.FcsError):
+        na.verify_host(arena, 128, off, ln, ok, 1)
 
 
 @pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")

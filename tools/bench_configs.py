@@ -78,7 +78,16 @@ def main():
         bad = spot_check(o, lambda i: arena[i * L:(i + 1) * L].cpu().numpy(), crcs, idx)
         res["fixed_64M_x_1518"] = {"ms": ms, "GiB_s": n * L / ms / 1e-3 / GIB, "GB_s": n * L / ms / 1e6,
                                    "Mframes_s": n / ms / 1e3, "spot_bad": bad}
-        del arena, out
+        # RX verify mode over the same frames (random trailers: essentially every frame fails,
+        # the worst case for the bad-frame counter)
+        ok = torch.empty(n, dtype=torch.uint8, device=dev)
+        nbad = torch.zeros(1, dtype=torch.int64, device=dev)
+        ms_v = time_dev(lambda: na.verify_fixed_dev(arena, L, L, n, ok, nbad, torch.cuda.current_stream()),
+                        a.reps, torch)
+        res["verify_fixed_64M_x_1518"] = {"ms": ms_v, "GB_s": n * L / ms_v / 1e6, "bad": int(nbad.item()),
+                                          "expected_bad": int((torch.from_numpy(crcs.view(np.int32)) !=
+                                                               0x2144DF1C).sum())}
+        del arena, out, ok
         torch.cuda.empty_cache()
 
     # ---------------- IMIX 128 M frames ----------------
