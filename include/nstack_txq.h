@@ -1,0 +1,75 @@
+/*
+ * nstack_txq.h — batched TX call site for nstack's ether_send.
+ *
+ * Reference: ether_send(handle, dst, proto, buf, bsize), /root/reference/src/linux/ether.c:214-272,
+ * builds one frame in a stack VLA, computes its FCS with ether_fcs (:262), stores it
+ * little-endian after the covered bytes (:263) and calls sendto once per frame (:265). Its
+ * callers (ether_output_reply, src/ether.c:39-53; ip_send, arp) run on the main, ingress,
+ * egress and TCP-timer threads concurrently.
+ *
+ * fcs_txq_send() keeps that contract per call — same frame bytes, same return value (bytes sent
+ * or -errno), same -EMSGSIZE rule — but frames from all producer threads are assembled into one
+ * pinned batch arena, their FCSs are computed together on the GPU (ether_fcs_tx_host), and the
+ * batch leaves through one sink call (sendmmsg for the provided sinks). A batch is flushed when it
+ * holds max_batch frames, or the flusher is idle and the batch's oldest frame has lingered
+ * flush_usec microseconds (0: leave as soon as the flusher is free). The queue double-buffers:
+ * producers fill batch k+1 while batch k is on the GPU/wire, so batches grow with the offered
+ * load by themselves and a linger is only worth it for fire-and-forget senders.
+ * fcs_txq_send() blocks until its own frame has been handed to the sink and returns that frame's
+ * result. If the GPU step fails, every frame of that batch returns its -errno and none is sent:
+ * no frame ever leaves with an FCS that was not computed by the engine.
+ */
+#ifndef NSTACK_TXQ_H
+#define NSTACK_TXQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct fcs_txq fcs_txq_t;
+
+/* Transmit n finished frames (header + payload + pad + FCS; sizes[i] bytes at frames[i]).
+ * Must store each frame's result in res[i]: bytes sent, or -errno (as sendto's result at
+ * src/linux/ether.c:265-269). Called from the queue's flusher thread, one batch at a time. */
+typedef void (*fcs_txq_sink_fn)(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res,
+                                uint32_t n);
+
+/* src_mac: the interface MAC ether_send copies into h_src (eth->el_mac, :258).
+ * max_batch: frames per batch (1 .. 65536); flush_usec: linger of a non-full batch (see above). */
+fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t flush_usec,
+                          fcs_txq_sink_fn sink, void *sink_ctx);
+/* ether_send semantics: returns frame_size = 14 + max(bsize, 56) + 4 on success, -EMSGSIZE when
+ * that exceeds 1518 (checked before anything is queued, :234-237), or the sink's / engine's
+ * -errno. Thread-safe; blocks until the frame's batch has been sent. */
+int fcs_txq_send(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize);
+/* Fire-and-forget form: returns frame_size once the frame is queued (or -EMSGSIZE / -EINVAL);
+ * its send result only feeds the error counter of fcs_txq_stats. */
+int fcs_txq_send_async(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf,
+                       size_t bsize);
+/* Flush whatever is queued now and wait for it. Returns 0 or -errno (bad queue). */
+int fcs_txq_flush(fcs_txq_t *q);
+/* Flushes, stops the flusher thread and frees the queue. */
+void fcs_txq_destroy(fcs_txq_t *q);
+/* Counters since creation: frames handed to the sink (or failed by the engine), batches, and
+ * frames whose result was not frame_size (send or engine errors). Any pointer may be NULL. */
+void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint64_t *errors);
+
+/* ---- provided sinks ---- */
+/* ctx = pointer to an int file descriptor of a CONNECTED socket (e.g. a socketpair or a
+ * connected AF_PACKET/UDP socket): one sendmmsg per batch, no per-message address. */
+void fcs_txq_sink_fd(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res, uint32_t n);
+/* AF_PACKET raw socket, as ether_send uses it (:241-253): ctx = struct fcs_txq_packet_ctx*.
+ * Each frame's sockaddr_ll takes sll_protocol and sll_addr from the frame's own header. */
+struct fcs_txq_packet_ctx {
+    int fd;
+    int ifindex;
+};
+void fcs_txq_sink_packet(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res, uint32_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* NSTACK_TXQ_H */

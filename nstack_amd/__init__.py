@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -27,6 +27,9 @@ EXPORTS = [
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
     "fcs_tables_blob",
+    # include/nstack_txq.h — batched TX call site
+    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats",
+    "fcs_txq_sink_fd", "fcs_txq_sink_packet",
 ]
 
 
@@ -71,6 +74,14 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_read_stream_dev": (i32, [vp, u64, vp, vp]),
         "fcs_timed_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, i32, c.POINTER(c.c_float)]),
         "fcs_tables_blob": (i32, [vp, u64]),
+        "fcs_txq_create": (vp, [vp, u32, u32, vp, vp]),
+        "fcs_txq_send": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
+        "fcs_txq_flush": (i32, [vp]),
+        "fcs_txq_destroy": (None, [vp]),
+        "fcs_txq_send_async": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
+        "fcs_txq_stats": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
+        "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
+        "fcs_txq_sink_packet": (None, [vp, vp, vp, vp, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -199,3 +210,44 @@ def tables_blob():
     buf = np.zeros(8192, dtype=np.uint32)
     n = _check(load().fcs_tables_blob(buf.ctypes.data, buf.size), "fcs_tables_blob")
     return buf[:n].copy()
+
+
+class TxQueue:
+    """Batched ether_send (include/nstack_txq.h; src/linux/ether.c:214-272) over a connected
+    socket fd: send() has ether_send's return contract (frame_size or -errno); frames from all
+    threads are FCS'd together on the GPU and leave in one sendmmsg per batch."""
+
+    def __init__(self, src_mac: bytes, fd: int, max_batch: int = 256, flush_usec: int = 0):
+        L = load()
+        self._fd = ctypes.c_int(fd)
+        self._mac = (ctypes.c_uint8 * 6)(*src_mac)
+        sink = ctypes.cast(L.fcs_txq_sink_fd, ctypes.c_void_p)
+        self._q = L.fcs_txq_create(self._mac, max_batch, flush_usec, sink, ctypes.addressof(self._fd))
+        if not self._q:
+            raise FcsError(-errno.EINVAL, "fcs_txq_create")
+
+    def send(self, dst: bytes, proto: int, payload: bytes) -> int:
+        return load().fcs_txq_send(self._q, bytes(dst), proto, bytes(payload), len(payload))
+
+    def send_async(self, dst: bytes, proto: int, payload: bytes) -> int:
+        return load().fcs_txq_send_async(self._q, bytes(dst), proto, bytes(payload), len(payload))
+
+    def flush(self) -> None:
+        _check(load().fcs_txq_flush(self._q), "fcs_txq_flush")
+
+    def stats(self):
+        """(frames, batches, errors) since creation."""
+        f, b, e = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        load().fcs_txq_stats(self._q, ctypes.byref(f), ctypes.byref(b), ctypes.byref(e))
+        return int(f.value), int(b.value), int(e.value)
+
+    def close(self) -> None:
+        if self._q:
+            load().fcs_txq_destroy(self._q)
+            self._q = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()

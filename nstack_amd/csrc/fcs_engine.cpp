@@ -76,6 +76,10 @@ struct DevState {
     uint32_t *d_blob = nullptr;
     std::mutex pipe_mu;      // one host pipeline at a time per device
     Pipe pipe;
+    std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
+    hipStream_t tx_stream = nullptr;
+    uint32_t *tx_len = nullptr, *tx_out = nullptr;   // pinned, device-mapped
+    uint64_t tx_cap = 0;
     std::mutex one_mu;       // single-frame (drop-in ether_fcs) staging
     hipStream_t one_stream = nullptr;
     uint8_t *one_d = nullptr, *one_h = nullptr;
@@ -173,12 +177,14 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     return 0;
 }
 
+// off == nullptr: frame i starts at arena + i * stride (TX slots of variable covered length).
 int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint64_t *off,
                const uint32_t *len, uint32_t *out, uint64_t n, hipStream_t st, uint8_t *ok = nullptr,
-               unsigned long long *bad = nullptr) {
+               unsigned long long *bad = nullptr, uint64_t stride = 0) {
     fcs::KParams p{};
     p.ok = ok;
     p.bad = bad;
+    p.stride = stride;
     p.base = (uint64_t)arena;
     p.off = off;
     p.len = len;
@@ -384,6 +390,41 @@ int run_host_job(DevState *ds, const HostJob &job) {
     return 0;
 }
 
+// Small TX batches in pinned memory (the TX queue's arenas): no staging copies — the kernel reads
+// the frames and writes the FCSs through device-mapped pinned memory, one launch, one sync; the
+// host then stores each FCS little-endian after its covered bytes (src/linux/ether.c:263).
+constexpr uint64_t kZeroCopyMaxBytes = 8ull << 20;
+
+int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t stride, const uint32_t *len, uint64_t n) {
+    std::lock_guard<std::mutex> lk(ds->tx_mu);
+    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    if (!ds->tx_stream) HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (n > ds->tx_cap) {
+        if (ds->tx_len) hipHostFree(ds->tx_len);
+        if (ds->tx_out) hipHostFree(ds->tx_out);
+        ds->tx_len = ds->tx_out = nullptr;
+        ds->tx_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(n, 4096);
+        HIPTRY(hipHostMalloc(&ds->tx_len, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx len)");
+        HIPTRY(hipHostMalloc(&ds->tx_out, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx out)");
+        ds->tx_cap = cap;
+    }
+    std::memcpy(ds->tx_len, len, n * 4);
+    void *dbase = nullptr, *dlen = nullptr, *dout = nullptr;
+    if (hipHostGetDevicePointer(&dbase, base, 0) != hipSuccess) {   // pinned but not mapped
+        (void)hipGetLastError();
+        return 1;
+    }
+    HIPTRY(hipHostGetDevicePointer(&dlen, ds->tx_len, 0), "hipHostGetDevicePointer(len)");
+    HIPTRY(hipHostGetDevicePointer(&dout, ds->tx_out, 0), "hipHostGetDevicePointer(out)");
+    int rc = launch_var(ds, dbase, n * stride, nullptr, (const uint32_t *)dlen, (uint32_t *)dout, n, ds->tx_stream,
+                        nullptr, nullptr, stride);
+    if (rc) return rc;
+    HIPTRY(hipStreamSynchronize(ds->tx_stream), "hipStreamSynchronize(tx)");
+    for (uint64_t i = 0; i < n; i++) std::memcpy(base + i * stride + len[i], &ds->tx_out[i], 4);
+    return 0;
+}
+
 int engine_devices(std::vector<DevState *> *out) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -506,6 +547,9 @@ void fcs_engine_fini(void) {
             if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
         }
         if (pp.stream) hipStreamDestroy(pp.stream);
+        if (ds->tx_stream) hipStreamDestroy(ds->tx_stream);
+        if (ds->tx_len) hipHostFree(ds->tx_len);
+        if (ds->tx_out) hipHostFree(ds->tx_out);
         if (ds->one_stream) hipStreamDestroy(ds->one_stream);
         if (ds->one_d) hipFree(ds->one_d);
         if (ds->one_h) hipHostFree(ds->one_h);
@@ -576,6 +620,13 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
         if ((uint64_t)len[i] + 4 > stride)
             return fail(EINVAL, "frame %llu: len %u + FCS does not fit stride %llu", (unsigned long long)i,
                         len[i], (unsigned long long)stride);
+    if (n * stride <= kZeroCopyMaxBytes && is_pinned(base)) {
+        std::vector<DevState *> devs;
+        int rc = engine_devices(&devs);
+        if (rc) return rc;
+        rc = run_tx_zero_copy(devs[0], (uint8_t *)base, stride, len, n);
+        if (rc <= 0) return rc;   // 1: the frames are not device-mapped; take the staged pipeline
+    }
     HostJob job{(const uint8_t *)base, n * stride, nullptr, len, stride, 0, nullptr, (uint8_t *)base, 0, n,
                 nullptr, nullptr};
     return run_host_sharded(job, n);
@@ -678,7 +729,7 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
 
 void *fcs_host_alloc(uint64_t bytes) {
     void *p = nullptr;
-    if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess) {
+    if (hipHostMalloc(&p, bytes, hipHostMallocMapped | hipHostMallocPortable) != hipSuccess) {
         fail(ENOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
         return nullptr;
     }

@@ -125,7 +125,7 @@ __device__ __forceinline__ Item frame_item(const KParams &p, uint64_t f) {
     Item it;
     if (VAR) {
         const uint32_t L = p.len[f];
-        it.end = p.base + p.off[f] + L;
+        it.end = p.base + (p.off ? p.off[f] : f * p.stride) + L;
         it.len = L;
         it.m = L ? (L + (kSegBytes - 1)) / kSegBytes : 1u;
     } else {
@@ -706,7 +706,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
         const uint64_t f = w0 + lane;
         const bool act = f < p.n;
         const uint32_t L = act ? p.len[f] : 0u;
-        const uint64_t E = act ? p.base + p.off[f] + L : p.lo4;
+        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;   // off == null: slots of p.stride
         const bool small = act && L <= (uint32_t)kChunkBytes;
         const bool med = act && !small && L <= 8u * kChunkBytes;
         const bool big = act && L > 8u * kChunkBytes;

@@ -1,5 +1,6 @@
-"""The C-ABI boundary: the product library loads, exports exactly what include/nstack_fcs.h
-declares, and (without a GPU) refuses to compute instead of falling back to the CPU."""
+"""The C-ABI boundary: the product library loads, exports exactly what include/*.h declare
+(nstack_fcs.h: the FCS engine; nstack_txq.h: the batched TX call site), and (without a GPU)
+refuses to compute instead of falling back to the CPU."""
 import ctypes
 import os
 import re
@@ -11,12 +12,16 @@ import nstack_amd as na
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "nstack_fcs.h")
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("nstack_fcs.h", "nstack_txq.h")]
 
 
 def _declared():
-    src = open(HEADER).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src)) - {"defined"})
+    names = set()
+    for h in HEADERS:
+        src = open(h).read()
+        src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+        names |= set(re.findall(r"\b([a-z_][a-z0-9_]*)\s*\(", src))
+    return sorted(names - {"defined", "void"})
 
 
 def test_header_declares_python_exports():
