@@ -54,6 +54,10 @@ int fcs_engine_device_count(void);
 const char *fcs_last_error(void);
 /* Engine/kernel description string (kernel geometry and table layout). */
 const char *fcs_engine_version(void);
+/* Tuning: variable-length batches of at most `frames` frames use the latency-optimised kernel
+ * (one quarter-wave per frame), larger ones the throughput-optimised windowed kernel. Results are
+ * identical either way. Default 16384. Returns the previous value. */
+uint64_t fcs_engine_set_var_threshold(uint64_t frames);
 
 /* ---- device-resident batches (pointers in HBM of the current device) ---- */
 /* Variable-length frames: frame i = arena[off[i] .. off[i]+len[i]), all inside

@@ -56,6 +56,11 @@ void fcs_txq_destroy(fcs_txq_t *q);
 /* Counters since creation: frames handed to the sink (or failed by the engine), batches, and
  * frames whose result was not frame_size (send or engine errors). Any pointer may be NULL. */
 void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint64_t *errors);
+/* Flusher time since creation, in ns, summed over batches: waiting for producers to finish
+ * assembling, the GPU step (ether_fcs_tx_host), the sink, the whole per-batch busy time (their
+ * sum plus bookkeeping), and pickup (a batch's first frame queued -> the flusher closing it). */
+void fcs_txq_timing(const fcs_txq_t *q, uint64_t *ns_ready, uint64_t *ns_gpu, uint64_t *ns_sink,
+                    uint64_t *ns_busy, uint64_t *ns_pickup);
 
 /* ---- provided sinks ---- */
 /* ctx = pointer to an int file descriptor of a CONNECTED socket (e.g. a socketpair or a

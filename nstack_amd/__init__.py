@@ -17,18 +17,18 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "set_var_threshold", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
     "fcs_tables_blob",
     # include/nstack_txq.h — batched TX call site
-    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats",
+    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
 ]
 
@@ -60,6 +60,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_engine_device_count": (i32, []),
         "fcs_last_error": (c.c_char_p, []),
         "fcs_engine_version": (c.c_char_p, []),
+        "fcs_engine_set_var_threshold": (u64, [u64]),
         "ether_fcs_batch_dev": (i32, [vp, u64, vp, vp, vp, u64, vp]),
         "ether_fcs_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp]),
         "ether_fcs_batch_host": (i32, [vp, u64, vp, vp, vp, u64]),
@@ -80,6 +81,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_txq_destroy": (None, [vp]),
         "fcs_txq_send_async": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
         "fcs_txq_stats": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
+        "fcs_txq_timing": (None, [vp] + [c.POINTER(u64)] * 5),
         "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
         "fcs_txq_sink_packet": (None, [vp, vp, vp, vp, u32]),
     }
@@ -114,6 +116,11 @@ def version() -> str:
 
 def engine_init(ndev: int = 0) -> int:
     return _check(load().fcs_engine_init(ndev), "fcs_engine_init")
+
+
+def set_var_threshold(frames: int) -> int:
+    """Variable-length batches of <= frames use the quarter-wave kernel; returns the old value."""
+    return int(load().fcs_engine_set_var_threshold(frames))
 
 
 def engine_fini() -> None:

@@ -157,6 +157,11 @@ int grid_for(const DevState *ds, uint64_t n) {
 
 uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
 
+// Variable-length batches of at most this many frames take the quarter-wave-per-frame kernel
+// (every frame in flight at once: lowest latency); larger ones the windowed kernel (throughput).
+// 16384 = 4 frames x 16 waves x 256 CUs: one item per quarter-wave on a full chip.
+std::atomic<uint64_t> g_var_threshold{16384};
+
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
                  uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
     fcs::KParams p{};
@@ -173,7 +178,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
     p.dbg = g_dbg;
-    HIPTRY(fcs::launch_fcs(false, p, grid_for(ds, n), st), "launching fcs_kernel<fixed>");
+    HIPTRY(fcs::launch_fcs(false, false, p, grid_for(ds, n), st), "launching fcs_kernel<fixed>");
     return 0;
 }
 
@@ -194,7 +199,8 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     p.hi4 = ceil4((uint64_t)arena + arena_bytes);
     p.zmax = fcs::kChunkBytes;
     p.blob = ds->d_blob;
-    HIPTRY(fcs::launch_fcs(true, p, grid_for(ds, n), st), "launching fcs_kernel<var>");
+    const bool windowed = n > g_var_threshold.load(std::memory_order_relaxed);
+    HIPTRY(fcs::launch_fcs(true, windowed, p, grid_for(ds, n), st), "launching fcs_kernel<var>");
     return 0;
 }
 
@@ -560,6 +566,10 @@ void fcs_engine_fini(void) {
     g_dev.clear();
     g_engine_devs.clear();
     hipSetDevice(cur);
+}
+
+uint64_t fcs_engine_set_var_threshold(uint64_t frames) {
+    return g_var_threshold.exchange(frames);
 }
 
 int fcs_engine_device_count(void) {

@@ -847,7 +847,7 @@ __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t s
 }
 
 // ---- host-side launchers (the engine TU never names the kernels) ----
-hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st) {
+hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st) {
     const bool tiny = p.hi4 - p.lo4 < 2 * kChunkBytes;
 #ifdef FCS_NO_SINGLE   // measurement-only build
     const bool single = false;
@@ -857,13 +857,16 @@ hipError_t launch_fcs(bool var, const KParams &p, int grid, hipStream_t st) {
 #define FCS_LAUNCH(V, T, S) \
     hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kWgThreads), 0, st, p)
     if (var) {
-#ifdef FCS_OLD_VAR   // measurement-only build: the frame-per-quarter variable-length kernel
-        if (tiny) FCS_LAUNCH(true, true, false);
-        else FCS_LAUNCH(true, false, false);
-#else
-        if (tiny) hipLaunchKernelGGL((fcs_var_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
-        else hipLaunchKernelGGL((fcs_var_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
-#endif
+        // windowed: throughput form (64-frame windows per wave, length classes);
+        // otherwise one quarter-wave per frame, every frame in flight at once (small batches)
+        if (!windowed) {
+            if (tiny) FCS_LAUNCH(true, true, false);
+            else FCS_LAUNCH(true, false, false);
+        } else if (tiny) {
+            hipLaunchKernelGGL((fcs_var_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
+        } else {
+            hipLaunchKernelGGL((fcs_var_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+        }
     } else if (tiny) {
         if (single) FCS_LAUNCH(false, true, true);
         else FCS_LAUNCH(false, true, false);

@@ -34,8 +34,14 @@ using Clock = std::chrono::steady_clock;
 
 struct Waiter {
     int result = 0;
-    bool done = false;
+    std::atomic<bool> done{false};   // set last by the flusher; the producer may be spinning on it
 };
+
+// Hand-offs spin this long before sleeping on a condition variable: a futex wake-up costs tens of
+// microseconds, more than the GPU step of a small batch.
+constexpr auto kSpin = std::chrono::microseconds(50);
+
+inline void cpu_relax() { __builtin_ia32_pause(); }
 
 struct Batch {
     uint8_t *arena = nullptr;            // cap slots of kSlot bytes (pinned when possible)
@@ -67,6 +73,10 @@ struct fcs_txq {
     uint64_t flush_target = 0;            // flush() wants batches <= this closed now
     bool stop = false;
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
+    uint64_t ns_ready = 0, ns_gpu = 0, ns_sink = 0, ns_busy = 0;   // flusher time split
+    uint64_t ns_pickup = 0;               // first frame of a batch queued -> batch closed
+    std::atomic<uint32_t> queued{0};      // frames reserved in the open batch (mirror, for spinning)
+    std::atomic<bool> stop_req{false};    // mirror of stop for the spinning flusher
     std::thread th;
 };
 
@@ -78,13 +88,31 @@ void flusher(fcs_txq *q) {
         Batch *B = &q->b[q->open];
         for (;;) {
             if (B->reserved == q->cap || q->stop) break;
-            if (B->reserved > 0 && q->flush_target >= B->seq) break;
-            if (B->reserved == 0) {
-                q->cv_flusher.wait(lk);
-            } else if (q->cv_flusher.wait_until(lk, B->first + std::chrono::microseconds(q->flush_usec)) ==
-                       std::cv_status::timeout) {
-                if (B->reserved > 0) break;
+            if (B->reserved > 0 && (q->flush_usec == 0 || q->flush_target >= B->seq)) break;
+            if (B->reserved > 0) {
+                // linger for company. Short lingers spin: a timed futex sleep is rounded up by the
+                // kernel's timer slack (50 us by default), longer than the whole GPU step.
+                const auto deadline = B->first + std::chrono::microseconds(q->flush_usec);
+                if (q->flush_usec <= 1000) {
+                    lk.unlock();
+                    while (Clock::now() < deadline && q->queued.load(std::memory_order_acquire) < q->cap &&
+                           !q->stop_req.load(std::memory_order_acquire))
+                        cpu_relax();
+                    lk.lock();
+                } else {
+                    q->cv_flusher.wait_until(lk, deadline);
+                }
+                if (B->reserved == q->cap || q->stop || Clock::now() >= deadline || q->flush_target >= B->seq) break;
+                continue;
             }
+            // idle: spin a little for the next frame, then sleep until a producer or flush() calls
+            lk.unlock();
+            const auto until = Clock::now() + kSpin;
+            while (q->queued.load(std::memory_order_acquire) == 0 && Clock::now() < until &&
+                   !q->stop_req.load(std::memory_order_acquire))
+                cpu_relax();
+            lk.lock();
+            if (B->reserved == 0 && !q->stop && q->flush_target < B->seq) q->cv_flusher.wait(lk);
         }
         if (B->reserved == 0) {   // stop requested and nothing left
             q->seq_done = B->seq - 1;
@@ -93,17 +121,22 @@ void flusher(fcs_txq *q) {
         }
         // close B; producers move on to the other buffer
         const uint32_t n = B->reserved;
+        q->ns_pickup += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - B->first).count();
         q->open ^= 1;
         Batch &N = q->b[q->open];
         N.reserved = 0;
         N.ready.store(0, std::memory_order_relaxed);
         N.seq = B->seq + 1;
+        q->queued.store(0, std::memory_order_relaxed);
         q->cv_prod.notify_all();
         lk.unlock();
 
+        const auto t0 = Clock::now();
         while (B->ready.load(std::memory_order_acquire) < n) std::this_thread::yield();
+        const auto t1 = Clock::now();
         // FCS of every frame, written little-endian after its covered bytes (ether.c:262-263)
         const int rc = ether_fcs_tx_host(B->arena, kSlot, B->covered.data(), n);
+        const auto t2 = Clock::now();
         if (rc == 0) {
             for (uint32_t i = 0; i < n; i++) {
                 B->frames[i] = B->arena + (uint64_t)i * kSlot;
@@ -114,13 +147,19 @@ void flusher(fcs_txq *q) {
         } else {
             for (uint32_t i = 0; i < n; i++) B->res[i] = rc;   // nothing leaves unchecked
         }
+        const auto t3 = Clock::now();
 
         lk.lock();
+        auto ns = [](Clock::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
+        q->ns_ready += ns(t1 - t0);
+        q->ns_gpu += ns(t2 - t1);
+        q->ns_sink += ns(t3 - t2);
+        q->ns_busy += ns(Clock::now() - t0);
         for (uint32_t i = 0; i < n; i++) {
             if (B->res[i] != (int)(B->covered[i] + kFcsLen)) q->n_errors++;
             if (Waiter *w = B->waiters[i]) {   // null: fcs_txq_send_async
                 w->result = B->res[i];
-                w->done = true;
+                w->done.store(true, std::memory_order_release);   // last touch: w may vanish now
             }
         }
         q->seq_done = B->seq;
@@ -184,6 +223,7 @@ int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf
     const uint32_t slot = B.reserved++;
     if (slot == 0) B.first = Clock::now();
     B.waiters[slot] = w;
+    q->queued.store(B.reserved, std::memory_order_release);
     if (slot == 0 || B.reserved == q->cap) q->cv_flusher.notify_one();
     lk.unlock();
 
@@ -208,8 +248,12 @@ int fcs_txq_send(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const uint8
     Waiter w;
     const int rc = enqueue(q, dst, proto, buf, bsize, &w);
     if (rc < 0) return rc;
-    std::unique_lock<std::mutex> lk(q->mu);
-    while (!w.done) q->cv_prod.wait(lk);
+    const auto until = Clock::now() + kSpin;
+    while (!w.done.load(std::memory_order_acquire) && Clock::now() < until) cpu_relax();
+    if (!w.done.load(std::memory_order_acquire)) {
+        std::unique_lock<std::mutex> lk(q->mu);
+        while (!w.done.load(std::memory_order_acquire)) q->cv_prod.wait(lk);
+    }
     return w.result;
 }
 
@@ -234,6 +278,7 @@ void fcs_txq_destroy(fcs_txq_t *q) {
         {
             std::lock_guard<std::mutex> lk(q->mu);
             q->stop = true;
+            q->stop_req.store(true, std::memory_order_release);
         }
         q->cv_flusher.notify_one();
         q->th.join();
@@ -255,6 +300,18 @@ void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint
     if (frames) *frames = m->n_frames;
     if (batches) *batches = m->n_batches;
     if (errors) *errors = m->n_errors;
+}
+
+void fcs_txq_timing(const fcs_txq_t *q, uint64_t *ns_ready, uint64_t *ns_gpu, uint64_t *ns_sink,
+                    uint64_t *ns_busy, uint64_t *ns_pickup) {
+    if (!q) return;
+    fcs_txq *m = const_cast<fcs_txq *>(q);
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (ns_ready) *ns_ready = m->ns_ready;
+    if (ns_gpu) *ns_gpu = m->ns_gpu;
+    if (ns_sink) *ns_sink = m->ns_sink;
+    if (ns_busy) *ns_busy = m->ns_busy;
+    if (ns_pickup) *ns_pickup = m->ns_pickup;
 }
 
 // ---- sinks ----

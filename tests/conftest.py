@@ -49,3 +49,13 @@ def golden():
     with open(os.path.join(GOLDEN, "kat.json")) as f:
         kat = json.load(f)
     return {"vectors": vec, "arena": arena, "kat": kat}
+
+
+@pytest.fixture(params=["quarter", "windowed"])
+def var_kernel(request):
+    """Run a variable-length test through both var kernels (identical results required):
+    quarter = one quarter-wave per frame (small batches), windowed = 64-frame windows."""
+    import nstack_amd as na
+    old = na.set_var_threshold((1 << 63) if request.param == "quarter" else 0)
+    yield request.param
+    na.set_var_threshold(old)

@@ -67,7 +67,7 @@ def run_fixed(dev, base_t, stride, L, n):
 
 
 # ---------------------------------------------------------------- fixtures (golden, KAT)
-def test_golden_vectors_var(dev, golden):
+def test_golden_vectors_var(dev, var_kernel, golden):
     arena = np.frombuffer(golden["arena"], dtype=np.uint8).copy()
     fr = golden["vectors"]["frames"]
     got = run_var(dev, arena, [f["off"] for f in fr], [f["len"] for f in fr])
@@ -83,7 +83,7 @@ def test_golden_vectors_fixed_one_by_one(dev, golden):
         assert int(got[0]) == f["crc"], f
 
 
-def test_known_answers(dev, golden):
+def test_known_answers(dev, var_kernel, golden):
     for case in golden["kat"]["cases"]:
         b = bytes.fromhex(case["hex"]) if case["hex"] is not None else bytes([case["fill"]]) * case["len"]
         arr = np.frombuffer(b + b"\0" * 8, dtype=np.uint8).copy()
@@ -117,7 +117,7 @@ def test_fixed_edge_lengths_all_alignments(dev, oracle, L):
             assert np.array_equal(got, exp), (L, stride, lead, int(np.argmax(got != exp)))
 
 
-def test_frames_touching_allocation_edges(dev, oracle):
+def test_frames_touching_allocation_edges(dev, var_kernel, oracle):
     """Frame 0 at the very start and the last frame ending at the very end of the buffer."""
     for L in (1, 5, 70, 1517, 1518, 9000):
         n = 33
@@ -130,7 +130,7 @@ def test_frames_touching_allocation_edges(dev, oracle):
 
 
 # ---------------------------------------------------------------- variable length
-def test_random_lengths_random_offsets(dev, oracle):
+def test_random_lengths_random_offsets(dev, var_kernel, oracle):
     rng = np.random.default_rng(5)
     n = 20000
     ln = rng.integers(0, 9019, n).astype(np.uint32)
@@ -150,7 +150,7 @@ def imix(n, seed):
     return ln
 
 
-def test_imix_packed(dev, oracle):
+def test_imix_packed(dev, var_kernel, oracle):
     ln = imix(120000, 3)
     off = np.zeros(len(ln), dtype=np.uint64)
     off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
@@ -229,7 +229,7 @@ def test_baseline_size_properties(dev, oracle):
 
 
 # ---------------------------------------------------------------- host-side entry points
-def test_fixed_host_and_batch_host(dev, oracle):
+def test_fixed_host_and_batch_host(dev, var_kernel, oracle):
     n, L = 300000, 1518
     host = np.random.default_rng(8).integers(0, 256, n * L, dtype=np.uint8)
     out = np.zeros(n, dtype=np.uint32)
@@ -244,7 +244,7 @@ def test_fixed_host_and_batch_host(dev, oracle):
     assert np.array_equal(out2, oracle_var(oracle, arena, off, ln))
 
 
-def test_tx_mode_matches_ether_send_layout(dev, oracle):
+def test_tx_mode_matches_ether_send_layout(dev, var_kernel, oracle):
     """ether_send (src/linux/ether.c:222-263): frame = hdr + payload + zero pad, FCS over
     frame_size-4 bytes stored little-endian at the end. Batched TX must produce byte-identical
     frames; every frame then satisfies the CRC residue 0x2144DF1C."""

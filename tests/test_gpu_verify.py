@@ -67,7 +67,7 @@ def run_verify_var(dev, arena, off, ln):
     return ok.cpu().numpy(), int(bad.item())
 
 
-def test_verify_var_all_classes(dev, oracle):
+def test_verify_var_all_classes(dev, var_kernel, oracle):
     """Small (<= 96), medium (<= 768), big (> 768) and multi-segment frames, corrupted 20 %."""
     rng = np.random.default_rng(41)
     lens = [int(x) for x in rng.choice([0, 1, 3, 4, 5, 60, 64, 74, 96, 97, 200, 576, 768, 769,
@@ -81,7 +81,7 @@ def test_verify_var_all_classes(dev, oracle):
     assert not ok[ln < 4].any()
 
 
-def test_verify_var_edges_and_tiny_arena(dev, oracle):
+def test_verify_var_edges_and_tiny_arena(dev, var_kernel, oracle):
     """Frames at the very start/end of the arena, and an arena too small for chunk windows."""
     rng = np.random.default_rng(42)
     for lens in ([74], [4, 8, 12], [70, 74, 96], [1514, 74], [5] * 30):
@@ -93,7 +93,7 @@ def test_verify_var_edges_and_tiny_arena(dev, oracle):
         assert bad == int((exp == 0).sum())
 
 
-def test_verify_host_matches_device(dev, oracle):
+def test_verify_host_matches_device(dev, var_kernel, oracle):
     rng = np.random.default_rng(43)
     lens = [int(x) for x in rng.integers(70, 1519, 20000)]
     arena, off, ln = build_rx_batch(oracle, rng, lens, corrupt_frac=0.05)

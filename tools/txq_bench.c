@@ -134,8 +134,9 @@ int main(int argc, char **argv) {
     for (int t = 0; t < P; t++) pthread_join(th[t], NULL);
     if (Q) fcs_txq_flush(Q);
     const double t1 = now();
-    uint64_t frames = 0, batches = 0, errors = 0;
+    uint64_t frames = 0, batches = 0, errors = 0, nr = 0, ng = 0, ns = 0, nb = 0, np_ = 0;
     if (Q) fcs_txq_stats(Q, &frames, &batches, &errors);
+    if (Q) fcs_txq_timing(Q, &nr, &ng, &ns, &nb, &np_);
     if (SOCK) {
         while (atomic_load(&sunk_frames) < (unsigned long long)P * M && now() - t1 < 10) usleep(1000);
         shutdown(sock_tx, SHUT_RDWR);
@@ -146,11 +147,14 @@ int main(int argc, char **argv) {
     const double dt = t1 - t0, nf = (double)P * M;
     printf("{\"mode\": \"%s\", \"sink\": \"%s\", \"producers\": %d, \"frames\": %.0f, \"payload\": %d, "
            "\"max_batch\": %d, \"flush_usec\": %d, \"s\": %.4f, \"Mframes_s\": %.4f, \"Gbit_s\": %.3f, "
-           "\"mean_batch\": %.1f, \"bad_results\": %llu, \"sunk_frames\": %llu, \"queue_errors\": %llu}\n",
+           "\"mean_batch\": %.1f, \"bad_results\": %llu, \"sunk_frames\": %llu, \"queue_errors\": %llu, "
+           "\"us_per_batch\": {\"ready\": %.1f, \"gpu\": %.1f, \"sink\": %.1f, \"busy\": %.1f, \"pickup\": %.1f, \"wall\": %.1f}}\n",
            DROPIN ? "dropin" : (ASYNC ? "async" : "txq"), SOCK ? "socketpair" : "null", P, nf, PAYLOAD, BATCH, FLUSH_US, dt,
            nf / dt / 1e6, (double)atomic_load(&sunk_bytes) * 8 / dt / 1e9, batches ? (double)frames / batches : 1.0,
            (unsigned long long)atomic_load(&bad_results), (unsigned long long)atomic_load(&sunk_frames),
-           (unsigned long long)errors);
+           (unsigned long long)errors, batches ? nr / 1e3 / batches : 0.0, batches ? ng / 1e3 / batches : 0.0,
+           batches ? ns / 1e3 / batches : 0.0, batches ? nb / 1e3 / batches : 0.0, batches ? np_ / 1e3 / batches : 0.0,
+           batches ? dt * 1e6 / batches : 0.0);
     if (Q) fcs_txq_destroy(Q);
     return (atomic_load(&bad_results) || errors) ? 2 : 0;
 }
