@@ -146,21 +146,36 @@ constexpr uint32_t kResidue = 0x2144DF1Cu;
 
 // Result store for one frame per lane with st set; called by the whole wave (convergent).
 // FCS mode: out[i] = FCS. Verify mode (ok != null; frames carry their FCS trailer): ok[i] = 1 iff
-// the FCS over the whole frame equals the residue; non-matching frames are counted into *bad with
-// one atomic per wave. Both may be requested together.
-__device__ __forceinline__ void emit(uint32_t *out, uint8_t *ok, unsigned long long *bad, bool st, uint64_t i,
-                                     uint32_t fcs) {
-    if (out != nullptr && st) out[i] = fcs;
-    if (ok != nullptr) {
+// the FCS over the whole frame equals the residue; non-matching frames are counted in the wave's
+// LDS slot (lane 0 only touches it) and added to *bad once per wave at kernel exit (flush_bad), so
+// an all-bad batch costs no atomics on the data path. Both outputs may be requested together.
+__device__ __forceinline__ uint64_t *wave_bad(const uint8_t *lds) {   // the kernels' own __shared__ array
+    return reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(lds) + kLdsBad) + (threadIdx.x >> 6);
+}
+
+__device__ __forceinline__ void emit(const KParams &p, const uint8_t *lds, bool st, uint64_t i, uint32_t fcs) {
+    if (p.out != nullptr && st) p.out[i] = fcs;
+    if (p.ok != nullptr) {
         const bool good = fcs == kResidue;
-        if (st) ok[i] = good ? 1 : 0;
+        if (st) p.ok[i] = good ? 1 : 0;
         const uint64_t m = __ballot(st && !good);
-        if (m != 0 && (threadIdx.x & 63) == 0) atomicAdd(bad, (unsigned long long)__popcll(m));
+        if (m != 0 && (threadIdx.x & 63) == 0) *wave_bad(lds) += (uint64_t)__popcll(m);
+    }
+}
+
+__device__ __forceinline__ void init_bad(const uint8_t *lds) {
+    if ((threadIdx.x & 63) == 0) *wave_bad(lds) = 0;
+}
+
+__device__ __forceinline__ void flush_bad(const KParams &p, const uint8_t *lds) {
+    if (p.ok != nullptr && (threadIdx.x & 63) == 0) {
+        const uint64_t b = *wave_bad(lds);
+        if (b) atomicAdd(p.bad, (unsigned long long)b);
     }
 }
 
 // Chunk loads are issued at raised wave priority: a wave about to feed the memory pipe goes ahead
-// of waves busy with CRC arithmetic (+1.3 % on 64 M x 1518, tools/ab.py). Scoped: the wave drops
+// of waves busy with CRC arithmetic (+1.6 % on 64 M x 1518, tools/ab.py). Scoped: the wave drops
 // back to priority 0 right after its loads are issued.
 #ifndef FCS_LOAD_PRIO
 #define FCS_LOAD_PRIO 1
@@ -358,7 +373,7 @@ struct Lane {
         if (__any(last)) {
             uint32_t v = last ? lane_shift(lds, s, lanebase) : 0u;
             v = row_xor(v);
-            emit(p.out, p.ok, p.bad, last && j == 15, c.f, c.it.len ? ~v : 0u);
+            emit(p, lds, last && j == 15, c.f, c.it.len ? ~v : 0u);
         }
     }
 };
@@ -388,6 +403,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
 
     stage_tables(p, lds);
+    init_bad(lds);
 
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
@@ -439,6 +455,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
         L.process(C, CC, s);
     }
 #endif
+    flush_bad(p, lds);
 }
 
 
@@ -460,9 +477,7 @@ __device__ __forceinline__ uint64_t stamp() {
 
 struct SingleLane {
     uint64_t *dbg;
-    uint32_t *out;
-    uint8_t *ok;
-    unsigned long long *bad;
+    const KParams *kp;
     const uint8_t *lds;
     int j;
     uint32_t base0, base1, lanebase, x0, zmax;
@@ -512,7 +527,7 @@ struct SingleLane {
         uint32_t v = lane_shift(lds, uniform_shift<kLdsH48>(lds, xa, xb), lanebase);
 #endif
         v = row_xor(v);
-        emit(out, ok, bad, act && j == 15, fi, ~v);
+        emit(*kp, lds, act && j == 15, fi, ~v);
 #ifdef FCS_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts2 = stamp();
@@ -537,15 +552,14 @@ __device__ __forceinline__ void issue_raw(uint64_t a, uint32_t r, Raw &c) {
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     stage_tables(p, lds);
+    init_bad(lds);
 
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
     SingleLane S;
     S.dbg = p.dbg;
-    S.out = p.out;
-    S.ok = p.ok;
-    S.bad = p.bad;
+    S.kp = &p;
     S.lds = lds;
     S.j = j;
     S.base0 = r4;
@@ -615,6 +629,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
         end = endB;
         fi += Q;
     }
+    flush_bad(p, lds);
 }
 
 
@@ -703,17 +718,65 @@ __device__ __forceinline__ int clamp_zr(int64_t z) {
     return z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
 }
 
+// One half-unit item of the windowed var kernel (fcs_var_kernel): 8 half-units of 8 lanes.
+// unit_issue resolves this lane's frame and chunk and issues its loads; unit_finish computes the
+// chunk, reduces each frame's lanes and stores.
+struct UnitItem {
+    Chunk ch;
+    uint32_t meta;   // zr + 1 (bits 0-7) | valid (8) | full row (9) | small lane (10) | empty frame (11) |
+                     // window lane of this lane's frame (16-21)
+};
+
+template <bool TINY>
+__device__ __forceinline__ void unit_issue(const KParams &p, const uint8_t *lists, uint32_t Ehi, uint32_t Elo,
+                                           uint32_t L, uint32_t nf, uint32_t nfm, uint32_t nu, uint32_t ns,
+                                           uint32_t t, int lane, int j, UnitItem &it) {
+    const uint32_t u = t + (uint32_t)(lane >> 3);
+    const bool isfull = u < 2 * nf;   // same for both halves of a row
+    const bool issmall = u >= nfm;
+    const uint32_t si = (u - nfm) * 8 + (uint32_t)(lane & 7);   // small frame rank
+    const bool valid = issmall ? (u < nu && si < ns) : u < nu;
+    const int src = valid ? (int)lists[isfull ? 64 + (u >> 1) : (issmall ? 192 + si : u - 2 * nf)] : 0;
+    const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+    const uint32_t Lg = (uint32_t)__shfl((int)L, src);
+    const int c = isfull ? j : (issmall ? 0 : (lane & 7));   // chunk index back from the frame end
+    const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (c + 1);
+    const int zr = clamp_zr((int64_t)(Eg - Lg) - cstart);
+    issue_any<TINY>(p, cstart, valid && zr < kChunkBytes, it.ch);
+    it.meta = (uint32_t)((valid ? zr : kChunkBytes) + 1) | (valid ? 1u << 8 : 0u) | (isfull ? 1u << 9 : 0u) |
+              (issmall ? 1u << 10 : 0u) | (Lg == 0 ? 1u << 11 : 0u) | ((uint32_t)src << 16);
+}
+
+template <bool TINY>
+__device__ __forceinline__ void unit_finish(const KParams &p, const uint8_t *lds, const UnitItem &it, uint64_t w0,
+                                            int lane, int j, uint32_t base0, uint32_t base1, uint32_t lanebase) {
+    const bool valid = it.meta & (1u << 8), isfull = it.meta & (1u << 9), issmall = it.meta & (1u << 10);
+    const int zr = (int)(it.meta & 0xFFu) - 1;
+    const uint32_t own = chunk_value<TINY>(lds, it.ch, zr, valid ? inv_start(lds, zr) : 0u, base0, base1);
+    uint32_t v = lane_shift(lds, own, lanebase);   // A_{96 j}
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // half_mirror
+    // full rows join their halves (row_mirror); medium upper halves used A_{96(c+8)}: undo A_768
+    const uint32_t joined = v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
+    const uint32_t fixed = uniform_shift<kLdsM768>(lds, v, 0u);
+    v = isfull ? joined : (issmall ? own : (j >= 8 ? fixed : v));
+    emit(p, lds, valid && (isfull ? j == 15 : (issmall || (lane & 7) == 7)), w0 + ((it.meta >> 16) & 63u),
+         (it.meta & (1u << 11)) ? 0u : ~v);
+}
+
 template <bool TINY>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
     stage_tables(p, lds);
+    init_bad(lds);
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
     const uint32_t base0 = r4, base1 = 0x10000u | r4, lanebase = kLdsLane | r4;
-    uint8_t *lists = lds + kLdsWave + wave * kLdsWaveBytes;   // [0,64): medium, [64,128): big
+    uint8_t *lists = lds + kLdsWave + wave * kLdsWaveBytes;   // medium | full | multi | small, 64 each
     const uint64_t GW = (uint64_t)gridDim.x * (kWgThreads / 64);
 
     for (uint64_t w0 = ((uint64_t)blockIdx.x * (kWgThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
@@ -724,52 +787,42 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
         const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;   // off == null: slots of p.stride
         const bool small = act && L <= (uint32_t)kChunkBytes;
         const bool med = act && !small && L <= 8u * kChunkBytes;
-        const bool big = act && L > 8u * kChunkBytes;
-        const uint64_t mmask = __ballot(med), bmask = __ballot(big);
-        const uint32_t nm = (uint32_t)__popcll(mmask), nb = (uint32_t)__popcll(bmask);
+        const bool full = act && L > 8u * kChunkBytes && L <= (uint32_t)kSegBytes;
+        const bool multi = act && L > (uint32_t)kSegBytes;
+        const uint64_t mmask = __ballot(med), fmask = __ballot(full), xmask = __ballot(multi);
+        const uint32_t nm = (uint32_t)__popcll(mmask), nf = (uint32_t)__popcll(fmask), nx = (uint32_t)__popcll(xmask);
         const uint32_t rm = __builtin_amdgcn_mbcnt_hi((uint32_t)(mmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mmask, 0u));
-        const uint32_t rb = __builtin_amdgcn_mbcnt_hi((uint32_t)(bmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bmask, 0u));
+        const uint32_t rf = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+        const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
         if (med) lists[rm] = (uint8_t)lane;
-        if (big) lists[64 + rb] = (uint8_t)lane;
+        if (full) lists[64 + rf] = (uint8_t)lane;
+        if (multi) lists[128 + rx] = (uint8_t)lane;
+        const uint64_t smask = __ballot(small);
+        const uint32_t ns = (uint32_t)__popcll(smask);
+        const uint32_t rs = __builtin_amdgcn_mbcnt_hi((uint32_t)(smask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smask, 0u));
+        if (small) lists[192 + rs] = (uint8_t)lane;
         const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
 
-        // ---- small frames: each in its own lane ----
-        if (__any(small)) {
-            const int zr = small ? (int)(kChunkBytes - L) : kChunkBytes;
-            Chunk c;
-            issue_any<TINY>(p, (int64_t)E - kChunkBytes, small && L > 0, c);
-            const uint32_t v = chunk_value<TINY>(lds, c, zr, small ? inv_start(lds, zr) : 0u, base0, base1);
-            emit(p.out, p.ok, p.bad, small, f, L ? ~v : 0u);
+        // ---- half-units (8 lanes each, 8 per item), in this order:
+        //      full frame (769..1536 B): two halves of one 16-lane row (chunk index = j);
+        //      medium frame (97..768 B): one half (chunk index = lane & 7);
+        //      small frames (<= 96 B): eight per half, one lane each, a single chunk.
+        //      Full frames come first, so their rows are aligned. ----
+        const uint32_t nfm = 2 * nf + nm;
+        const uint32_t nu = nfm + (ns + 7) / 8;
+        // one item at a time: a second item in flight measured 5-7 % slower here (the var loop is
+        // issue-bound, and the extra registers cost waits), unlike the fixed kernels
+        for (uint32_t t = 0; t < nu; t += 8) {
+            UnitItem A;
+            unit_issue<TINY>(p, lists, Ehi, Elo, L, nf, nfm, nu, ns, t, lane, j, A);
+            unit_finish<TINY>(p, lds, A, w0, lane, j, base0, base1, lanebase);
         }
 
-        // ---- medium frames: 8 lanes each, 8 per item ----
-        for (uint32_t t = 0; t < nm; t += 8) {
-            const uint32_t rank = t + (uint32_t)(lane >> 3);
-            const bool valid = rank < nm;
-            const int src = valid ? (int)lists[rank] : 0;
-            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
-            const uint32_t Lg = (uint32_t)__shfl((int)L, src);
-            const int c8 = lane & 7;
-            const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (c8 + 1);
-            const int zr = clamp_zr((int64_t)(Eg - Lg) - cstart);
-            Chunk c;
-            issue_any<TINY>(p, cstart, valid && zr < kChunkBytes, c);
-            uint32_t v = chunk_value<TINY>(lds, c, valid ? zr : kChunkBytes, valid ? inv_start(lds, zr) : 0u,
-                                           base0, base1);
-            v = lane_shift(lds, v, lanebase);
-            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
-            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
-            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // half_mirror
-            const uint32_t fixed = uniform_shift<kLdsM768>(lds, v, 0u);
-            v = (j >= 8) ? fixed : v;
-            emit(p.out, p.ok, p.bad, valid && c8 == 7, w0 + (uint32_t)src, Lg ? ~v : 0u);
-        }
-
-        // ---- big frames: 16 lanes each, 4 per item, segment by segment ----
-        for (uint32_t t = 0; t < nb; t += 4) {
+        // ---- multi-segment frames (> 1536 B): 16 lanes each, 4 per item, segment by segment ----
+        for (uint32_t t = 0; t < nx; t += 4) {
             const uint32_t rank = t + (uint32_t)(lane >> 4);
-            const bool valid = rank < nb;
-            const int src = valid ? (int)lists[64 + rank] : 0;
+            const bool valid = rank < nx;
+            const int src = valid ? (int)lists[128 + rank] : 0;
             const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
             const uint32_t Lq = (uint32_t)__shfl((int)L, src);
             const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
@@ -787,9 +840,10 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
             }
             uint32_t v = lane_shift(lds, s, lanebase);
             v = row_xor(v);
-            emit(p.out, p.ok, p.bad, valid && j == 15, w0 + (uint32_t)src, Lq ? ~v : 0u);
+            emit(p, lds, valid && j == 15, w0 + (uint32_t)src, Lq ? ~v : 0u);
         }
     }
+    flush_bad(p, lds);
 }
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).

@@ -46,8 +46,9 @@ constexpr uint32_t kLdsH24 = 148480;    // 8 x 16 x 4 B = 512 (A_24)
 constexpr uint32_t kLdsInv = 148992;    // 96 x 4 B = 384
 constexpr uint32_t kLdsM768 = 149376;   // 8 x 16 x 4 B = 512 (A_{-768})
 constexpr uint32_t kLdsWave = 149888;   // per-wave scratch for the variable-length kernel
-constexpr uint32_t kLdsWaveBytes = 128; //   (two 64-entry frame lists per wave)
-constexpr uint32_t kLdsBytes = kLdsWave + 16 * kLdsWaveBytes;   // 151936
+constexpr uint32_t kLdsWaveBytes = 256; //   (four 64-entry frame lists per wave)
+constexpr uint32_t kLdsBad = kLdsWave + 16 * kLdsWaveBytes;    // 153984: per-wave u64 failing-frame count (verify)
+constexpr uint32_t kLdsBytes = kLdsBad + 16 * 8;                // 154112
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)

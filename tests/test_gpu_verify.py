@@ -144,3 +144,24 @@ def test_verify_baseline_size_residue(dev):
     torch.cuda.synchronize()
     assert int(bad.item()) == len(idx)
     assert torch.nonzero(ok == 0).flatten().tolist() == sorted(idx.tolist())
+
+
+def test_verify_counts_every_bad_frame(dev, var_kernel):
+    """All-bad batch (random trailers): the per-wave LDS counters must add up to exactly the
+    number of frames whose FCS over the whole frame is not the residue (computed by the FCS path)."""
+    n, L = 1 << 20, 1518
+    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, n * L, 91, 0)
+    crc = torch.empty(n, dtype=torch.int32, device=dev)
+    na.fixed_dev(arena, L, L, n, crc)
+    expect = int((crc != RESIDUE).sum().item())
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    na.verify_fixed_dev(arena, L, L, n, ok, bad)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == expect and int((ok == 0).sum().item()) == expect
+    off = torch.arange(n, dtype=torch.int64, device=dev) * L
+    ln = torch.full((n,), L, dtype=torch.int32, device=dev)
+    na.verify_dev(arena, n * L, off, ln, ok, bad, n)
+    torch.cuda.synchronize()
+    assert int(bad.item()) == expect
