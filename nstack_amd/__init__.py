@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "set_var_threshold", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -30,6 +30,8 @@ EXPORTS = [
     # include/nstack_txq.h — batched TX call site
     "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
+    # include/nstack_pcap.h — frame batches on disk
+    "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
 ]
 
 
@@ -84,6 +86,9 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_txq_timing": (None, [vp] + [c.POINTER(u64)] * 5),
         "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
         "fcs_txq_sink_packet": (None, [vp, vp, vp, vp, u32]),
+        "fcs_pcap_scan": (i32, [c.c_char_p, c.POINTER(u64), c.POINTER(u64), c.POINTER(u32), c.POINTER(u64)]),
+        "fcs_pcap_read": (c.c_int64, [c.c_char_p, vp, u64, vp, vp, u64]),
+        "fcs_pcap_write": (i32, [c.c_char_p, vp, vp, vp, u64, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -258,3 +263,32 @@ class TxQueue:
 
     def __exit__(self, *exc):
         self.close()
+
+
+def pcap_scan(path: str):
+    """(frames, captured bytes, link type, truncated records) of a classic pcap file."""
+    n, b, t = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+    lt = ctypes.c_uint32(0)
+    _check(load().fcs_pcap_scan(os.fsencode(path), ctypes.byref(n), ctypes.byref(b), ctypes.byref(lt),
+                                ctypes.byref(t)), "fcs_pcap_scan")
+    return int(n.value), int(b.value), int(lt.value), int(t.value)
+
+
+def pcap_read(path: str):
+    """Load a pcap into the batch layout: (arena u8, off u64, len u32, link type) as numpy arrays."""
+    import numpy as np
+    n, b, lt, _ = pcap_scan(path)
+    arena = np.zeros(max(b, 1), dtype=np.uint8)
+    off = np.zeros(max(n, 1), dtype=np.uint64)
+    ln = np.zeros(max(n, 1), dtype=np.uint32)
+    got = _check(load().fcs_pcap_read(os.fsencode(path), arena.ctypes.data, arena.size, off.ctypes.data,
+                                      ln.ctypes.data, n), "fcs_pcap_read")
+    return arena[:b], off[:got], ln[:got], lt
+
+
+def pcap_write(path: str, arena, off, length, linktype: int = 1) -> None:
+    import numpy as np
+    off = np.ascontiguousarray(off, dtype=np.uint64)
+    length = np.ascontiguousarray(length, dtype=np.uint32)
+    _check(load().fcs_pcap_write(os.fsencode(path), _ptr(arena), off.ctypes.data, length.ctypes.data,
+                                 len(off), linktype), "fcs_pcap_write")

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/nstack_fcs.h"
+#include "fcs_error.hpp"
 #include "fcs_launch.hpp"
 #include "fcs_tables.hpp"
 
@@ -504,6 +505,16 @@ int run_host_sharded(HostJob job, uint64_t n) {
 }
 
 }  // namespace
+
+int fcs::set_error(int err, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return -err;
+}
 
 extern "C" {
 
