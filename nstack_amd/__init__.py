@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -32,7 +32,14 @@ EXPORTS = [
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
+    # include/nstack_inet.h — batched Internet checksums (opt-in)
+    "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_ip_checksum",
+    "inet_tcp_checksum", "inet_udp_checksum",
 ]
+
+# include/nstack_inet.h modes: the reference function each result reproduces
+INET_CSUM_IP, INET_CSUM_TCP, INET_CSUM_UDP = 0, 1, 2
+INET_MODES = {"ip": INET_CSUM_IP, "tcp": INET_CSUM_TCP, "udp": INET_CSUM_UDP}
 
 
 class FcsError(RuntimeError):
@@ -89,6 +96,12 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_pcap_scan": (i32, [c.c_char_p, c.POINTER(u64), c.POINTER(u64), c.POINTER(u32), c.POINTER(u64)]),
         "fcs_pcap_read": (c.c_int64, [c.c_char_p, vp, u64, vp, vp, u64]),
         "fcs_pcap_write": (i32, [c.c_char_p, vp, vp, vp, u64, u32]),
+        "inet_csum_batch_dev": (i32, [i32, vp, u64, vp, vp, vp, vp, u64, vp]),
+        "inet_csum_fixed_dev": (i32, [i32, vp, u64, u32, u64, vp, vp, vp]),
+        "inet_csum_batch_host": (i32, [i32, vp, u64, vp, vp, vp, vp, u64]),
+        "inet_ip_checksum": (c.c_uint16, [vp, c.c_size_t]),
+        "inet_tcp_checksum": (c.c_uint16, [u32, u32, vp, c.c_size_t]),
+        "inet_udp_checksum": (c.c_uint16, [vp, c.c_size_t, u32, u32]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)
@@ -292,3 +305,42 @@ def pcap_write(path: str, arena, off, length, linktype: int = 1) -> None:
     length = np.ascontiguousarray(length, dtype=np.uint32)
     _check(load().fcs_pcap_write(os.fsencode(path), _ptr(arena), off.ctypes.data, length.ctypes.data,
                                  len(off), linktype), "fcs_pcap_write")
+
+
+# ---- Internet checksums (include/nstack_inet.h; src/ip.c:39, src/tcp.c:167, src/udp.c:136) ----
+def _mode(mode) -> int:
+    return INET_MODES[mode] if isinstance(mode, str) else int(mode)
+
+
+def inet_batch_dev(mode, arena, arena_bytes: int, off, length, addr, out, n: int, stream=None) -> None:
+    """out[i] (u16) = the reference checksum of arena[off[i]:off[i]+len[i]] (device arrays)."""
+    _check(load().inet_csum_batch_dev(_mode(mode), _ptr(arena), arena_bytes, _ptr(off), _ptr(length),
+                                      _ptr(addr), _ptr(out), n, _stream(stream)), "inet_csum_batch_dev")
+
+
+def inet_fixed_dev(mode, base, stride: int, length: int, n: int, addr, out, stream=None) -> None:
+    _check(load().inet_csum_fixed_dev(_mode(mode), _ptr(base), stride, length, n, _ptr(addr), _ptr(out),
+                                      _stream(stream)), "inet_csum_fixed_dev")
+
+
+def inet_batch_host(mode, arena, arena_bytes: int, off, length, addr, out, n: int) -> None:
+    _check(load().inet_csum_batch_host(_mode(mode), _ptr(arena), arena_bytes, _ptr(off), _ptr(length),
+                                       _ptr(addr), _ptr(out), n), "inet_csum_batch_host")
+
+
+def ip_checksum(data) -> int:
+    """ip_checksum(dp, bsize) of src/ip.c:39-62, computed on the GPU."""
+    b = bytes(data)
+    return load().inet_ip_checksum(b, len(b))
+
+
+def tcp_checksum(src: int, dst: int, data) -> int:
+    """tcp_checksum(&src, &dst, dp, bsize) of src/tcp.c:167-213 (host-order addresses)."""
+    b = bytes(data)
+    return load().inet_tcp_checksum(src, dst, b, len(b))
+
+
+def udp_checksum(data, src: int, dst: int) -> int:
+    """udp_checksum(buff, len, src, dst) of src/udp.c:136-174 (raw in_addr_t values)."""
+    b = bytes(data)
+    return load().inet_udp_checksum(b, len(b), src, dst)

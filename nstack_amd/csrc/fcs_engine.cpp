@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "../../include/nstack_fcs.h"
+#include "fcs_device.hpp"
 #include "fcs_error.hpp"
 #include "fcs_launch.hpp"
 #include "fcs_tables.hpp"
@@ -505,6 +506,24 @@ int run_host_sharded(HostJob job, uint64_t n) {
 }
 
 }  // namespace
+
+int fcs::current_device(int *dev, int *cus) {
+    DevState *ds = nullptr;
+    const int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    *dev = ds->dev;
+    *cus = ds->cus;
+    return 0;
+}
+
+int fcs::engine_device0(int *dev, int *cus) {
+    std::vector<DevState *> devs;
+    const int rc = engine_devices(&devs);
+    if (rc) return rc;
+    *dev = devs[0]->dev;
+    *cus = devs[0]->cus;
+    return 0;
+}
 
 int fcs::set_error(int err, const char *fmt, ...) {
     char buf[512];

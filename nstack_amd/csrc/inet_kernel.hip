@@ -1,0 +1,150 @@
+// inet_kernel.hip — batched Internet checksums (RFC 1071 one's-complement sums) for gfx950.
+//
+// Serves SURVEY.md §8f row 3: the per-packet byte loops of nstack's
+//   ip_checksum   /root/reference/src/ip.c:39-62     (IP headers; ICMP via src/icmp.c:42,74)
+//   tcp_checksum  /root/reference/src/tcp.c:167-213  (12-byte pseudo header, then the segment)
+//   udp_checksum  /root/reference/src/udp.c:136-174  (the segment, then the pseudo header)
+// as one launch over many packets; out[i] is bit-identical to the reference function's return
+// value (a host-order u16 whose memory bytes are the on-wire checksum).
+//
+// Arithmetic. All three are one's-complement sums of little-endian 16-bit words (the reference
+// memcpy's host-order words; RFC 1071's byte-order independence makes that the byte-swapped
+// checksum, which is exactly what it stores). Because 2^16 == 1 (mod 0xffff), a sum of 32-bit
+// words folded to 16 bits has the same residue, so each lane adds whole dwords of its 16-byte
+// chunks into a 64-bit register (v_add_co / v_addc per dword) and only the 16-lane total is
+// folded. A packet starting at an odd address pairs its bytes the other way round against the
+// aligned memory words: the memory-aligned sum M then satisfies P == 256*M (mod 0xffff), i.e.
+// P = swap16(fold(M)). The exact-zero case is kept apart from 0xffff (fold never maps a
+// nonzero sum to 0), because ip/tcp start their accumulator at 0xffff (ip.c:42, tcp.c:172):
+// the only input where that differs from a zero start is all-zero data (return 0x0000).
+//
+// Work decomposition. A QUARTER-WAVE (16 lanes) per packet; lane j loads the packet's aligned
+// 16-byte chunks j, j+16, ... (global_load_dwordx4; a group reads 256 contiguous bytes per
+// instruction, the four groups of a wave the next packets), six chunks per lane in flight per
+// round (1536 bytes per packet per round). Only the first and last chunk of a packet are
+// masked. The 16 lane sums are added with 4 DPP steps; lane 0 adds the pseudo header and init,
+// folds, complements and stores. No LDS, no tables: HBM read bandwidth is the roofline.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "inet_launch.hpp"
+
+namespace inet {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGroup = 16;       // lanes per packet
+constexpr int kRound = 6;        // chunks per lane per round
+constexpr int kThreads = 256;
+
+template <typename T>
+__device__ __forceinline__ T gload(uint64_t addr) {
+    return *reinterpret_cast<const __attribute__((address_space(1))) T *>(addr);
+}
+
+__device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
+
+// End-around-carry fold to [0, 0xffff]; 0 only for x == 0.
+__device__ __forceinline__ uint32_t fold64(uint64_t x) {
+    uint64_t y = (x & 0xffffffffull) + (x >> 32);
+    y = (y & 0xffffu) + (y >> 16);
+    y = (y & 0xffffu) + (y >> 16);
+    return (uint32_t)((y & 0xffffu) + (y >> 16));
+}
+
+// Sum over a 16-lane row; every lane ends with the row's sum.
+__device__ __forceinline__ uint32_t row_sum(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);  // row_mirror
+    return v;
+}
+
+// Byte mask of dword d of a chunk from a 16-bit keep mask (bit b = keep byte b of the chunk).
+__device__ __forceinline__ uint32_t byte_mask(uint32_t keep16, int d) {
+    const uint32_t b4 = (keep16 >> (4 * d)) & 0xfu;
+    return ((b4 * 0x00204081u) & 0x01010101u) * 0xffu;
+}
+
+// Pseudo-header contribution and accumulator start of each mode (exact integers, summed in the
+// little-endian word domain the reference uses).
+template <int MODE>
+__device__ __forceinline__ uint32_t pseudo(const IParams &p, uint64_t i, uint32_t len) {
+    const uint32_t l16 = swap16(len & 0xffffu);   // htons(len): size_t truncated to 16 bits
+    if (MODE == kIp) return 0xffffu;              // acc = 0xffff (src/ip.c:42)
+    const uint32_t s = p.addr[2 * i], d = p.addr[2 * i + 1];
+    if (MODE == kTcp)                             // acc = 0xffff; {htonl(src), htonl(dst), 0, 6, htons(len)}
+        return 0xffffu + swap16(s >> 16) + swap16(s & 0xffffu) + swap16(d >> 16) + swap16(d & 0xffffu) +
+               0x0600u + l16;                     // (src/tcp.c:172-195)
+    // udp: sum = 0; raw in_addr_t halves, htons(IPPROTO_UDP), htons(length) (src/udp.c:146,160-167)
+    return (s & 0xffffu) + (s >> 16) + (d & 0xffffu) + (d >> 16) + 0x1100u + l16;
+}
+
+template <bool VAR, int MODE>
+__global__ __launch_bounds__(kThreads) void inet_kernel(IParams p) {
+    const uint32_t lane = threadIdx.x & (kGroup - 1);
+    const uint64_t ngrp = ((uint64_t)gridDim.x * kThreads) / kGroup;
+    for (uint64_t i = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / kGroup; i < p.n; i += ngrp) {
+        const uint64_t start = VAR ? p.base + p.off[i] : p.base + i * p.stride;
+        const uint32_t len = VAR ? p.len[i] : p.flen;
+        const uint64_t end = start + len;
+        const uint64_t c0 = start & ~15ull;
+        const uint32_t nch = len ? (uint32_t)((((end + 15) & ~15ull) - c0) >> 4) : 0u;
+        uint64_t acc = 0;
+        for (uint32_t k0 = 0; k0 < nch; k0 += kGroup * kRound) {
+            u32x4 v[kRound];
+#pragma unroll
+            for (int j = 0; j < kRound; j++) {
+                const uint32_t k = k0 + lane + kGroup * j;
+                v[j] = gload<u32x4>(c0 + 16ull * (k < nch ? k : nch - 1));   // idle lanes re-read the last chunk
+            }
+#pragma unroll
+            for (int j = 0; j < kRound; j++) {
+                const uint32_t k = k0 + lane + kGroup * j;
+                if (k >= nch) continue;
+                u32x4 w = v[j];
+                if (k == 0 || k == nch - 1) {   // the packet's edge chunks: keep bytes in [start, end)
+                    const uint64_t ca = c0 + 16ull * k;
+                    const uint32_t lo = start > ca ? (uint32_t)(start - ca) : 0u;
+                    const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
+                    const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+                    w.x &= byte_mask(keep, 0);
+                    w.y &= byte_mask(keep, 1);
+                    w.z &= byte_mask(keep, 2);
+                    w.w &= byte_mask(keep, 3);
+                }
+                acc += (uint64_t)w.x + w.y;
+                acc += (uint64_t)w.z + w.w;
+            }
+        }
+        const uint32_t s = fold64(row_sum(fold64(acc)));   // <= 16 * 0xffff before the outer fold
+        if (lane == 0) {
+            const uint32_t m = (start & 1) ? swap16(s) : s;   // odd start: P = swap16(fold(M))
+            const uint32_t t = fold64((uint64_t)pseudo<MODE>(p, i, len) + m);
+            p.out[i] = (uint16_t)~t;
+        }
+    }
+}
+
+hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, hipStream_t st) {
+    if (!p.n) return hipSuccess;
+    const uint64_t per_block = kThreads / kGroup;
+    uint64_t want = (p.n + per_block - 1) / per_block;
+    const uint64_t cap = (uint64_t)cus * 8;   // 32 waves per CU, persistent over the packets
+    const int grid = (int)(want < cap ? want : cap);
+#define INET_LAUNCH(V, M) hipLaunchKernelGGL((inet_kernel<V, M>), dim3(grid), dim3(kThreads), 0, st, p)
+    if (var) {
+        if (mode == kTcp) INET_LAUNCH(true, kTcp);
+        else if (mode == kUdp) INET_LAUNCH(true, kUdp);
+        else INET_LAUNCH(true, kIp);
+    } else {
+        if (mode == kTcp) INET_LAUNCH(false, kTcp);
+        else if (mode == kUdp) INET_LAUNCH(false, kUdp);
+        else INET_LAUNCH(false, kIp);
+    }
+#undef INET_LAUNCH
+    return hipGetLastError();
+}
+
+}  // namespace inet

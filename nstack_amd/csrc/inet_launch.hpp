@@ -1,0 +1,26 @@
+// inet_launch.hpp — host-side launcher of the Internet-checksum kernel (inet_kernel.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace inet {
+
+// Modes = the reference function whose return value out[i] reproduces (include/nstack_inet.h).
+constexpr int kIp = 0;    // ip_checksum   src/ip.c:39-62
+constexpr int kTcp = 1;   // tcp_checksum  src/tcp.c:167-213
+constexpr int kUdp = 2;   // udp_checksum  src/udp.c:136-174
+
+struct IParams {
+    uint64_t base;          // fixed: packet 0 start; var: arena start
+    uint64_t stride;        // fixed only
+    const uint64_t *off;    // var only
+    const uint32_t *len;    // var only
+    const uint32_t *addr;   // tcp/udp: (src, dst) per packet
+    uint16_t *out;
+    uint64_t n;
+    uint32_t flen;          // fixed: packet length
+};
+
+hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, hipStream_t st);
+
+}  // namespace inet

@@ -1,0 +1,149 @@
+/*
+ * oracle/inet_oracle.c — TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
+ *
+ * Only tests/ may load this. The product library (nstack_amd/libnstack_fcs.so) computes every
+ * Internet checksum in its HIP kernel (nstack_amd/csrc/inet_kernel.hip) and has no CPU path.
+ *
+ * What it restates, loop for loop:
+ *   ip_checksum(dp, bsize)               /root/reference/src/ip.c:39-62
+ *     acc = 0xffff (:42); 16-bit words read with memcpy in HOST byte order (:47), added with an
+ *     end-around carry "if (acc > 0xffff) acc -= 0xffff" (:48-50); an odd trailing byte is the
+ *     low byte of a zeroed word (:53-58); return ~acc truncated to 16 bits (:61).
+ *     Also the ICMP checksum (src/icmp.c:42,74 call ip_checksum).
+ *   tcp_checksum(src, dst, dp, bsize)    /root/reference/src/tcp.c:167-213
+ *     the same loop (acc = 0xffff) first over the 12-byte packed pseudo header
+ *     {htonl(src), htonl(dst), 0, IP_PROTO_TCP = 6, htons(bsize)} (:176-188, :190-195), then over
+ *     the segment (:197-209). src/dst are host-order IPv4 addresses (nstack_sockaddr.inet4_addr).
+ *   udp_checksum(buff, len, src, dst)    /root/reference/src/udp.c:136-174 (static)
+ *     sum = 0 (:146), u16 words in host order (:148), "if (sum & 0x80000000) fold" inside the
+ *     loop (:150-151), odd byte added as a low byte (:156-157), then the two halves of the raw
+ *     in_addr_t src and dst as they lie in memory (:143,160-164), htons(IPPROTO_UDP) (:166),
+ *     htons(len) (:167); fold while (sum >> 16) (:170-171); return ~sum (:174).
+ *
+ * Pinning: the reference's src/ip.c / src/tcp.c / src/udp.c could not be built here (the
+ * request to compile src/ip.c was refused), and the reference's tests hold no
+ * checksum fixture. tests/test_inet_oracle.py therefore pins this restatement to published
+ * known answers (the RFC 1071 §3 numeric example, a textbook IPv4 header) and to an
+ * independent big-endian formulation of RFC 1071 in tests/golden/make_inet_golden.py. Parity
+ * with the reference's own functions is "unpinned" in the sense of the task statement: no
+ * output of the reference itself backs these vectors.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+
+static uint16_t bswap16(uint16_t x) { return (uint16_t)((x << 8) | (x >> 8)); }
+static uint32_t bswap32(uint32_t x)
+{
+    return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+}
+
+/* src/ip.c:39-62 (this container is little-endian x86-64, like the reference's targets). */
+uint16_t oracle_ip_checksum(const void *dp, size_t bsize)
+{
+    const uint8_t *data = (const uint8_t *) dp;
+    uint32_t acc = 0xffff;
+    uint16_t word;
+    size_t i;
+
+    for (i = 0; i + 1 < bsize; i += 2) {
+        memcpy(&word, data + i, 2);
+        acc += word;
+        if (acc > 0xffff)
+            acc -= 0xffff; /* ntohs(0xffff) == 0xffff */
+    }
+    if (bsize & 1) {
+        word = 0;
+        memcpy(&word, data + bsize - 1, 1);
+        acc += word;
+        if (acc > 0xffff)
+            acc -= 0xffff;
+    }
+    return (uint16_t) ~acc;
+}
+
+/* src/tcp.c:167-213; src/dst in host order. */
+uint16_t oracle_tcp_checksum(uint32_t src, uint32_t dst, const void *dp, size_t bsize)
+{
+    const uint8_t *data = (const uint8_t *) dp;
+    uint32_t acc = 0xffff;
+    uint16_t word;
+    size_t i;
+    uint8_t ph[12];
+    const uint32_t s = bswap32(src), d = bswap32(dst); /* htonl */
+    const uint16_t l = bswap16((uint16_t) bsize);       /* htons(bsize) truncates to 16 bits */
+
+    memcpy(ph, &s, 4);
+    memcpy(ph + 4, &d, 4);
+    ph[8] = 0;
+    ph[9] = 6; /* IP_PROTO_TCP */
+    memcpy(ph + 10, &l, 2);
+
+    for (i = 0; i + 1 < 12; i += 2) {
+        memcpy(&word, ph + i, 2);
+        acc += word;
+        if (acc > 0xffff)
+            acc -= 0xffff;
+    }
+    for (i = 0; i + 1 < bsize; i += 2) {
+        memcpy(&word, data + i, 2);
+        acc += word;
+        if (acc > 0xffff)
+            acc -= 0xffff;
+    }
+    if (bsize & 1) {
+        word = 0;
+        memcpy(&word, data + bsize - 1, 1);
+        acc += word;
+        if (acc > 0xffff)
+            acc -= 0xffff;
+    }
+    return (uint16_t) ~acc;
+}
+
+/* src/udp.c:136-174; src/dst are the raw in_addr_t values the caller passes. */
+uint16_t oracle_udp_checksum(const void *buff, size_t len, uint32_t src, uint32_t dst)
+{
+    const uint8_t *buf = (const uint8_t *) buff;
+    uint16_t ip_src[2], ip_dst[2], w;
+    uint32_t sum = 0;
+    size_t length = len;
+
+    memcpy(ip_src, &src, 4);
+    memcpy(ip_dst, &dst, 4);
+    while (len > 1) {
+        memcpy(&w, buf, 2);
+        buf += 2;
+        sum += w;
+        if (sum & 0x80000000u)
+            sum = (sum & 0xFFFF) + (sum >> 16);
+        len -= 2;
+    }
+    if (len & 1)
+        sum += *buf;
+    sum += ip_src[0];
+    sum += ip_src[1];
+    sum += ip_dst[0];
+    sum += ip_dst[1];
+    sum += bswap16(17);               /* htons(IPPROTO_UDP) */
+    sum += bswap16((uint16_t) length); /* htons(length) */
+    while (sum >> 16)
+        sum = (sum & 0xFFFF) + (sum >> 16);
+    return (uint16_t) ~sum;
+}
+
+/* Batch helper with the product's argument convention: mode 0 = ip, 1 = tcp, 2 = udp; addr holds
+ * (src, dst) per packet for tcp/udp (NULL for ip). Packet i = arena[off[i] .. off[i] + len[i]). */
+void oracle_inet_batch(int mode, const uint8_t *arena, const uint64_t *off, const uint32_t *len,
+                       const uint32_t *addr, uint16_t *out, size_t n)
+{
+    for (size_t i = 0; i < n; i++) {
+        const uint8_t *p = arena + off[i];
+        if (mode == 1)
+            out[i] = oracle_tcp_checksum(addr[2 * i], addr[2 * i + 1], p, len[i]);
+        else if (mode == 2)
+            out[i] = oracle_udp_checksum(p, len[i], addr[2 * i], addr[2 * i + 1]);
+        else
+            out[i] = oracle_ip_checksum(p, len[i]);
+    }
+}

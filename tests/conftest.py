@@ -59,3 +59,30 @@ def var_kernel(request):
     old = na.set_var_threshold((1 << 63) if request.param == "quarter" else 0)
     yield request.param
     na.set_var_threshold(old)
+
+
+@pytest.fixture(scope="session")
+def inet_oracle():
+    """CPU restatement of ip_checksum / tcp_checksum / udp_checksum (test infrastructure only)."""
+    so = os.path.join(ROOT, "oracle", "_build", "liboracle_inet.so")
+    if not os.path.exists(so):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle"), "all"], check=True)
+    L = ctypes.CDLL(so)
+    u16, u32, vp, sz = ctypes.c_uint16, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t
+    L.oracle_ip_checksum.restype = u16
+    L.oracle_ip_checksum.argtypes = [vp, sz]
+    L.oracle_tcp_checksum.restype = u16
+    L.oracle_tcp_checksum.argtypes = [u32, u32, vp, sz]
+    L.oracle_udp_checksum.restype = u16
+    L.oracle_udp_checksum.argtypes = [vp, sz, u32, u32]
+    L.oracle_inet_batch.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, sz]
+    return L
+
+
+@pytest.fixture(scope="session")
+def inet_golden():
+    with open(os.path.join(GOLDEN, "inet_vectors.json")) as f:
+        vec = json.load(f)
+    with open(os.path.join(GOLDEN, vec["arena"]), "rb") as f:
+        vec["arena_bytes"] = f.read()
+    return vec

@@ -1,5 +1,6 @@
 """The C-ABI boundary: the product library loads, exports exactly what include/*.h declare
-(nstack_fcs.h: the FCS engine; nstack_txq.h: the batched TX call site), and (without a GPU)
+(nstack_fcs.h: the FCS engine; nstack_txq.h: the batched TX call site; nstack_pcap.h;
+nstack_inet.h: the opt-in Internet checksums), and (without a GPU)
 refuses to compute instead of falling back to the CPU."""
 import ctypes
 import os
@@ -12,7 +13,7 @@ import nstack_amd as na
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "nstack_fcs.h")
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("nstack_fcs.h", "nstack_txq.h", "nstack_pcap.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("nstack_fcs.h", "nstack_txq.h", "nstack_pcap.h", "nstack_inet.h")]
 
 
 def _declared():
@@ -87,3 +88,32 @@ def test_dropin_aborts_without_gpu():
     p = subprocess.run(["python", "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=120)
     assert p.returncode != 0
     assert "no usable GPU engine" in p.stderr
+
+
+def test_inet_signatures_mirror_reference_functions():
+    # src/ip.c:39, src/tcp.c:167-170, src/udp.c:136-139 (argument meaning kept, names prefixed:
+    # ip.c stays linked in nstack, so the GPU forms cannot reuse its global symbol)
+    src = open(os.path.join(ROOT, "include", "nstack_inet.h")).read()
+    assert re.search(r"uint16_t\s+inet_ip_checksum\(const void \*dp, size_t bsize\);", src)
+    assert re.search(r"uint16_t\s+inet_tcp_checksum\(uint32_t src, uint32_t dst, const void \*dp, size_t bsize\);", src)
+    assert re.search(r"uint16_t\s+inet_udp_checksum\(const void \*dp, size_t len, uint32_t src, uint32_t dst\);", src)
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")
+def test_inet_fails_loudly_without_gpu():
+    import numpy as np
+    lib = na.load()
+    arena = np.zeros(64, dtype=np.uint8)
+    off = np.zeros(1, dtype=np.uint64)
+    ln = np.full(1, 20, dtype=np.uint32)
+    out = np.zeros(1, dtype=np.uint16)
+    assert lib.inet_csum_batch_host(0, arena.ctypes.data, 64, off.ctypes.data, ln.ctypes.data, None,
+                                    out.ctypes.data, 1) == -19
+    assert lib.inet_csum_batch_host(7, arena.ctypes.data, 64, off.ctypes.data, ln.ctypes.data, None,
+                                    out.ctypes.data, 1) == -22   # unknown mode
+    assert lib.inet_csum_batch_host(1, arena.ctypes.data, 64, off.ctypes.data, ln.ctypes.data, None,
+                                    out.ctypes.data, 1) == -22   # tcp needs addresses
+    assert lib.inet_csum_fixed_dev(0, ctypes.c_void_p(64), 20, 20, 1, None, ctypes.c_void_p(64), None) == -19
+    p = subprocess.run(["python", "-c", "import nstack_amd as na; na.ip_checksum(bytes(20))"],
+                       capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert p.returncode != 0 and "no usable GPU engine" in p.stderr
