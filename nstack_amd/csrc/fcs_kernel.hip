@@ -42,7 +42,11 @@ constexpr int kSingleMaskWords = 8;                // SINGLE variant: front-lane
 // LDS wait drain the prefetched chunk loads.
 template <typename T>
 __device__ __forceinline__ T gload(uint64_t addr) {
+#ifdef FCS_NT   // measurement-only build: non-temporal (nt) frame loads
+    return __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) T *>(addr));
+#else
     return *reinterpret_cast<const __attribute__((address_space(1))) T *>(addr);
+#endif
 }
 
 // a ^ b ^ c in one VALU op: gfx950's v_bitop3_b32 with truth table 0x96.
@@ -889,8 +893,10 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4 *__restric
     uint32_t acc = 0;
     const uint64_t st = (uint64_t)gridDim.x * blockDim.x;
     uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t pb = (uint64_t)p;
     for (; i + 3 * st < n16; i += 4 * st) {
-        const u32x4 a = p[i], b = p[i + st], c = p[i + 2 * st], e = p[i + 3 * st];
+        const u32x4 a = gload<u32x4>(pb + 16 * i), b = gload<u32x4>(pb + 16 * (i + st)),
+                    c = gload<u32x4>(pb + 16 * (i + 2 * st)), e = gload<u32x4>(pb + 16 * (i + 3 * st));
         acc ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ e.x ^ e.y ^
                e.z ^ e.w;
     }

@@ -39,7 +39,11 @@ constexpr int kThreads = 256;
 
 template <typename T>
 __device__ __forceinline__ T gload(uint64_t addr) {
+#ifdef FCS_NT   // measurement-only build: non-temporal (nt) packet loads
+    return __builtin_nontemporal_load(reinterpret_cast<const __attribute__((address_space(1))) T *>(addr));
+#else
     return *reinterpret_cast<const __attribute__((address_space(1))) T *>(addr);
+#endif
 }
 
 __device__ __forceinline__ uint32_t swap16(uint32_t x) { return ((x & 0xffu) << 8) | ((x >> 8) & 0xffu); }
@@ -81,49 +85,100 @@ __device__ __forceinline__ uint32_t pseudo(const IParams &p, uint64_t i, uint32_
     return (s & 0xffffu) + (s >> 16) + (d & 0xffffu) + (d >> 16) + 0x1100u + l16;
 }
 
+// One packet's geometry.
+struct Pkt {
+    uint64_t start, c0;   // first byte; its 16-byte aligned chunk
+    uint32_t len, nch;    // bytes; 16-byte chunks touched (0 for an empty packet)
+};
+
+template <bool VAR>
+__device__ __forceinline__ Pkt packet(const IParams &p, uint64_t i, uint64_t off, uint32_t len) {
+    Pkt k;
+    k.start = VAR ? p.base + off : p.base + i * p.stride;
+    k.len = VAR ? len : p.flen;
+    k.c0 = k.start & ~15ull;
+    const uint64_t end = k.start + k.len;
+    k.nch = k.len ? (uint32_t)((((end + 15) & ~15ull) - k.c0) >> 4) : 0u;
+    return k;
+}
+
+// Issue the loads of round k0 of packet k. Lanes past the packet's last chunk re-read that chunk
+// (an L1/L2 hit; zeroed in accumulate): unconditional loads from one base keep the round's
+// six loads back to back. An empty packet loads nothing.
+__device__ __forceinline__ void issue(const Pkt &k, uint32_t k0, uint32_t lane, u32x4 (&v)[kRound]) {
+    if (k.nch == 0) return;
+#pragma unroll
+    for (int j = 0; j < kRound; j++) {
+        const uint32_t c = k0 + lane + kGroup * j;
+        v[j] = gload<u32x4>(k.c0 + 16ull * (c < k.nch ? c : k.nch - 1));
+    }
+}
+
+// Add round k0 of packet k into acc (only the packet's first and last chunk are masked).
+__device__ __forceinline__ void accumulate(const Pkt &k, uint32_t k0, uint32_t lane, const u32x4 (&v)[kRound],
+                                           uint64_t &acc) {
+#pragma unroll
+    for (int j = 0; j < kRound; j++) {
+        const uint32_t c = k0 + lane + kGroup * j;
+        if (c >= k.nch) continue;
+        u32x4 w = v[j];
+        if (c == 0 || c + 1 == k.nch) {   // edge chunks: keep bytes in [start, end)
+            const uint64_t ca = k.c0 + 16ull * c, end = k.start + k.len;
+            const uint32_t lo = k.start > ca ? (uint32_t)(k.start - ca) : 0u;
+            const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
+            const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+            w.x &= byte_mask(keep, 0);
+            w.y &= byte_mask(keep, 1);
+            w.z &= byte_mask(keep, 2);
+            w.w &= byte_mask(keep, 3);
+        }
+        acc += (uint64_t)w.x + w.y;
+        acc += (uint64_t)w.z + w.w;
+    }
+}
+
+// Software-pipelined per group of 16 lanes: while packet i is reduced, the loads of the group's
+// next packet are in flight and (variable batches) the offset/length of the one after that.
 template <bool VAR, int MODE>
 __global__ __launch_bounds__(kThreads) void inet_kernel(IParams p) {
     const uint32_t lane = threadIdx.x & (kGroup - 1);
     const uint64_t ngrp = ((uint64_t)gridDim.x * kThreads) / kGroup;
-    for (uint64_t i = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / kGroup; i < p.n; i += ngrp) {
-        const uint64_t start = VAR ? p.base + p.off[i] : p.base + i * p.stride;
-        const uint32_t len = VAR ? p.len[i] : p.flen;
-        const uint64_t end = start + len;
-        const uint64_t c0 = start & ~15ull;
-        const uint32_t nch = len ? (uint32_t)((((end + 15) & ~15ull) - c0) >> 4) : 0u;
+    uint64_t i = ((uint64_t)blockIdx.x * kThreads + threadIdx.x) / kGroup;
+    if (i >= p.n) return;   // whole groups leave together
+    auto meta_off = [&](uint64_t q) -> uint64_t { return VAR && q < p.n ? p.off[q] : 0ull; };
+    auto meta_len = [&](uint64_t q) -> uint32_t { return VAR && q < p.n ? p.len[q] : 0u; };
+    Pkt cur = packet<VAR>(p, i, meta_off(i), meta_len(i));
+    uint64_t noff = meta_off(i + ngrp);
+    uint32_t nlen = meta_len(i + ngrp);
+    u32x4 va[kRound], vb[kRound];
+    issue(cur, 0, lane, va);
+    // one packet: its round-0 chunks are in `v`; the next packet's go into `w`. Returns false
+    // after the group's last packet. (Two copies with the buffers swapped: no register moves.)
+    auto step = [&](u32x4 (&v)[kRound], u32x4 (&w)[kRound]) -> bool {
+        const uint64_t inext = i + ngrp;
+        const bool more = inext < p.n;
+        Pkt nxt = packet<VAR>(p, inext, noff, nlen);
+        if (!more) nxt.nch = 0;
+        noff = meta_off(inext + ngrp);   // two packets ahead
+        nlen = meta_len(inext + ngrp);
+        issue(nxt, 0, lane, w);          // one packet ahead
         uint64_t acc = 0;
-        for (uint32_t k0 = 0; k0 < nch; k0 += kGroup * kRound) {
-            u32x4 v[kRound];
-#pragma unroll
-            for (int j = 0; j < kRound; j++) {
-                const uint32_t k = k0 + lane + kGroup * j;
-                v[j] = gload<u32x4>(c0 + 16ull * (k < nch ? k : nch - 1));   // idle lanes re-read the last chunk
-            }
-#pragma unroll
-            for (int j = 0; j < kRound; j++) {
-                const uint32_t k = k0 + lane + kGroup * j;
-                if (k >= nch) continue;
-                u32x4 w = v[j];
-                if (k == 0 || k == nch - 1) {   // the packet's edge chunks: keep bytes in [start, end)
-                    const uint64_t ca = c0 + 16ull * k;
-                    const uint32_t lo = start > ca ? (uint32_t)(start - ca) : 0u;
-                    const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
-                    const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-                    w.x &= byte_mask(keep, 0);
-                    w.y &= byte_mask(keep, 1);
-                    w.z &= byte_mask(keep, 2);
-                    w.w &= byte_mask(keep, 3);
-                }
-                acc += (uint64_t)w.x + w.y;
-                acc += (uint64_t)w.z + w.w;
-            }
+        accumulate(cur, 0, lane, v, acc);
+        for (uint32_t k0 = kGroup * kRound; k0 < cur.nch; k0 += kGroup * kRound) {   // > 1536 B
+            issue(cur, k0, lane, v);
+            accumulate(cur, k0, lane, v, acc);
         }
         const uint32_t s = fold64(row_sum(fold64(acc)));   // <= 16 * 0xffff before the outer fold
         if (lane == 0) {
-            const uint32_t m = (start & 1) ? swap16(s) : s;   // odd start: P = swap16(fold(M))
-            const uint32_t t = fold64((uint64_t)pseudo<MODE>(p, i, len) + m);
+            const uint32_t m = (cur.start & 1) ? swap16(s) : s;   // odd start: P = swap16(fold(M))
+            const uint32_t t = fold64((uint64_t)pseudo<MODE>(p, i, cur.len) + m);
             p.out[i] = (uint16_t)~t;
         }
+        i = inext;
+        cur = nxt;
+        return more;
+    };
+    while (step(va, vb) && step(vb, va)) {
     }
 }
 

@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--len", type=int, default=1518)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--what", default="fcs", help="comma list of fcs,stream,inet (inet: ip_checksum, fixed)")
     ap.add_argument("--imix", action="store_true",
                     help="variable-length path: --frames IMIX frames (7:4:1 of 64/576/1518, shuffled)")
     a = ap.parse_args()
@@ -35,6 +36,12 @@ def main():
                                             ctypes.c_void_p, ctypes.c_void_p]
         lib.ether_fcs_batch_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
+        lib.fcs_read_stream_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        lib.inet_csum_fixed_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+        lib.inet_csum_batch_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64,
+                                            ctypes.c_void_p]
         lib.fcs_fill_splitmix64_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_void_p]
         libs.append(lib)
@@ -50,30 +57,43 @@ def main():
         total = n * L
     arena = torch.empty(total, dtype=torch.uint8, device=dev)
     libs[0].fcs_fill_splitmix64_dev(arena.data_ptr(), total, 11, 0, None)
-    outs = [torch.empty(n, dtype=torch.int32, device=dev) for _ in libs]
+    outs = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in libs]
+    sink = torch.zeros(4, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream()
-    times = [[] for _ in libs]
-    for r in range(a.rounds + 1):
-        for i, lib in enumerate(libs):
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record(st)
-            for _ in range(a.reps):
-                if a.imix:
-                    rc = lib.ether_fcs_batch_dev(arena.data_ptr(), total, off.data_ptr(), ln.data_ptr(),
-                                                 outs[i].data_ptr(), n, st.cuda_stream)
-                else:
-                    rc = lib.ether_fcs_fixed_dev(arena.data_ptr(), L, L, n, outs[i].data_ptr(), st.cuda_stream)
-                assert rc == 0, rc
-            e1.record(st)
-            torch.cuda.synchronize()
-            if r:
-                times[i].append(e0.elapsed_time(e1) / a.reps)
-    for i, p in enumerate(a.libs):
-        med, mn = statistics.median(times[i]), min(times[i])
-        same = bool(torch.equal(outs[i], outs[0]))
-        print(f"{os.path.basename(p):28s} median {med:8.3f} ms  min {mn:8.3f} ms  "
-              f"{total / med / 1e6:8.1f} GB/s  same_as_first={same}")
+    whats = a.what.split(",")
+    times = {(w, i): [] for w in whats for i in range(len(libs))}
 
+    def launch(w, i, lib):
+        if w == "stream":
+            return lib.fcs_read_stream_dev(arena.data_ptr(), total, sink.data_ptr(), st.cuda_stream)
+        if w == "inet" and a.imix:
+            return lib.inet_csum_batch_dev(0, arena.data_ptr(), total, off.data_ptr(), ln.data_ptr(), None,
+                                           outs[i].data_ptr(), n, st.cuda_stream)
+        if w == "inet":
+            return lib.inet_csum_fixed_dev(0, arena.data_ptr(), L, L, n, None, outs[i].data_ptr(), st.cuda_stream)
+        if a.imix:
+            return lib.ether_fcs_batch_dev(arena.data_ptr(), total, off.data_ptr(), ln.data_ptr(),
+                                           outs[i].data_ptr(), n, st.cuda_stream)
+        return lib.ether_fcs_fixed_dev(arena.data_ptr(), L, L, n, outs[i].data_ptr(), st.cuda_stream)
+
+    res = {}
+    for w in whats:
+        for r in range(a.rounds + 1):
+            for i, lib in enumerate(libs):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(st)
+                for _ in range(a.reps):
+                    rc = launch(w, i, lib)
+                    assert rc == 0, rc
+                e1.record(st)
+                torch.cuda.synchronize()
+                if r:
+                    times[(w, i)].append(e0.elapsed_time(e1) / a.reps)
+        for i, p in enumerate(a.libs):
+            med, mn = statistics.median(times[(w, i)]), min(times[(w, i)])
+            same = bool(torch.equal(outs[i], outs[0])) if w != "stream" else None
+            print(f"{w:6s} {os.path.basename(p):28s} median {med:8.3f} ms  min {mn:8.3f} ms  "
+                  f"{total / med / 1e6:8.1f} GB/s  same_as_first={same}", flush=True)
 
 if __name__ == "__main__":
     main()

@@ -9,7 +9,7 @@ mkdir -p "$HERE/variants"
 while [ $# -ge 2 ]; do
   name=$1; flags=$2; shift 2
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared $flags \
-     -o "$HERE/variants/libfcs_$name.so" "$ROOT/nstack_amd/csrc/fcs_kernel.hip" "$ROOT"/nstack_amd/csrc/*.cpp -lpthread 2>/dev/null &
+     -o "$HERE/variants/libfcs_$name.so" "$ROOT/nstack_amd/csrc/fcs_kernel.hip" "$ROOT/nstack_amd/csrc/inet_kernel.hip" "$ROOT"/nstack_amd/csrc/*.cpp -lpthread 2>/dev/null &
 done
 wait
 ls "$HERE/variants"
