@@ -540,8 +540,8 @@ extern "C" {
 const char *fcs_last_error(void) { return g_last_error.c_str(); }
 
 const char *fcs_engine_version(void) {
-    return "nstack-fcs 0.2 gfx950: quarter-wave/frame, 96B lane chunks as 2 chains, slice-by-4 "
-           "LDS x32 replicas, v_perm addressing, DPP reduce";
+    return "nstack-fcs 0.3 gfx950: quarter-wave/frame, 96B lane chunks as 2 chains, slice-by-4 "
+           "LDS x32 replicas, v_perm addressing, DPP reduce; var: flat chunk stream per 64-frame window";
 }
 
 int fcs_engine_init(int ndev) {

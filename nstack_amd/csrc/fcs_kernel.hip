@@ -398,7 +398,25 @@ __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
     }
     const uint32_t *src = p.blob + kBlobLane;
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
-    for (int i = tid; i < (int)(kBlobWords - kBlobLane); i += kWgThreads) dst[i] = src[i];
+    for (int i = tid; i < (int)(kBlobFlat - kBlobLane); i += kWgThreads) dst[i] = src[i];
+    __syncthreads();
+}
+
+// Flat variable-length kernel staging: the same data and uniform tables, and the chunk-shift
+// tables C_c in place of the per-lane tables.
+__device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds) {
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 8192; i += kWgThreads) {
+        const int h = i >> 12, b = (i >> 4) & 255, odd = (i >> 3) & 1;
+        const int k = h == 0 ? (odd ? 2 : 3) : (odd ? 0 : 1);
+        const uint32_t v = p.blob[kBlobSlice + 256 * k + b];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
+    }
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsJump);
+    for (int i = tid; i < (int)(kBlobFlat - kBlobJump); i += kWgThreads) dst[i] = p.blob[kBlobJump + i];
+    uint32_t *fl = reinterpret_cast<uint32_t *>(lds + kLdsFlat);
+    for (int i = tid; i < (int)(kFlatBytes / 4); i += kWgThreads) fl[i] = p.blob[kBlobFlat + i];
     __syncthreads();
 }
 
@@ -638,7 +656,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
 
 
 // ---------------------------------------------------------------------------------------------
-// Variable-length frames (IMIX-shaped batches): windowed class scheduling.
+// Variable-length frames (IMIX-shaped batches): windowed class scheduling. Superseded by
+// fcs_flat_kernel below (+16 % on IMIX); kept as the measurement baseline (-DFCS_VAR_HALFUNIT).
 // A wave owns windows of 64 consecutive frames (frame i of a window <-> lane i for metadata).
 // The window's frames are split by length into classes that use lanes differently:
 //   small  (len <= 96):  the owning lane alone processes the frame as one chunk (chunk 0, no
@@ -850,6 +869,163 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
     flush_bad(p, lds);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Variable-length frames, flat chunk stream (fcs_flat_kernel).
+// A wave owns windows of 64 consecutive frames. Every frame of at most 1536 bytes needs
+// k = ceil(len / 96) chunks (an empty frame one dummy chunk); the window's chunks are numbered
+// frame by frame (exclusive prefix P over the window) and dealt to the lanes 64 at a time, so
+// every lane of an item carries a real chunk whatever the mix of lengths (a 576-B frame takes
+// 6 lanes, not 8; small, medium and full frames pack without gaps). Per item a lane finds its
+// frame from the frame-start marks (one LDS byte per chunk slot, a ballot and a popcount),
+// computes its chunk's register exactly as the other kernels do, shifts it by A_{96c} for its
+// chunk index c (tables indexed by c, stride 4 mod 64 banks) and XORs it into the frame's LDS
+// accumulator (ds_xor). At the end of the window lane i stores frame i's FCS: one coalesced
+// store per window. Frames over 1536 bytes take the segment loop of fcs_var_kernel.
+// ---------------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t chunk_shift(const uint8_t *lds, uint32_t s, uint32_t c) {
+    uint32_t r[8];
+    const uint32_t base = kLdsFlat + c * kFlatStride;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        r[t] = lds_rd(lds, base + (sh & 0x3Cu) + t * 64);
+    }
+    return xor9(r, 0u);
+}
+
+template <bool TINY>
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    stage_tables_flat(p, lds);
+    init_bad(lds);
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int j = lane & (kGroup - 1);
+    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
+    const uint32_t base0 = r4, base1 = 0x10000u | r4;
+    uint32_t *acc = reinterpret_cast<uint32_t *>(lds + kLdsWave + wave * kLdsWaveBytes);   // 64 frames
+    uint8_t *mark = lds + kLdsFlatMark + wave * 64;
+    uint8_t *list = lds + kLdsFlatList + wave * 64;
+    acc[lane] = 0u;
+    mark[lane] = 0;
+    const uint64_t GW = (uint64_t)gridDim.x * (kWgThreads / 64);
+
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kWgThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
+        // ---- window metadata: lane i <-> frame w0 + i ----
+        const uint64_t f = w0 + lane;
+        const bool act = f < p.n;
+        const uint32_t L = act ? p.len[f] : 0u;
+        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;
+        const bool multi = act && L > (uint32_t)kSegBytes;
+        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
+        uint32_t incl = k;   // inclusive prefix over the window
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t P = incl - k;
+        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+        const uint64_t fmask = __ballot(k != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+        if (k) list[rank] = (uint8_t)lane;
+        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
+
+        // one item = 64 chunks; resolve lane -> (frame, chunk) and issue its loads
+        struct FlatItem {
+            Chunk ch;
+            int src, zr;
+            uint32_t c;
+            bool valid;
+        };
+        auto prep = [&](uint32_t g0, uint32_t tag, FlatItem &it) {
+            // frame starts inside this item: mark their slot, then lane g finds its frame's rank
+            // as (frames started before the item) + (marks at or below g) - 1
+            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = (uint8_t)tag;
+            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
+            const uint64_t M = __ballot(mark[lane] == (uint8_t)tag);
+            const uint32_t g = g0 + (uint32_t)lane;
+            it.valid = g < K;
+            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
+            it.src = it.valid ? (int)list[rk & 63u] : 0;
+            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, it.src) << 32) | (uint32_t)__shfl((int)Elo, it.src);
+            const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
+            const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
+            it.c = it.valid ? g - Pg : 0u;   // chunk index back from the frame end
+            const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
+            it.zr = it.valid ? clamp_zr((int64_t)(Eg - Lg) - cstart) : kChunkBytes;
+            issue_any<TINY>(p, cstart, it.valid && it.zr < kChunkBytes, it.ch);
+        };
+        auto finish = [&](const FlatItem &it) {
+            const uint32_t own = chunk_value<TINY>(lds, it.ch, it.zr, it.valid ? inv_start(lds, it.zr) : 0u, base0, base1);
+            const uint32_t v = chunk_shift(lds, own, it.c & 15u);
+            if (it.valid && v) atomicXor(&acc[it.src], v);
+        };
+#ifdef FCS_FLAT_PIPE   // measurement-only build: the next item's loads in flight during this one
+        if (K) {
+            FlatItem A, B;
+            prep(0, 1, A);
+            uint32_t g0 = 64, tag = 2;
+            while (true) {
+                if (g0 >= K) { finish(A); break; }
+                prep(g0, tag, B);
+                finish(A);
+                g0 += 64; tag++;
+                if (g0 >= K) { finish(B); break; }
+                prep(g0, tag, A);
+                finish(B);
+                g0 += 64; tag++;
+            }
+        }
+#else
+        for (uint32_t g0 = 0, tag = 1; g0 < K; g0 += 64, tag++) {
+            FlatItem it;
+            prep(g0, tag, it);
+            finish(it);
+        }
+#endif
+
+        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment ----
+        const uint64_t xmask = __ballot(multi);
+        const uint32_t nx = (uint32_t)__popcll(xmask);
+        if (nx) {
+            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
+            if (multi) mark[rx] = (uint8_t)lane;   // the marks are free again: reuse them as the multi list
+            for (uint32_t t = 0; t < nx; t += 4) {
+                const uint32_t rnk = t + (uint32_t)(lane >> 4);
+                const bool valid = rnk < nx;
+                const int src = valid ? (int)mark[rnk] : 0;
+                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
+                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
+                uint32_t s = 0;
+                for (uint32_t q = 0; __any(q < m); q++) {
+                    const bool on = q < m;
+                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
+                                           (int64_t)kChunkBytes * (j + 1);
+                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
+                    Chunk cc;
+                    issue_any<TINY>(p, cstart, on && zr < kChunkBytes, cc);
+                    const uint32_t r = chunk_value<TINY>(lds, cc, zr, (on && q == 0) ? inv_start(lds, zr) : 0u,
+                                                         base0, base1);
+                    s = on ? (q == 0 ? r : uniform_shift<kLdsJump>(lds, s, r)) : s;
+                }
+                const uint32_t v = row_xor(chunk_shift(lds, s, (uint32_t)j));
+                if (valid && j == 15) acc[src] = v;
+            }
+            if (multi) mark[rx] = 0;
+        }
+
+        // ---- one coalesced store per window; clear the window state ----
+        const uint32_t a = acc[lane];
+        emit(p, lds, act, f, L ? ~a : 0u);
+        acc[lane] = 0u;
+        mark[lane] = 0;
+    }
+    flush_bad(p, lds);
+}
+
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
     x += 0x9E3779B97F4A7C15ull;
@@ -932,15 +1108,23 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #define FCS_LAUNCH(V, T, S) \
     hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kWgThreads), 0, st, p)
     if (var) {
-        // windowed: throughput form (64-frame windows per wave, length classes);
+        // windowed: throughput form (64-frame windows per wave, chunks dealt flat to the lanes);
         // otherwise one quarter-wave per frame, every frame in flight at once (small batches)
         if (!windowed) {
             if (tiny) FCS_LAUNCH(true, true, false);
             else FCS_LAUNCH(true, false, false);
         } else if (tiny) {
+#ifdef FCS_VAR_HALFUNIT   // measurement-only build: the half-unit windowed kernel it replaced
             hipLaunchKernelGGL((fcs_var_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
+#else
+            hipLaunchKernelGGL((fcs_flat_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
+#endif
         } else {
+#ifdef FCS_VAR_HALFUNIT
             hipLaunchKernelGGL((fcs_var_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+#else
+            hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+#endif
         }
     } else if (tiny) {
         if (single) FCS_LAUNCH(false, true, true);

@@ -17,6 +17,9 @@
 //                                                     zero bytes, equals the all-ones init)
 //   half-row fix  M   = A_{-768}                     (8-lane groups in lanes 8..15 of a row
 //                                                     used the lane tables of lanes 8..15)
+//   chunk shifts  C_c = A_{96 c}         c = 0..15   (flat variable-length kernel: a lane's
+//                                                     chunk index is data-dependent, so the
+//                                                     table is indexed by c, not by lane)
 // These are constants of the algorithm, computed once per process; no frame bytes are ever
 // checksummed on the host (the product has no CPU CRC path).
 #pragma once
@@ -49,6 +52,16 @@ constexpr uint32_t kLdsWave = 149888;   // per-wave scratch for the variable-len
 constexpr uint32_t kLdsWaveBytes = 256; //   (four 64-entry frame lists per wave)
 constexpr uint32_t kLdsBad = kLdsWave + 16 * kLdsWaveBytes;    // 153984: per-wave u64 failing-frame count (verify)
 constexpr uint32_t kLdsBytes = kLdsBad + 16 * 8;                // 154112
+// The flat variable-length kernel keeps C_c in the lane-table region instead (it never uses the
+// per-lane tables): nibble table t of C_c at kLdsFlat + c*kFlatStride + t*64 + e*4. The stride is
+// 132 dwords (== 4 mod 64 banks), so lanes with different c spread over the banks. Per-wave
+// frame-start marks and rank -> lane lists follow it.
+constexpr uint32_t kLdsFlat = kLdsLane;
+constexpr uint32_t kFlatStride = 528;
+constexpr uint32_t kFlatBytes = 16 * kFlatStride;              // 8448
+constexpr uint32_t kLdsFlatMark = kLdsFlat + kFlatBytes;        // 16 waves x 64 B
+constexpr uint32_t kLdsFlatList = kLdsFlatMark + 16 * 64;       // 16 waves x 64 B
+static_assert(kLdsFlatList + 16 * 64 <= kLdsJump, "flat scratch fits the lane-table region");
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
@@ -58,7 +71,8 @@ constexpr uint32_t kBlobH48 = kBlobJump + 8 * 16;       // uint32 [8][16]
 constexpr uint32_t kBlobH24 = kBlobH48 + 8 * 16;        // uint32 [8][16]
 constexpr uint32_t kBlobInv = kBlobH24 + 8 * 16;        // uint32 [96]
 constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
-constexpr uint32_t kBlobWords = kBlobM768 + 8 * 16;
+constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][132] (C_c, LDS order)
+constexpr uint32_t kBlobWords = kBlobFlat + kFlatBytes / 4;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -116,6 +130,11 @@ struct Tables {
         nibble_table(-768, nt);
         for (int t = 0; t < 8; t++)
             for (int e = 0; e < 16; e++) b[kBlobM768 + t * 16 + e] = nt[t][e];
+        for (int c = 0; c < 16; c++) {
+            nibble_table((long)kChunkBytes * c, nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobFlat + c * (kFlatStride / 4) + t * 16 + e] = nt[t][e];
+        }
         return b;
     }
 };
