@@ -57,6 +57,11 @@ int inet_csum_fixed_dev(int mode, const void *base, uint64_t stride, uint32_t le
 int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, const uint64_t *off,
                          const uint32_t *len, const uint32_t *addr, uint16_t *out, uint64_t n);
 
+/* Tuning: batches of more than `packets` packets use the flat kernel (packets dealt to lanes by
+ * size, for throughput), smaller ones one 16-lane group per packet (latency).
+ * Results are identical either way. Default 16384. Returns the previous value. */
+uint64_t inet_csum_set_flat_threshold(uint64_t packets);
+
 /* ---- single packet, same arguments and result as the reference functions ---- */
 uint16_t inet_ip_checksum(const void *dp, size_t bsize);                          /* ip.c:39  */
 uint16_t inet_tcp_checksum(uint32_t src, uint32_t dst, const void *dp, size_t bsize); /* tcp.c:167 */

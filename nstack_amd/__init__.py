@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -33,7 +33,7 @@ EXPORTS = [
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
     # include/nstack_inet.h — batched Internet checksums (opt-in)
-    "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_ip_checksum",
+    "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_csum_set_flat_threshold", "inet_ip_checksum",
     "inet_tcp_checksum", "inet_udp_checksum",
 ]
 
@@ -99,6 +99,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "inet_csum_batch_dev": (i32, [i32, vp, u64, vp, vp, vp, vp, u64, vp]),
         "inet_csum_fixed_dev": (i32, [i32, vp, u64, u32, u64, vp, vp, vp]),
         "inet_csum_batch_host": (i32, [i32, vp, u64, vp, vp, vp, vp, u64]),
+        "inet_csum_set_flat_threshold": (u64, [u64]),
         "inet_ip_checksum": (c.c_uint16, [vp, c.c_size_t]),
         "inet_tcp_checksum": (c.c_uint16, [u32, u32, vp, c.c_size_t]),
         "inet_udp_checksum": (c.c_uint16, [vp, c.c_size_t, u32, u32]),
@@ -326,6 +327,11 @@ def inet_fixed_dev(mode, base, stride: int, length: int, n: int, addr, out, stre
 def inet_batch_host(mode, arena, arena_bytes: int, off, length, addr, out, n: int) -> None:
     _check(load().inet_csum_batch_host(_mode(mode), _ptr(arena), arena_bytes, _ptr(off), _ptr(length),
                                        _ptr(addr), _ptr(out), n), "inet_csum_batch_host")
+
+
+def inet_set_flat_threshold(packets: int) -> int:
+    """Variable-length batches of more than `packets` packets use the flat kernel; returns the old value."""
+    return int(load().inet_csum_set_flat_threshold(packets))
 
 
 def ip_checksum(data) -> int:

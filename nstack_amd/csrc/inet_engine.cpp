@@ -8,6 +8,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -37,6 +38,8 @@ int hip_fail(hipError_t e, const char *what) {
         hipError_t e_ = (expr);                            \
         if (e_ != hipSuccess) return hip_fail(e_, what);   \
     } while (0)
+
+std::atomic<uint64_t> g_flat_min{16384};   // see inet_csum_set_flat_threshold
 
 int check_mode(int mode, const uint32_t *addr) {
     if (mode != INET_CSUM_IP && mode != INET_CSUM_TCP && mode != INET_CSUM_UDP)
@@ -164,7 +167,7 @@ int run_host(int mode, const uint8_t *arena, const uint64_t *off, const uint32_t
         p.addr = addr ? s.d_addr : nullptr;
         p.out = s.d_out;
         p.n = np;
-        HIPTRY(inet::launch_inet(true, mode, p, cus, st), "launching inet_kernel");
+        HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), st), "launching inet_kernel");
         HIPTRY(hipMemcpyAsync(s.h_out, s.d_out, np * 2, hipMemcpyDeviceToHost, st), "D2H checksums");
         HIPTRY(hipEventRecord(s.done, st), "hipEventRecord");
         s.live = true;
@@ -223,7 +226,7 @@ int inet_csum_batch_dev(int mode, const void *arena, uint64_t arena_bytes, const
     p.addr = addr;
     p.out = out;
     p.n = n;
-    HIPTRY(inet::launch_inet(true, mode, p, cus, (hipStream_t)stream), "launching inet_kernel<var>");
+    HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), (hipStream_t)stream), "launching inet_kernel<var>");
     return 0;
 }
 
@@ -242,7 +245,7 @@ int inet_csum_fixed_dev(int mode, const void *base, uint64_t stride, uint32_t le
     p.addr = addr;
     p.out = out;
     p.n = n;
-    HIPTRY(inet::launch_inet(false, mode, p, cus, (hipStream_t)stream), "launching inet_kernel<fixed>");
+    HIPTRY(inet::launch_inet(false, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), (hipStream_t)stream), "launching inet_kernel<fixed>");
     return 0;
 }
 
@@ -258,6 +261,8 @@ int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, cons
                                   (unsigned long long)arena_bytes);
     return run_host(mode, (const uint8_t *)arena, off, len, addr, out, n);
 }
+
+uint64_t inet_csum_set_flat_threshold(uint64_t packets) { return g_flat_min.exchange(packets); }
 
 uint16_t inet_ip_checksum(const void *dp, size_t bsize) {
     return single_or_die(INET_CSUM_IP, dp, bsize, 0, 0, "inet_ip_checksum");

@@ -182,7 +182,128 @@ __global__ __launch_bounds__(kThreads) void inet_kernel(IParams p) {
     }
 }
 
-hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, hipStream_t st) {
+// ---------------------------------------------------------------------------------------------
+// Variable-length batches, flat chunk stream (inet_flat_kernel): a wave owns windows of 64
+// consecutive packets. Packet i needs k = ceil(nch / 6) lane units of six 16-byte chunks (96 B,
+// interleaved: unit u holds chunks u, u + k, ..., so the packet's lanes load coalesced rows);
+// the window's units are numbered packet by packet and dealt to the lanes 64 at a time, so a
+// 64-byte packet takes one lane instead of a 16-lane round. A lane finds its packet from
+// frame-start marks (as fcs_flat_kernel), loads its six chunks, masks the packet's edge chunks,
+// and adds its folded sum into the packet's LDS accumulator (ds_add_u64). The sum needs no
+// position shift, so a packet of any length stays in the stream. Lane i finishes packet i at the
+// end of the window (coalesced u16 stores).
+// ---------------------------------------------------------------------------------------------
+constexpr int kUnit = 6;   // 16-byte chunks per lane unit
+
+template <bool VAR, int MODE>
+__global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
+    __shared__ unsigned long long acc_s[kThreads / 64][64];
+    __shared__ uint8_t mark_s[kThreads / 64][64];
+    __shared__ uint8_t list_s[kThreads / 64][64];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    unsigned long long *acc = acc_s[wave];
+    uint8_t *mark = mark_s[wave], *list = list_s[wave];
+    acc[lane] = 0ull;
+    mark[lane] = 0;
+    const uint64_t GW = (uint64_t)gridDim.x * (kThreads / 64);
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
+        const uint64_t i = w0 + lane;
+        const bool act = i < p.n;
+        const uint32_t len = act ? (VAR ? p.len[i] : p.flen) : 0u;
+        const uint64_t start = act ? p.base + (VAR ? p.off[i] : i * p.stride) : 0ull;
+        const uint64_t c0 = start & ~15ull;
+        const uint32_t nch = len ? (uint32_t)((((start + len + 15) & ~15ull) - c0) >> 4) : 0u;
+        const uint32_t k = (nch + kUnit - 1) / kUnit;
+        uint32_t incl = k;   // inclusive prefix over the window
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t P = incl - k;
+        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+        const uint64_t fmask = __ballot(k != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+        if (k) list[rank] = (uint8_t)lane;
+        const uint32_t c0lo = (uint32_t)c0, c0hi = (uint32_t)(c0 >> 32);
+        const uint32_t edges = (uint32_t)(start & 15) | ((uint32_t)((start + len) & 15) << 8);
+
+        for (uint32_t g0 = 0; g0 < K; g0 += 64) {
+            // a long packet spans any number of items, so marks are cleared after use (not tagged)
+            const bool starts = k && P >= g0 && P < g0 + 64;
+            if (starts) mark[P - g0] = 1;
+            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
+            const uint64_t M = __ballot(mark[lane] != 0);
+            if (starts) mark[P - g0] = 0;
+            const uint32_t g = g0 + (uint32_t)lane;
+            const bool valid = g < K;
+            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
+            const int src = valid ? (int)list[rk & 63u] : 0;
+            const uint64_t cb = ((uint64_t)(uint32_t)__shfl((int)c0hi, src) << 32) | (uint32_t)__shfl((int)c0lo, src);
+            const uint32_t nc = (uint32_t)__shfl((int)nch, src);
+            const uint32_t Pg = (uint32_t)__shfl((int)P, src);
+            const uint32_t eg = (uint32_t)__shfl((int)edges, src);
+            // unit u of a k-unit packet holds chunks u, u + k, ..., u + 5k: load q of the packet's k
+            // lanes reads k consecutive chunks (coalesced), the sum does not care about the order
+            const uint32_t u = g - Pg, kg = (nc + kUnit - 1) / kUnit;
+            if (valid) {
+                u32x4 v[kUnit];
+#pragma unroll
+                for (int q = 0; q < kUnit; q++) {
+                    const uint32_t c = u + q * kg;
+                    v[q] = gload<u32x4>(cb + 16ull * (c < nc ? c : nc - 1));   // past the end: a cache hit, zeroed below
+                }
+                uint64_t s = 0;
+#pragma unroll
+                for (int q = 0; q < kUnit; q++) {
+                    const uint32_t c = u + q * kg;
+                    if (c >= nc) continue;
+                    u32x4 w = v[q];
+                    if (c == 0 || c + 1 == nc) {   // the packet's edge chunks: keep bytes in [start, end)
+                        const uint32_t lo = c == 0 ? (eg & 0xffu) : 0u;
+                        const uint32_t e15 = (eg >> 8) & 0xffu;
+                        const uint32_t hi = (c + 1 == nc && e15) ? e15 : 16u;
+                        const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+                        w.x &= byte_mask(keep, 0);
+                        w.y &= byte_mask(keep, 1);
+                        w.z &= byte_mask(keep, 2);
+                        w.w &= byte_mask(keep, 3);
+                    }
+                    s += (uint64_t)w.x + w.y;
+                    s += (uint64_t)w.z + w.w;
+                }
+                const uint32_t f = fold64(s);   // 0 only for an all-zero unit
+                if (f) atomicAdd(&acc[src], (unsigned long long)f);
+            }
+        }
+
+        // ---- packet i: fold, odd-start swap, pseudo header and init, complement; clear state ----
+        const uint32_t m0 = fold64(acc[lane]);
+        const uint32_t m = (start & 1) ? swap16(m0) : m0;   // odd start: P = swap16(fold(M))
+        if (act) p.out[i] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, i, len) + m);
+        acc[lane] = 0ull;
+        mark[lane] = 0;
+    }
+}
+
+hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, hipStream_t st) {
+    if (p.n > flat_min) {
+        const uint64_t windows = (p.n + 63) / 64, per_block = kThreads / 64;
+        const uint64_t want = (windows + per_block - 1) / per_block, cap = (uint64_t)cus * 8;
+        const int grid = (int)(want < cap ? want : cap);
+#define INET_FLAT(V, M) hipLaunchKernelGGL((inet_flat_kernel<V, M>), dim3(grid), dim3(kThreads), 0, st, p)
+        if (var) {
+            if (mode == kTcp) INET_FLAT(true, kTcp);
+            else if (mode == kUdp) INET_FLAT(true, kUdp);
+            else INET_FLAT(true, kIp);
+        } else {
+            if (mode == kTcp) INET_FLAT(false, kTcp);
+            else if (mode == kUdp) INET_FLAT(false, kUdp);
+            else INET_FLAT(false, kIp);
+        }
+#undef INET_FLAT
+        return hipGetLastError();
+    }
     if (!p.n) return hipSuccess;
     const uint64_t per_block = kThreads / kGroup;
     uint64_t want = (p.n + per_block - 1) / per_block;

@@ -21,6 +21,8 @@ struct IParams {
     uint32_t flen;          // fixed: packet length
 };
 
-hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, hipStream_t st);
+// Batches of more than flat_min packets take the flat chunk-stream kernel,
+// smaller ones one 16-lane group per packet (every packet in flight at once).
+hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, hipStream_t st);
 
 }  // namespace inet

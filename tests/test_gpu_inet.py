@@ -26,6 +26,15 @@ def dev():
     return torch.device("cuda:0")
 
 
+@pytest.fixture(params=["group", "flat"])
+def inet_kernel(request):
+    """Run a test through both kernels (identical results required): group = one 16-lane group
+    per packet (small batches), flat = packets dealt to lanes by size."""
+    old = na.inet_set_flat_threshold((1 << 63) if request.param == "group" else 0)
+    yield request.param
+    na.inet_set_flat_threshold(old)
+
+
 def to_dev(arr: np.ndarray, dev):
     return torch.from_numpy(np.ascontiguousarray(arr)).to(dev)
 
@@ -62,7 +71,7 @@ def golden_groups(g):
         yield mode, arena, off, ln, (None if mode == "ip" else addr), exp, recs
 
 
-def test_golden_batch_dev(dev, inet_golden):
+def test_golden_batch_dev(dev, inet_golden, inet_kernel):
     for mode, arena, off, ln, addr, exp, recs in golden_groups(inet_golden):
         got = run_batch_dev(dev, mode, arena, off, ln, addr)
         bad = np.nonzero(got != exp)[0]
@@ -70,7 +79,7 @@ def test_golden_batch_dev(dev, inet_golden):
                                for i in bad[:10]]
 
 
-def test_golden_batch_host(dev, inet_golden):
+def test_golden_batch_host(dev, inet_golden, inet_kernel):
     for mode, arena, off, ln, addr, exp, _ in golden_groups(inet_golden):
         out = np.zeros(len(off), dtype=np.uint16)
         na.inet_batch_host(mode, arena, arena.nbytes, off, ln, addr, out, len(off))
@@ -96,7 +105,7 @@ def test_single_forms_match_oracle(dev, inet_oracle):
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("start,stride,L", [(14, 1518, 1500), (34, 1518, 1480), (14, 1518, 20),
                                              (0, 1500, 1500), (1, 97, 61), (3, 9000, 8997), (5, 64, 0)])
-def test_fixed_dev_vs_oracle(dev, inet_oracle, mode, start, stride, L):
+def test_fixed_dev_vs_oracle(dev, inet_oracle, mode, start, stride, L, inet_kernel):
     """Fixed-stride packets inside frames: the IP datagram at +14, the TCP segment at +34, the IP
     header alone, odd strides/starts (every alignment), jumbo, and empty packets."""
     n = 6000
@@ -115,7 +124,7 @@ def test_fixed_dev_vs_oracle(dev, inet_oracle, mode, start, stride, L):
 
 
 @pytest.mark.parametrize("mode", MODES)
-def test_random_var_vs_oracle(dev, inet_oracle, mode):
+def test_random_var_vs_oracle(dev, inet_oracle, mode, inet_kernel):
     """20k packets, random lengths 0..3000 (IMIX-heavy), random (overlapping) offsets."""
     rng = np.random.default_rng(11 + len(mode))
     n = 20000
@@ -129,7 +138,7 @@ def test_random_var_vs_oracle(dev, inet_oracle, mode):
     assert np.array_equal(got, oracle_batch(inet_oracle, mode, arena, off, ln, a))
 
 
-def test_quirks(dev, inet_oracle):
+def test_quirks(dev, inet_oracle, inet_kernel):
     """nstack-specific results: all-zero data (acc = 0xffff start), sums that are a nonzero
     multiple of 0xffff, the htons(len) truncation above 64 KiB, and headers that verify to 0."""
     cases = [bytes(40), b"\xff\xff", b"\xff\xff" * 3, b"\x00\x01\xff\xfe", bytes(1), b"\xff"]
@@ -163,7 +172,7 @@ def test_concurrent_single_callers(dev, inet_oracle):
     assert not errs
 
 
-def test_large_fixed_sampled(dev, inet_oracle, oracle):
+def test_large_fixed_sampled(dev, inet_oracle, oracle, inet_kernel):
     """4 M TCP segments (+34, 1480 B) inside device-generated 1518-B frames: 3000 sampled
     packets against the oracle, and two half launches equal one launch."""
     n, stride, start, L = 4 << 20, 1518, 34, 1480

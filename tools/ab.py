@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--what", default="fcs", help="comma list of fcs,stream,inet (inet: ip_checksum, fixed)")
+    ap.add_argument("--mix", default="64,576,1518:7,4,1",
+                    help="with --imix: lengths:weights of the variable-length mix")
     ap.add_argument("--imix", action="store_true",
                     help="variable-length path: --frames IMIX frames (7:4:1 of 64/576/1518, shuffled)")
     a = ap.parse_args()
@@ -48,7 +50,11 @@ def main():
     if a.imix:
         import numpy as np
         rng = np.random.default_rng(7)
-        ln_np = rng.choice(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.uint32), n)
+        lens_s, w_s = a.mix.split(":")
+        pool = []
+        for Lx, wx in zip(lens_s.split(","), w_s.split(",")):
+            pool += [int(Lx)] * int(wx)
+        ln_np = rng.choice(np.array(pool, dtype=np.uint32), n)
         ln = torch.from_numpy(ln_np.view(np.int32)).to(dev)
         off = torch.zeros(n, dtype=torch.int64, device=dev)
         off[1:] = torch.cumsum(ln[:-1].to(torch.int64), 0)
