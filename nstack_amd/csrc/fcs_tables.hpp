@@ -54,11 +54,12 @@ constexpr uint32_t kLdsBad = kLdsWave + 16 * kLdsWaveBytes;    // 153984: per-wa
 constexpr uint32_t kLdsBytes = kLdsBad + 16 * 8;                // 154112
 // The flat variable-length kernel keeps C_c in the lane-table region instead (it never uses the
 // per-lane tables): nibble table t of C_c at kLdsFlat + c*kFlatStride + t*64 + e*4. The stride is
-// 132 dwords (== 4 mod 64 banks), so lanes with different c spread over the banks. Per-wave
-// frame-start marks and rank -> lane lists follow it.
+// 136 dwords (== 8 mod 64 banks), so lanes with different c spread over the banks: 2.09 cycles per
+// 32-lane access on IMIX items against 2.45 at 132 dwords and 3.96 at 128 (bank simulation with
+// random nibbles). Per-wave frame-start marks and rank -> lane lists follow it.
 constexpr uint32_t kLdsFlat = kLdsLane;
-constexpr uint32_t kFlatStride = 528;
-constexpr uint32_t kFlatBytes = 16 * kFlatStride;              // 8448
+constexpr uint32_t kFlatStride = 544;
+constexpr uint32_t kFlatBytes = 16 * kFlatStride;              // 8704
 constexpr uint32_t kLdsFlatMark = kLdsFlat + kFlatBytes;        // 16 waves x 64 B
 constexpr uint32_t kLdsFlatList = kLdsFlatMark + 16 * 64;       // 16 waves x 64 B
 static_assert(kLdsFlatList + 16 * 64 <= kLdsJump, "flat scratch fits the lane-table region");
@@ -71,7 +72,7 @@ constexpr uint32_t kBlobH48 = kBlobJump + 8 * 16;       // uint32 [8][16]
 constexpr uint32_t kBlobH24 = kBlobH48 + 8 * 16;        // uint32 [8][16]
 constexpr uint32_t kBlobInv = kBlobH24 + 8 * 16;        // uint32 [96]
 constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
-constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][132] (C_c, LDS order)
+constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][136] (C_c, LDS order)
 constexpr uint32_t kBlobWords = kBlobFlat + kFlatBytes / 4;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
