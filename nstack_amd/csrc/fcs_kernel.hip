@@ -524,7 +524,11 @@ struct SingleLane {
 #endif
         uint32_t w[kChunkWords];
 #pragma unroll
+#ifdef FCS_ABL_NOALIGN   // measurement-only build: no realignment (wrong CRCs unless r == 0)
+        for (int i = 0; i < kChunkWords; i++) w[i] = d[i];
+#else
         for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#endif
 #pragma unroll
         for (int i = 0; i < kSingleMaskWords; i++)
             if (4 * i < (int)zmax) w[i] &= m[i];

@@ -28,6 +28,8 @@ constexpr uint32_t kHeaderLen = 14;     // ETHER_HEADER_LEN (src/nstack_ether.h:
 constexpr uint32_t kMinPayload = 56;    // ETHER_MINLEN - ETHER_FCS_LEN (:28-31; ether.c:223)
 constexpr uint32_t kFcsLen = 4;         // ETHER_FCS_LEN
 constexpr uint32_t kSlot = 1518;        // ETHER_MAXLEN + ETHER_FCS_LEN: largest frame_size
+constexpr uint32_t kStride = 1536;      // arena slot pitch: whole cache lines, so producers filling
+                                        // neighbouring slots never share a line
 constexpr uint32_t kMaxBatch = 65536;
 
 using Clock = std::chrono::steady_clock;
@@ -43,19 +45,35 @@ constexpr auto kSpin = std::chrono::microseconds(50);
 
 inline void cpu_relax() { __builtin_ia32_pause(); }
 
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now().time_since_epoch()).count();
+}
+
+// What a producer leaves for the flusher in its slot. `ready` = the batch sequence number once
+// the frame is assembled, so the flag needs no reset between uses of the buffer.
+struct alignas(64) SlotMeta {
+    Waiter *w = nullptr;                 // null: fcs_txq_send_async
+    uint32_t covered = 0;
+    std::atomic<uint64_t> ready{0};
+};
+
 struct Batch {
-    uint8_t *arena = nullptr;            // cap slots of kSlot bytes (pinned when possible)
+    uint8_t *arena = nullptr;            // cap slots of kStride bytes (pinned when possible)
     bool pinned = false;
-    std::vector<uint32_t> covered;       // FCS-covered bytes (frame_size - 4) per slot
+    std::vector<SlotMeta> meta;          // per slot, one cache line each (written by its producer)
+    std::vector<uint32_t> covered;       // FCS-covered bytes (frame_size - 4) per slot (flusher)
     std::vector<uint32_t> sizes;         // frame_size per slot
     std::vector<uint8_t *> frames;
     std::vector<int> res;
-    std::vector<Waiter *> waiters;
-    uint32_t reserved = 0;               // slots handed out (under fcs_txq::mu)
-    std::atomic<uint32_t> ready{0};      // slots fully assembled by their producers
-    uint64_t seq = 0;
-    Clock::time_point first;
+    std::atomic<int64_t> first_ns{0};    // when slot 0 was reserved (0: not yet stamped)
 };
+
+// The open batch and its fill level in one word, so producers reserve slots with one atomic add
+// and no lock: bits 63..32 = batch sequence number (the batch lives in b[seq & 1]), 31..0 = slots
+// reserved. The flusher closes a batch by swapping in (seq + 1, 0).
+inline uint64_t st_pack(uint64_t seq, uint32_t r) { return (seq << 32) | r; }
+inline uint64_t st_seq(uint64_t s) { return s >> 32; }
+inline uint32_t st_res(uint64_t s) { return (uint32_t)s; }
 
 }  // namespace
 
@@ -64,82 +82,116 @@ struct fcs_txq {
     uint32_t cap = 0, flush_usec = 0;
     fcs_txq_sink_fn sink = nullptr;
     void *ctx = nullptr;
+    Batch b[2];
+    std::atomic<uint64_t> st{0};          // (open batch seq, slots reserved): see st_pack
+    std::atomic<bool> idle{false};        // flusher asleep waiting for a first frame
+    std::atomic<bool> stop_req{false};
+    // slow paths (sleeping, flush(), statistics) take mu
     std::mutex mu;
     std::condition_variable cv_flusher;   // producers / flush() -> flusher
     std::condition_variable cv_prod;      // flusher -> producers (batch swapped, results ready)
-    Batch b[2];
-    int open = 0;                         // producers fill b[open]
     uint64_t seq_done = 0;                // last batch handed to the sink
     uint64_t flush_target = 0;            // flush() wants batches <= this closed now
-    bool stop = false;
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
     uint64_t ns_ready = 0, ns_gpu = 0, ns_sink = 0, ns_busy = 0;   // flusher time split
     uint64_t ns_pickup = 0;               // first frame of a batch queued -> batch closed
-    std::atomic<uint32_t> queued{0};      // frames reserved in the open batch (mirror, for spinning)
-    std::atomic<bool> stop_req{false};    // mirror of stop for the spinning flusher
     std::thread th;
 };
 
 namespace {
 
-void flusher(fcs_txq *q) {
-    std::unique_lock<std::mutex> lk(q->mu);
+uint64_t flush_target(fcs_txq *q) {
+    std::lock_guard<std::mutex> lk(q->mu);
+    return q->flush_target;
+}
+
+// Wait until the open batch has a frame to leave with; returns false when stopping with nothing
+// left. Decides like the locked version did: leave when full, when flush() asks, at once when
+// flush_usec == 0, else after the oldest frame has lingered flush_usec.
+bool wait_for_batch(fcs_txq *q, uint64_t seq) {
     for (;;) {
-        Batch *B = &q->b[q->open];
-        for (;;) {
-            if (B->reserved == q->cap || q->stop) break;
-            if (B->reserved > 0 && (q->flush_usec == 0 || q->flush_target >= B->seq)) break;
-            if (B->reserved > 0) {
-                // linger for company. Short lingers spin: a timed futex sleep is rounded up by the
-                // kernel's timer slack (50 us by default), longer than the whole GPU step.
-                const auto deadline = B->first + std::chrono::microseconds(q->flush_usec);
-                if (q->flush_usec <= 1000) {
-                    lk.unlock();
-                    while (Clock::now() < deadline && q->queued.load(std::memory_order_acquire) < q->cap &&
-                           !q->stop_req.load(std::memory_order_acquire))
-                        cpu_relax();
-                    lk.lock();
-                } else {
-                    q->cv_flusher.wait_until(lk, deadline);
-                }
-                if (B->reserved == q->cap || q->stop || Clock::now() >= deadline || q->flush_target >= B->seq) break;
+        uint64_t s = q->st.load(std::memory_order_seq_cst);
+        uint32_t r = st_res(s);
+        const bool stop = q->stop_req.load(std::memory_order_acquire);
+        if (r == 0) {
+            // stopping: mark the empty batch full so no producer can slip a frame in after we
+            // leave (it then sees stop_req and returns -ESHUTDOWN); lost the race: send it
+            if (stop) {
+                if (q->st.compare_exchange_strong(s, st_pack(seq, q->cap), std::memory_order_seq_cst)) return false;
                 continue;
             }
-            // idle: spin a little for the next frame, then sleep until a producer or flush() calls
-            lk.unlock();
+            // idle: spin a little for the next frame, then sleep until a producer, flush() or
+            // destroy wakes us (a producer taking slot 0 notifies when it sees idle set)
             const auto until = Clock::now() + kSpin;
-            while (q->queued.load(std::memory_order_acquire) == 0 && Clock::now() < until &&
+            while (st_res(q->st.load(std::memory_order_acquire)) == 0 && Clock::now() < until &&
                    !q->stop_req.load(std::memory_order_acquire))
                 cpu_relax();
-            lk.lock();
-            if (B->reserved == 0 && !q->stop && q->flush_target < B->seq) q->cv_flusher.wait(lk);
+            std::unique_lock<std::mutex> lk(q->mu);
+            q->idle.store(true, std::memory_order_seq_cst);
+            while (st_res(q->st.load(std::memory_order_seq_cst)) == 0 && !q->stop_req.load(std::memory_order_seq_cst))
+                q->cv_flusher.wait(lk);
+            q->idle.store(false, std::memory_order_relaxed);
+            continue;
         }
-        if (B->reserved == 0) {   // stop requested and nothing left
-            q->seq_done = B->seq - 1;
+        if (r >= q->cap || stop || q->flush_usec == 0 || flush_target(q) >= seq) return true;
+        // linger for company. Short lingers spin: a timed futex sleep is rounded up by the kernel's
+        // timer slack (50 us by default), longer than the whole GPU step.
+        Batch &B = q->b[seq & 1];
+        int64_t f = B.first_ns.load(std::memory_order_acquire);
+        if (f == 0) f = now_ns();   // slot 0's producer has not stamped it yet
+        const int64_t deadline = f + (int64_t)q->flush_usec * 1000;
+        if (q->flush_usec <= 1000) {
+            while (now_ns() < deadline && st_res(q->st.load(std::memory_order_acquire)) < q->cap &&
+                   !q->stop_req.load(std::memory_order_acquire))
+                cpu_relax();
+        } else {
+            std::unique_lock<std::mutex> lk(q->mu);
+            const auto left = std::chrono::nanoseconds(std::max<int64_t>(0, deadline - now_ns()));
+#ifdef FCS_TXQ_TSAN   // tools/tsan: GCC 11's libtsan misses pthread_cond_clockwait (steady-clock waits)
+            q->cv_flusher.wait_until(lk, std::chrono::system_clock::now() + left);
+#else
+            q->cv_flusher.wait_for(lk, left);
+#endif
+        }
+        if (now_ns() >= deadline) return true;
+    }
+}
+
+void flusher(fcs_txq *q) {
+    for (;;) {
+        const uint64_t seq = st_seq(q->st.load(std::memory_order_acquire));
+        if (!wait_for_batch(q, seq)) {   // stopping, nothing queued
+            std::lock_guard<std::mutex> lk(q->mu);
+            q->seq_done = seq - 1;
             q->cv_prod.notify_all();
-            break;
+            return;
         }
-        // close B; producers move on to the other buffer
-        const uint32_t n = B->reserved;
-        q->ns_pickup += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(Clock::now() - B->first).count();
-        q->open ^= 1;
-        Batch &N = q->b[q->open];
-        N.reserved = 0;
-        N.ready.store(0, std::memory_order_relaxed);
-        N.seq = B->seq + 1;
-        q->queued.store(0, std::memory_order_relaxed);
-        q->cv_prod.notify_all();
-        lk.unlock();
+        // close batch seq: producers move on to b[(seq + 1) & 1], which the previous iteration
+        // finished with (its results were delivered before we got here)
+        Batch *B = &q->b[seq & 1];
+        Batch &N = q->b[(seq + 1) & 1];
+        N.first_ns.store(0, std::memory_order_relaxed);
+        const uint64_t old = q->st.exchange(st_pack(seq + 1, 0), std::memory_order_acq_rel);
+        const uint32_t n = std::min(st_res(old), q->cap);   // producers past cap got no slot
+        {
+            std::lock_guard<std::mutex> lk(q->mu);   // producers waiting for a free slot
+            q->cv_prod.notify_all();
+        }
+        const int64_t f = B->first_ns.load(std::memory_order_acquire);
+        const uint64_t pickup = f ? (uint64_t)std::max<int64_t>(0, now_ns() - f) : 0;
 
         const auto t0 = Clock::now();
-        while (B->ready.load(std::memory_order_acquire) < n) std::this_thread::yield();
+        for (uint32_t i = 0; i < n; i++) {   // every reserved slot assembled by its producer
+            while (B->meta[i].ready.load(std::memory_order_acquire) != seq) std::this_thread::yield();
+            B->covered[i] = B->meta[i].covered;
+        }
         const auto t1 = Clock::now();
         // FCS of every frame, written little-endian after its covered bytes (ether.c:262-263)
-        const int rc = ether_fcs_tx_host(B->arena, kSlot, B->covered.data(), n);
+        const int rc = ether_fcs_tx_host(B->arena, kStride, B->covered.data(), n);
         const auto t2 = Clock::now();
         if (rc == 0) {
             for (uint32_t i = 0; i < n; i++) {
-                B->frames[i] = B->arena + (uint64_t)i * kSlot;
+                B->frames[i] = B->arena + (uint64_t)i * kStride;
                 B->sizes[i] = B->covered[i] + kFcsLen;
                 B->res[i] = -EIO;   // a sink that forgets a frame reports it as failed
             }
@@ -149,20 +201,21 @@ void flusher(fcs_txq *q) {
         }
         const auto t3 = Clock::now();
 
-        lk.lock();
+        std::lock_guard<std::mutex> lk(q->mu);
         auto ns = [](Clock::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
         q->ns_ready += ns(t1 - t0);
         q->ns_gpu += ns(t2 - t1);
         q->ns_sink += ns(t3 - t2);
         q->ns_busy += ns(Clock::now() - t0);
+        q->ns_pickup += pickup;
         for (uint32_t i = 0; i < n; i++) {
             if (B->res[i] != (int)(B->covered[i] + kFcsLen)) q->n_errors++;
-            if (Waiter *w = B->waiters[i]) {   // null: fcs_txq_send_async
+            if (Waiter *w = B->meta[i].w) {   // null: fcs_txq_send_async
                 w->result = B->res[i];
                 w->done.store(true, std::memory_order_release);   // last touch: w may vanish now
             }
         }
-        q->seq_done = B->seq;
+        q->seq_done = seq;
         q->n_frames += n;
         q->n_batches++;
         q->cv_prod.notify_all();
@@ -185,7 +238,7 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
     q->ctx = sink_ctx;
     for (int k = 0; k < 2; k++) {
         Batch &B = q->b[k];
-        const uint64_t bytes = (uint64_t)max_batch * kSlot;
+        const uint64_t bytes = (uint64_t)max_batch * kStride;
         B.arena = (uint8_t *)fcs_host_alloc(bytes);   // pinned: direct H2D
         B.pinned = B.arena != nullptr;
         if (!B.arena) B.arena = (uint8_t *)std::malloc(bytes);   // no GPU runtime: sends will fail
@@ -193,13 +246,13 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
             fcs_txq_destroy(q);
             return nullptr;
         }
+        B.meta = std::vector<SlotMeta>(max_batch);
         B.covered.assign(max_batch, 0);
         B.sizes.assign(max_batch, 0);
         B.frames.assign(max_batch, nullptr);
         B.res.assign(max_batch, 0);
-        B.waiters.assign(max_batch, nullptr);
     }
-    q->b[0].seq = 1;
+    q->st.store(st_pack(1, 0));
     q->th = std::thread(flusher, q);
     return q;
 }
@@ -207,37 +260,61 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
 }  // extern "C"
 
 namespace {
-// Reserve a slot in the open batch, assemble the frame there (outside the lock) and mark it
-// ready. w == nullptr: fire-and-forget (the result only feeds the error counter).
+// Reserve a slot in the open batch (one fetch_add, no lock), assemble the frame there and mark it
+// ready.
+// w == nullptr: fire-and-forget (the result only feeds the error counter).
 int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize, Waiter *w) {
     if (!q || !dst || (!buf && bsize)) return -EINVAL;
     const size_t frame_size = kHeaderLen + std::max<size_t>(bsize, kMinPayload) + kFcsLen;   // :222-224
     if (frame_size > kSlot) return -EMSGSIZE;                                                // :234-237
-    std::unique_lock<std::mutex> lk(q->mu);
-    while (!q->stop && q->b[q->open].reserved == q->cap) {   // batch full: wait for the swap
-        q->cv_flusher.notify_one();
-        q->cv_prod.wait(lk);
+    uint64_t s;
+    for (;;) {
+        if (q->stop_req.load(std::memory_order_acquire)) return -ESHUTDOWN;
+        s = q->st.load(std::memory_order_acquire);
+        if (st_res(s) < q->cap) {
+            // one fetch_add; a producer that overshoots the full batch got no slot and retries
+            // after the swap (the flusher takes min(reserved, cap))
+            s = q->st.fetch_add(1, std::memory_order_seq_cst);
+            if (st_res(s) < q->cap) break;
+        }
+        // batch full: wait for the flusher to swap in the next one
+        const uint64_t seq = st_seq(s);
+        const auto until = Clock::now() + kSpin;
+        while (st_seq(q->st.load(std::memory_order_acquire)) == seq && Clock::now() < until) cpu_relax();
+        std::unique_lock<std::mutex> lk(q->mu);
+        while (st_seq(q->st.load(std::memory_order_acquire)) == seq && !q->stop_req.load(std::memory_order_acquire)) {
+            q->cv_flusher.notify_one();
+            q->cv_prod.wait(lk);
+        }
     }
-    if (q->stop) return -ESHUTDOWN;
-    Batch &B = q->b[q->open];
-    const uint32_t slot = B.reserved++;
-    if (slot == 0) B.first = Clock::now();
-    B.waiters[slot] = w;
-    q->queued.store(B.reserved, std::memory_order_release);
-    if (slot == 0 || B.reserved == q->cap) q->cv_flusher.notify_one();
-    lk.unlock();
+    const uint64_t seq = st_seq(s);
+    const uint32_t slot = st_res(s);
+    Batch &B = q->b[seq & 1];
+    if (slot == 0) {
+        B.first_ns.store(now_ns(), std::memory_order_release);
+        if (q->idle.load(std::memory_order_seq_cst)) {   // the flusher went to sleep: wake it
+            std::lock_guard<std::mutex> lk(q->mu);
+            q->cv_flusher.notify_one();
+        }
+    }
+    if (slot + 1 == q->cap && q->flush_usec > 1000) {   // a long linger sleeps: a full batch ends it
+        std::lock_guard<std::mutex> lk(q->mu);
+        q->cv_flusher.notify_one();
+    }
 
     // assemble exactly as ether_send (:257-261): dst, src, htons(proto), payload, zero pad and
     // zeroed FCS slot; the engine fills the FCS (:262-263)
-    uint8_t *f = B.arena + (uint64_t)slot * kSlot;
+    uint8_t *f = B.arena + (uint64_t)slot * kStride;
     std::memcpy(f, dst, 6);
     std::memcpy(f + 6, q->mac, 6);
     f[12] = (uint8_t)(proto >> 8);
     f[13] = (uint8_t)proto;
     if (bsize) std::memcpy(f + kHeaderLen, buf, bsize);
     std::memset(f + kHeaderLen + bsize, 0, frame_size - kHeaderLen - bsize);
-    B.covered[slot] = (uint32_t)(frame_size - kFcsLen);
-    B.ready.fetch_add(1, std::memory_order_release);
+    SlotMeta &m = B.meta[slot];
+    m.w = w;
+    m.covered = (uint32_t)(frame_size - kFcsLen);
+    m.ready.store(seq, std::memory_order_release);
     return (int)frame_size;
 }
 }  // namespace
@@ -263,9 +340,9 @@ int fcs_txq_send_async(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const
 
 int fcs_txq_flush(fcs_txq_t *q) {
     if (!q) return -EINVAL;
+    const uint64_t s = q->st.load(std::memory_order_seq_cst);
+    const uint64_t target = st_res(s) ? st_seq(s) : st_seq(s) - 1;   // the open batch, else the one in flight
     std::unique_lock<std::mutex> lk(q->mu);
-    const Batch &B = q->b[q->open];
-    const uint64_t target = B.reserved ? B.seq : B.seq - 1;   // the open batch, else the one in flight
     q->flush_target = std::max(q->flush_target, target);
     q->cv_flusher.notify_one();
     while (q->seq_done < target) q->cv_prod.wait(lk);
@@ -277,10 +354,10 @@ void fcs_txq_destroy(fcs_txq_t *q) {
     if (q->th.joinable()) {
         {
             std::lock_guard<std::mutex> lk(q->mu);
-            q->stop = true;
-            q->stop_req.store(true, std::memory_order_release);
+            q->stop_req.store(true, std::memory_order_seq_cst);
+            q->cv_flusher.notify_one();
+            q->cv_prod.notify_all();
         }
-        q->cv_flusher.notify_one();
         q->th.join();
     }
     for (int k = 0; k < 2; k++) {

@@ -55,3 +55,39 @@ def test_no_gpu_fails_every_frame_and_sends_nothing():
     with pytest.raises(BlockingIOError):
         b.recv(2048)
     a.close(), b.close()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.skipif(_gpu_visible(), reason="checks the queue machinery on the no-GPU error path")
+@pytest.mark.parametrize("max_batch,linger", [(1, 0), (8, 0), (64, 20), (4096, 2000)])
+def test_many_producers_no_lost_frames(max_batch, linger):
+    """Lock-free slot reservation under contention: sync and fire-and-forget producers together,
+    tiny and large batches, spinning and sleeping lingers. Every frame is accounted for once and
+    every sync caller gets its (here -ENODEV) result; flush() and close() return."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    res = []
+    lock = threading.Lock()
+    n_sync, n_async, per = 12, 4, 150
+    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=linger) as q:
+        def sync_worker(k):
+            mine = [q.send(DST, 0x0800, bytes([k]) * (k * 37 % 1400)) for _ in range(per)]
+            with lock:
+                res.extend(mine)
+
+        def async_worker(k):
+            for i in range(per):
+                assert q.send_async(DST, 0x0800, bytes([i & 255]) * (i % 300)) > 0
+
+        th = [threading.Thread(target=sync_worker, args=(k,)) for k in range(n_sync)]
+        th += [threading.Thread(target=async_worker, args=(k,)) for k in range(n_async)]
+        for t in th:
+            t.start()
+        for t in th:
+            t.join()
+        q.flush()
+        frames, batches, errors = q.stats()
+    total = (n_sync + n_async) * per
+    assert res == [-19] * (n_sync * per)
+    assert frames == total and errors == total
+    assert batches >= -(-total // max_batch)
+    a.close(), b.close()

@@ -1,0 +1,17 @@
+// gpu_stub.cpp — host-only stand-ins for the engine entry points the TX queue calls, so the queue
+// logic (nstack_amd/csrc/fcs_txq.cpp) can run under ThreadSanitizer without a GPU: the "FCS" is a
+// placeholder word and each batch takes 20 us, like a small GPU step. Measurement tool only.
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <chrono>
+extern "C" {
+int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n) {
+    for (uint64_t i = 0; i < n; i++) { uint32_t c = 0xA5A5A5A5u ^ len[i]; std::memcpy((uint8_t*)base + i*stride + len[i], &c, 4); }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return 0;
+}
+void *fcs_host_alloc(uint64_t b) { return std::malloc(b); }
+void fcs_host_free(void *p) { std::free(p); }
+}

@@ -1,0 +1,13 @@
+#!/bin/bash
+# ThreadSanitizer run of the TX queue's lock-free reservation and hand-offs (host code only; the
+# GPU step is stubbed by gpu_stub.cpp). Exits non-zero on a TSan report or a lost/duplicated frame.
+set -eu
+HERE=$(cd "$(dirname "$0")" && pwd)
+ROOT=$(dirname "$(dirname "$HERE")")
+OUT=${TMPDIR:-/tmp}/txq_tsan
+g++ -std=c++17 -O1 -g -fsanitize=thread -DFCS_TXQ_TSAN -I"$ROOT/include" \
+    "$HERE/txq_stress.cpp" "$HERE/gpu_stub.cpp" "$ROOT/nstack_amd/csrc/fcs_txq.cpp" -o "$OUT" -lpthread
+for c in "1 0" "7 0" "7 30" "64 0" "64 3000" "4096 0" "4096 30" "4096 3000"; do
+  TSAN_OPTIONS="halt_on_error=1 exitcode=66" timeout -k 5 300 "$OUT" $c
+done
+echo "tsan: clean"
