@@ -14,7 +14,9 @@
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
+#include <chrono>
 #include <cstring>
+#include <map>
 #include <memory>
 #include <mutex>
 #include <string>
@@ -81,11 +83,16 @@ struct DevState {
     std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
     hipStream_t tx_stream = nullptr;
     uint32_t *tx_len = nullptr, *tx_out = nullptr;   // pinned, device-mapped
+    uint32_t *tx_dlen = nullptr, *tx_dout = nullptr; //   ... their device addresses
+    uint64_t *tx_flag = nullptr, *tx_dflag = nullptr; // completion word (signal_kernel), mapped
+    uint64_t tx_seq = 0;
     uint64_t tx_cap = 0;
     std::mutex one_mu;       // single-frame (drop-in ether_fcs) staging
     hipStream_t one_stream = nullptr;
-    uint8_t *one_d = nullptr, *one_h = nullptr;
-    uint32_t *one_dout = nullptr, *one_hout = nullptr;
+    uint8_t *one_h = nullptr, *one_hd = nullptr;      // pinned, device-mapped frame staging
+    uint32_t *one_hout = nullptr, *one_dout = nullptr;
+    uint64_t *one_flag = nullptr, *one_dflag = nullptr;
+    uint64_t one_seq = 0;
     uint64_t one_cap = 0;
 };
 
@@ -252,6 +259,47 @@ int ensure_pipe(DevState *ds, uint64_t bytes, uint64_t frames) {
     return 0;
 }
 
+// Ranges from fcs_host_alloc (the TX queue's arenas): host address -> device address without a
+// HIP query per small batch. Entries leave in fcs_host_free, before the memory is released.
+struct PinnedRange {
+    uint64_t bytes;
+    uint8_t *dev;
+};
+std::mutex g_pin_mu;
+std::map<uintptr_t, PinnedRange> g_pinned;
+
+uint8_t *pinned_dev_ptr(const void *p, uint64_t bytes) {
+    std::lock_guard<std::mutex> lk(g_pin_mu);
+    const uintptr_t a = (uintptr_t)p;
+    auto it = g_pinned.upper_bound(a);
+    if (it == g_pinned.begin()) return nullptr;
+    --it;
+    if (a < it->first || a + bytes > it->first + it->second.bytes) return nullptr;
+    return it->second.dev + (a - it->first);
+}
+
+// A small batch completes when signal_kernel, queued behind its FCS kernel, stores `v` into the
+// mapped completion word: the host spins on that word (a stream synchronisation costs ~3 us more
+// per round trip, tools/microbench/launch_lat.hip). Errors and stalls are still caught by
+// polling the stream now and then.
+int wait_flag(hipStream_t st, const uint64_t *flag, uint64_t v, const char *what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; i++) {
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+        __builtin_ia32_pause();
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(st);
+            if (q == hipSuccess) {
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+                return fail(EIO, "%s: stream idle but no completion signal", what);
+            }
+            if (q != hipErrorNotReady) return hip_fail(q, what);
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return fail(ETIMEDOUT, "%s: no completion after 10 s", what);
+        }
+    }
+}
+
 bool is_pinned(const void *p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -406,7 +454,12 @@ constexpr uint64_t kZeroCopyMaxBytes = 8ull << 20;
 int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t stride, const uint32_t *len, uint64_t n) {
     std::lock_guard<std::mutex> lk(ds->tx_mu);
     HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
-    if (!ds->tx_stream) HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
+    if (!ds->tx_stream) {
+        HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
+        HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dflag, ds->tx_flag, 0), "hipHostGetDevicePointer(flag)");
+        *ds->tx_flag = 0;
+    }
     if (n > ds->tx_cap) {
         if (ds->tx_len) hipHostFree(ds->tx_len);
         if (ds->tx_out) hipHostFree(ds->tx_out);
@@ -415,20 +468,22 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t stride, const uint32_
         const uint64_t cap = std::max<uint64_t>(n, 4096);
         HIPTRY(hipHostMalloc(&ds->tx_len, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx len)");
         HIPTRY(hipHostMalloc(&ds->tx_out, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx out)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dlen, ds->tx_len, 0), "hipHostGetDevicePointer(len)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dout, ds->tx_out, 0), "hipHostGetDevicePointer(out)");
         ds->tx_cap = cap;
     }
     std::memcpy(ds->tx_len, len, n * 4);
-    void *dbase = nullptr, *dlen = nullptr, *dout = nullptr;
-    if (hipHostGetDevicePointer(&dbase, base, 0) != hipSuccess) {   // pinned but not mapped
+    void *dbase = pinned_dev_ptr(base, n * stride);   // our own arenas: no HIP query
+    if (!dbase && hipHostGetDevicePointer(&dbase, base, 0) != hipSuccess) {   // pinned but not mapped
         (void)hipGetLastError();
         return 1;
     }
-    HIPTRY(hipHostGetDevicePointer(&dlen, ds->tx_len, 0), "hipHostGetDevicePointer(len)");
-    HIPTRY(hipHostGetDevicePointer(&dout, ds->tx_out, 0), "hipHostGetDevicePointer(out)");
-    int rc = launch_var(ds, dbase, n * stride, nullptr, (const uint32_t *)dlen, (uint32_t *)dout, n, ds->tx_stream,
-                        nullptr, nullptr, stride);
+    int rc = launch_var(ds, dbase, n * stride, nullptr, ds->tx_dlen, ds->tx_dout, n, ds->tx_stream, nullptr, nullptr,
+                        stride);
     if (rc) return rc;
-    HIPTRY(hipStreamSynchronize(ds->tx_stream), "hipStreamSynchronize(tx)");
+    const uint64_t v = ++ds->tx_seq;
+    HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
+    if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small TX batch"))) return rc;
     for (uint64_t i = 0; i < n; i++) std::memcpy(base + i * stride + len[i], &ds->tx_out[i], 4);
     return 0;
 }
@@ -586,11 +641,11 @@ void fcs_engine_fini(void) {
         if (ds->tx_stream) hipStreamDestroy(ds->tx_stream);
         if (ds->tx_len) hipHostFree(ds->tx_len);
         if (ds->tx_out) hipHostFree(ds->tx_out);
+        if (ds->tx_flag) hipHostFree(ds->tx_flag);
         if (ds->one_stream) hipStreamDestroy(ds->one_stream);
-        if (ds->one_d) hipFree(ds->one_d);
         if (ds->one_h) hipHostFree(ds->one_h);
-        if (ds->one_dout) hipFree(ds->one_dout);
         if (ds->one_hout) hipHostFree(ds->one_hout);
+        if (ds->one_flag) hipHostFree(ds->one_flag);
         if (ds->d_blob) hipFree(ds->d_blob);
     }
     g_dev.clear();
@@ -738,30 +793,30 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
     hipError_t e = hipGetDevice(&cur);
     if (e != hipSuccess) die("hipGetDevice", e);
     if ((e = hipSetDevice(dev)) != hipSuccess) die("hipSetDevice", e);
-    if (!ds->one_stream) {
+    if (!ds->one_stream) {   // zero-copy: the kernel reads the frame and writes the FCS in pinned memory
         if ((e = hipStreamCreateWithFlags(&ds->one_stream, hipStreamNonBlocking)) != hipSuccess) die("stream", e);
-        if ((e = hipMalloc(&ds->one_dout, 64)) != hipSuccess) die("hipMalloc", e);
-        if ((e = hipHostMalloc(&ds->one_hout, 64, hipHostMallocDefault)) != hipSuccess) die("hipHostMalloc", e);
+        if ((e = hipHostMalloc(&ds->one_hout, 64, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
+        if ((e = hipHostGetDevicePointer((void **)&ds->one_dout, ds->one_hout, 0)) != hipSuccess) die("map", e);
+        if ((e = hipHostMalloc(&ds->one_flag, 64, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
+        if ((e = hipHostGetDevicePointer((void **)&ds->one_dflag, ds->one_flag, 0)) != hipSuccess) die("map", e);
+        *ds->one_flag = 0;
     }
     if (bsize > ds->one_cap) {
-        if (ds->one_d) hipFree(ds->one_d);
         if (ds->one_h) hipHostFree(ds->one_h);
-        uint64_t cap = std::max<uint64_t>(4096, bsize + 64);
-        if ((e = hipMalloc(&ds->one_d, cap)) != hipSuccess) die("hipMalloc", e);
-        if ((e = hipHostMalloc(&ds->one_h, cap, hipHostMallocDefault)) != hipSuccess) die("hipHostMalloc", e);
+        const uint64_t cap = std::max<uint64_t>(4096, bsize + 64);
+        if ((e = hipHostMalloc(&ds->one_h, cap, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
+        if ((e = hipHostGetDevicePointer((void **)&ds->one_hd, ds->one_h, 0)) != hipSuccess) die("map", e);
         ds->one_cap = cap - 64;
     }
     std::memcpy(ds->one_h, data, bsize);
-    if ((e = hipMemcpyAsync(ds->one_d, ds->one_h, bsize, hipMemcpyHostToDevice, ds->one_stream)) != hipSuccess)
-        die("H2D", e);
-    rc = launch_fixed(ds, ds->one_d, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);
+    rc = launch_fixed(ds, ds->one_hd, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);
+    const uint64_t v = ++ds->one_seq;
+    if (!rc && (e = fcs::launch_signal(ds->one_dflag, v, ds->one_stream)) != hipSuccess) die("signal", e);
+    if (!rc) rc = wait_flag(ds->one_stream, ds->one_flag, v, "ether_fcs");
     if (rc) {
         std::fprintf(stderr, "nstack_fcs: ether_fcs: %s\n", g_last_error.c_str());
         std::abort();
     }
-    if ((e = hipMemcpyAsync(ds->one_hout, ds->one_dout, 4, hipMemcpyDeviceToHost, ds->one_stream)) != hipSuccess)
-        die("D2H", e);
-    if ((e = hipStreamSynchronize(ds->one_stream)) != hipSuccess) die("sync", e);
     const uint32_t c = ds->one_hout[0];
     hipSetDevice(cur);
     return c;
@@ -773,11 +828,23 @@ void *fcs_host_alloc(uint64_t bytes) {
         fail(ENOMEM, "hipHostMalloc(%llu) failed", (unsigned long long)bytes);
         return nullptr;
     }
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess && d) {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        g_pinned[(uintptr_t)p] = PinnedRange{bytes, (uint8_t *)d};
+    } else {
+        (void)hipGetLastError();
+    }
     return p;
 }
 
 void fcs_host_free(void *p) {
-    if (p) hipHostFree(p);
+    if (!p) return;
+    {
+        std::lock_guard<std::mutex> lk(g_pin_mu);
+        g_pinned.erase((uintptr_t)p);
+    }
+    hipHostFree(p);
 }
 
 int fcs_fill_splitmix64_dev(void *p, uint64_t bytes, uint64_t seed, uint64_t byte_offset, void *stream) {

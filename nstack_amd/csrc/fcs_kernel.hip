@@ -420,21 +420,16 @@ __device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds
     __syncthreads();
 }
 
+// The quarter-wave-per-frame loop of one workgroup (`blk` of `nblk`), tables already in LDS.
 template <bool VAR, bool TINY, bool SINGLE>
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-
-    stage_tables(p, lds);
-    init_bad(lds);
-
+__device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, uint32_t blk, uint32_t nblk) {
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4,
-                              (uint64_t)gridDim.x * kSlotsPerWg};
+    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg};
 
     typename Lane<VAR, TINY, SINGLE>::Pos A, B;
-    A.f = ((uint64_t)blockIdx.x * kSlotsPerWg) + (threadIdx.x / kGroup);
+    A.f = ((uint64_t)blk * kSlotsPerWg) + (threadIdx.x / kGroup);
     A.k = 0;
     A.act = A.f < p.n;
     A.it = (SINGLE || A.act) ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
@@ -477,6 +472,14 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
         L.process(C, CC, s);
     }
 #endif
+}
+
+template <bool VAR, bool TINY, bool SINGLE>
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    stage_tables(p, lds);
+    init_bad(lds);
+    fcs_body<VAR, TINY, SINGLE>(p, lds, blockIdx.x, gridDim.x);
     flush_bad(p, lds);
 }
 
@@ -1087,6 +1090,16 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4 *__restric
     if (acc == 0x9E3779B9u) sink[0] = acc;   // keep the loads live; practically never stores
 }
 
+// Completion signal for small host batches: launched behind the FCS kernel on the same stream,
+// it stores `v` into a device-mapped host word, on which the host spins instead of synchronising
+// the stream (cuts the hipStreamSynchronize wake-up from the round trip).
+__global__ void signal_kernel(uint64_t *flag, uint64_t v) {
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // TX mode helper: after the FCS kernel wrote crc[i], store it little-endian after each frame.
 __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t stride,
                                                        const uint32_t *len, const uint32_t *crc,
@@ -1143,6 +1156,11 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
         FCS_LAUNCH(false, false, false);
     }
 #undef FCS_LAUNCH
+    return hipGetLastError();
+}
+
+hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st) {
+    hipLaunchKernelGGL(signal_kernel, dim3(1), dim3(64), 0, st, flag, v);
     return hipGetLastError();
 }
 

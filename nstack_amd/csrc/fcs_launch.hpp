@@ -24,7 +24,9 @@ struct KParams {
 
 constexpr int kWgThreads = 1024;
 
+
 hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st);
+hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st);
 hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hipStream_t st);
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st);
 hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,
