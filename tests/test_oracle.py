@@ -103,3 +103,14 @@ def test_oracle_matches_compiled_reference(oracle):
         n = rng.randrange(0, 9100)
         b = os.urandom(n)
         assert ref.ether_fcs(b, n) == oracle.oracle_ether_fcs(b, n)
+
+
+def test_bench_host_generator_matches_device_generator_restatement(oracle):
+    """bench.py re-creates sampled frames with a numpy splitmix64 (no oracle in its timed leg);
+    it must equal the oracle's restatement of the device generator at any offset."""
+    import numpy as np
+    import bench
+    for seed, off, n in ((0x4E535441434B, 0, 1518), (0x4E535441434B, 1518 * 12345 + 3, 1518), (7, 5, 1), (1, 8, 64)):
+        buf = np.empty(n, dtype=np.uint8)
+        oracle.oracle_splitmix_fill(buf.ctypes.data, n, seed, off)
+        assert np.array_equal(bench.splitmix_bytes(seed, off, n), buf)
