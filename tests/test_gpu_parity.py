@@ -307,3 +307,26 @@ def test_bad_arguments_are_rejected(dev):
     t = torch.zeros(64, dtype=torch.uint8, device=dev)
     assert lib.ether_fcs_fixed_dev(ctypes.c_void_p(t.data_ptr()), 10, 20, 2, ctypes.c_void_p(t.data_ptr()), None) == -22
     assert lib.ether_fcs_fixed_dev(ctypes.c_void_p(t.data_ptr()), 10, 20, 0, ctypes.c_void_p(t.data_ptr()), None) == 0
+
+
+hyp = pytest.importorskip("hypothesis")
+from hypothesis import given, settings, strategies as hst  # noqa: E402
+
+
+@settings(max_examples=25, deadline=None, derandomize=True)
+@given(hst.lists(hst.tuples(hst.integers(0, 5000), hst.integers(0, 4095)), min_size=1, max_size=300),
+       hst.sampled_from(["quarter", "windowed"]))
+def test_var_batches_fuzz(dev, batch, kernel):
+    """Random lengths (0..5000 B, every segment count up to 4) at random, overlapping offsets with
+    every byte alignment, through both variable-length kernels, against zlib.crc32."""
+    old = na.set_var_threshold((1 << 63) if kernel == "quarter" else 0)
+    try:
+        rng = np.random.default_rng(len(batch))
+        arena = rng.integers(0, 256, 4096 + 5000 + 64, dtype=np.uint8)
+        ln = [L for L, _ in batch]
+        off = [o for _, o in batch]
+        got = run_var(dev, arena, off, ln)
+        for i, (L, o) in enumerate(batch):
+            assert got[i] == zlib.crc32(arena[o:o + L].tobytes()), (kernel, L, o)
+    finally:
+        na.set_var_threshold(old)
