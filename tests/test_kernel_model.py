@@ -41,3 +41,26 @@ def test_model_edges_and_alignment(lds):
         for S in (0, 1, 2, 3, 12000 - L):
             if 0 <= S and S + L <= len(mem):
                 assert km.model_frame(lds, mem, S, L) == zlib.crc32(mem[S:S + L]), (L, S)
+
+
+def _shift(s, n):
+    """A_n: the CRC register advanced over n zero bytes (reflected 0xEDB88320)."""
+    for _ in range(n):
+        for _ in range(8):
+            s = (s >> 1) ^ (0xEDB88320 if s & 1 else 0)
+    return s
+
+
+def test_flat_kernel_chunk_shift_tables():
+    """The flat variable-length kernel's C_c = A_{96c} nibble tables (fcs_tables.hpp kBlobFlat,
+    136-dword stride per c): chunk_shift(s, c) = XOR_t C_c[t][nibble_t(s)] must equal A_{96c}(s)."""
+    blob = na.tables_blob()
+    flat = km.BLOB_INV + km.CHUNK + 8 * 16   # kBlobM768 + 8 * 16
+    rng = random.Random(4)
+    for c in (0, 1, 5, 15):
+        for _ in range(3):
+            s = rng.getrandbits(32)
+            v = 0
+            for t in range(8):
+                v ^= int(blob[flat + c * 136 + t * 16 + ((s >> (4 * t)) & 15)])
+            assert v == _shift(s, 96 * c), (c, hex(s))
