@@ -94,7 +94,10 @@ int ether_fcs_verify_fixed_dev(const void *base, uint64_t stride, uint32_t len, 
 int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
                               const uint32_t *len, uint8_t *ok, uint64_t n);
 
-/* ---- pinned host memory for zero-copy-staging callers (optional) ---- */
+/* ---- pinned host memory for zero-copy-staging callers (optional) ----
+ * Pinned, device-mapped, portable host memory. Small TX batches in it (ether_fcs_tx_host) are
+ * read by the kernel in place. Release it with fcs_host_free only (the engine keeps the range's
+ * device address until then). */
 void *fcs_host_alloc(uint64_t bytes);
 void fcs_host_free(void *p);
 

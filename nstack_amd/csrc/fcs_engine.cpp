@@ -735,7 +735,7 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
         if ((uint64_t)len[i] + 4 > stride)
             return fail(EINVAL, "frame %llu: len %u + FCS does not fit stride %llu", (unsigned long long)i,
                         len[i], (unsigned long long)stride);
-    if (n * stride <= kZeroCopyMaxBytes && is_pinned(base)) {
+    if (n * stride <= kZeroCopyMaxBytes && (pinned_dev_ptr(base, n * stride) || is_pinned(base))) {
         std::vector<DevState *> devs;
         int rc = engine_devices(&devs);
         if (rc) return rc;
