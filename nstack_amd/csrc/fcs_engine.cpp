@@ -161,7 +161,12 @@ uint32_t mask_bound(uint32_t len) {
 int grid_for(const DevState *ds, uint64_t n) {
     const uint64_t slots = fcs::kWgThreads / fcs::kGroup;   // frame slots per workgroup
     const uint64_t want = (n + slots - 1) / slots;
-    return (int)std::max<uint64_t>(1, std::min<uint64_t>((uint64_t)ds->cus, want));
+#ifdef FCS_GRID_CUS   // measurement-only build: run the persistent grid on fewer CUs
+    const uint64_t cus = std::min<uint64_t>((uint64_t)ds->cus, FCS_GRID_CUS);
+#else
+    const uint64_t cus = (uint64_t)ds->cus;
+#endif
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>(cus, want));
 }
 
 uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
