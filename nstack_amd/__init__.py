@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -35,6 +35,8 @@ EXPORTS = [
     # include/nstack_inet.h — batched Internet checksums (opt-in)
     "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_csum_set_flat_threshold", "inet_ip_checksum",
     "inet_tcp_checksum", "inet_udp_checksum",
+    # include/nstack_rxq.h — batched RX call site with FCS verification
+    "fcs_rxq_create", "fcs_rxq_receive", "fcs_rxq_stats", "fcs_rxq_destroy",
 ]
 
 # include/nstack_inet.h modes: the reference function each result reproduces
@@ -100,6 +102,10 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "inet_csum_fixed_dev": (i32, [i32, vp, u64, u32, u64, vp, vp, vp]),
         "inet_csum_batch_host": (i32, [i32, vp, u64, vp, vp, vp, vp, u64]),
         "inet_csum_set_flat_threshold": (u64, [u64]),
+        "fcs_rxq_create": (vp, [i32, vp, u32, u32]),
+        "fcs_rxq_receive": (i32, [vp, vp, vp, c.c_size_t]),
+        "fcs_rxq_stats": (None, [vp] + [c.POINTER(u64)] * 5),
+        "fcs_rxq_destroy": (None, [vp]),
         "inet_ip_checksum": (c.c_uint16, [vp, c.c_size_t]),
         "inet_tcp_checksum": (c.c_uint16, [u32, u32, vp, c.c_size_t]),
         "inet_udp_checksum": (c.c_uint16, [vp, c.c_size_t, u32, u32]),
@@ -270,6 +276,46 @@ class TxQueue:
     def close(self) -> None:
         if self._q:
             load().fcs_txq_destroy(self._q)
+            self._q = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+
+class RxQueue:
+    """Batched ether_receive (include/nstack_rxq.h; src/linux/ether.c:180-212) on a socket fd:
+    receive() returns (payload_len, dst, src, proto, payload) like ether_receive (0 = nothing
+    queued, negative = -errno); with trailer=True every recvmmsg batch is FCS-verified on the GPU,
+    failing frames are dropped and the 4-byte trailer is stripped."""
+
+    def __init__(self, fd: int, own_mac: bytes, max_batch: int = 64, trailer: bool = True):
+        self._mac = (ctypes.c_uint8 * 6)(*own_mac)
+        self._q = load().fcs_rxq_create(fd, self._mac, max_batch, 1 if trailer else 0)
+        if not self._q:
+            raise FcsError(-errno.EINVAL, "fcs_rxq_create")
+        self._hdr = (ctypes.c_uint8 * 14)()
+        self._buf = (ctypes.c_uint8 * 2048)()
+
+    def receive(self, bsize: int = 2048):
+        r = load().fcs_rxq_receive(self._q, self._hdr, self._buf, min(bsize, 2048))
+        if r <= 0:
+            return r, None, None, None, b""
+        h = bytes(self._hdr)
+        proto = int.from_bytes(h[12:14], "little")   # host-order u16 in the struct
+        return r, h[0:6], h[6:12], proto, bytes(self._buf[:min(r, bsize)])
+
+    def stats(self):
+        """(frames, bad_fcs, echoes, dropped, batches) since creation."""
+        v = [ctypes.c_uint64(0) for _ in range(5)]
+        load().fcs_rxq_stats(self._q, *[ctypes.byref(x) for x in v])
+        return tuple(int(x.value) for x in v)
+
+    def close(self) -> None:
+        if self._q:
+            load().fcs_rxq_destroy(self._q)
             self._q = None
 
     def __enter__(self):

@@ -13,7 +13,7 @@ import nstack_amd as na
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "nstack_fcs.h")
-HEADERS = [os.path.join(ROOT, "include", h) for h in ("nstack_fcs.h", "nstack_txq.h", "nstack_pcap.h", "nstack_inet.h")]
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("nstack_fcs.h", "nstack_txq.h", "nstack_pcap.h", "nstack_inet.h", "nstack_rxq.h")]
 
 
 def _declared():

@@ -1,0 +1,62 @@
+"""Batched RX call site with GPU FCS verification (include/nstack_rxq.h).
+
+Frames are built as ether_send builds them (src/linux/ether.c:257-263: header, payload, zero pad,
+little-endian FCS over the rest) so the trailer is exactly what a link with rx-fcs delivers; a few
+are corrupted. Expected: the good frames come out in order with the trailer stripped, the
+corrupted ones are counted and never handed out."""
+import random
+import socket
+import struct
+import zlib
+
+import pytest
+
+import nstack_amd as na
+
+pytestmark = pytest.mark.gpu
+
+OWN = bytes([2, 0, 0, 0, 0, 1])
+PEER = bytes([2, 0, 0, 0, 0, 2])
+
+
+def ether_send_frame(payload, proto=0x0800, src=PEER, dst=OWN):
+    body = dst + src + proto.to_bytes(2, "big") + payload + bytes(max(0, 56 - len(payload)))
+    return body + struct.pack("<I", zlib.crc32(body))
+
+
+@pytest.mark.parametrize("max_batch", [1, 7, 64])
+def test_rx_verify_drops_corrupted_frames(max_batch):
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+    b.setblocking(False)
+    rng = random.Random(max_batch)
+    sent, good = [], []
+    for i in range(300):
+        pl = bytes(rng.randrange(256) for _ in range(rng.choice([0, 1, 46, 100, 576, 1480, 1500])))
+        f = bytearray(ether_send_frame(pl, proto=0x0800 + (i & 7)))
+        kind = rng.random()
+        if kind < 0.1:
+            f[rng.randrange(len(f))] ^= 1 << rng.randrange(8)      # corrupted anywhere, trailer included
+        elif kind < 0.15:
+            f[6:12] = OWN                                           # own echo (refresh its FCS)
+            f[-4:] = struct.pack("<I", zlib.crc32(bytes(f[:-4])))
+        else:
+            good.append((max(len(pl), 56), 0x0800 + (i & 7), pl + bytes(max(0, 56 - len(pl)))))
+        sent.append(bytes(f))
+    for f in sent:
+        a.send(f)
+    got = []
+    with na.RxQueue(b.fileno(), OWN, max_batch=max_batch, trailer=True) as q:
+        while True:
+            n, dst, src, proto, pl = q.receive()
+            if n == 0:
+                break
+            assert n > 0, n
+            assert dst == OWN and src == PEER
+            got.append((n, proto, pl))
+        frames, bad, echoes, dropped, batches = q.stats()
+    a.close(), b.close()
+    assert got == good
+    assert frames == len(sent) and dropped == 0
+    assert bad + echoes + len(good) == len(sent) and bad > 0 and echoes > 0

@@ -1,0 +1,68 @@
+"""Batched RX call site (include/nstack_rxq.h) — host logic that needs no GPU.
+
+ether_receive (src/linux/ether.c:180-212): 0 when nothing is queued (:196-198), own-MAC echoes
+skipped (:202), host-order ethertype (:206), min(len - 14, bsize) payload bytes copied and len - 14
+returned (:208-211). Without a GPU the FCS-trailer mode must refuse to hand out unchecked frames.
+"""
+import os
+import socket
+
+import pytest
+
+import nstack_amd as na
+
+OWN = bytes([2, 0, 0, 0, 0, 1])
+PEER = bytes([2, 0, 0, 0, 0, 2])
+
+
+def _gpu_visible():
+    return os.path.exists("/dev/kfd")
+
+
+def frame(src, proto, payload, dst=OWN):
+    return dst + src + proto.to_bytes(2, "big") + payload
+
+
+@pytest.fixture
+def pair():
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    b.setblocking(False)
+    yield a, b
+    a.close(), b.close()
+
+
+def test_receive_semantics_without_trailer(pair):
+    a, b = pair
+    with na.RxQueue(b.fileno(), OWN, max_batch=4, trailer=False) as q:
+        assert q.receive() == (0, None, None, None, b"")            # nothing queued -> 0
+        a.send(frame(PEER, 0x0800, b"A" * 100))
+        a.send(frame(OWN, 0x0806, b"echo"))                         # own echo: skipped
+        a.send(b"short")                                            # runt: dropped
+        a.send(frame(PEER, 0x86DD, b"B" * 1500))                     # 1514 B: the largest kept
+        a.send(frame(PEER, 0x0800, b"C" * 1501))                     # 1515 B: oversize, dropped
+        a.send(frame(PEER, 0x0806, b"D" * 46))
+        n, dst, src, proto, pl = q.receive()
+        assert (n, dst, src, proto, pl) == (100, OWN, PEER, 0x0800, b"A" * 100)
+        n, _, _, proto, pl = q.receive(bsize=10)                    # len returned, 10 bytes copied
+        assert (n, proto, pl) == (1500, 0x86DD, b"B" * 10)
+        n, _, _, proto, pl = q.receive()
+        assert (n, proto, pl) == (46, 0x0806, b"D" * 46)
+        assert q.receive()[0] == 0
+        frames, bad, echoes, dropped, batches = q.stats()
+        assert (frames, bad, echoes, dropped) == (6, 0, 1, 2) and batches >= 2
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")
+def test_trailer_mode_fails_loudly_without_gpu(pair):
+    a, b = pair
+    with na.RxQueue(b.fileno(), OWN, max_batch=8, trailer=True) as q:
+        a.send(frame(PEER, 0x0800, bytes(60)) + bytes(4))
+        assert q.receive()[0] == -19                                # -ENODEV: nothing unchecked
+
+
+def test_bad_arguments():
+    lib = na.load()
+    assert lib.fcs_rxq_create(-1, OWN, 8, 0) is None
+    assert lib.fcs_rxq_create(3, OWN, 0, 0) is None
+    assert lib.fcs_rxq_create(3, OWN, 8, 2) is None
+    assert lib.fcs_rxq_receive(None, None, None, 0) == -22
