@@ -86,6 +86,11 @@ struct DevState {
     uint32_t *tx_dlen = nullptr, *tx_dout = nullptr; //   ... their device addresses
     uint64_t *tx_flag = nullptr, *tx_dflag = nullptr; // completion word (signal_kernel), mapped
     uint64_t tx_seq = 0;
+    uint64_t *vz_off = nullptr, *vz_doff = nullptr;  // small RX verify batches (same stream and lock):
+    uint32_t *vz_len = nullptr, *vz_dlen = nullptr;  //   offsets, lengths, ok flags and the bad count,
+    uint8_t *vz_ok = nullptr, *vz_dok = nullptr;     //   pinned and device-mapped; the kernel's bad
+    unsigned long long *vz_dbad = nullptr;           //   count goes to device scratch (no PCIe atomics)
+    uint64_t vz_cap = 0;
     uint64_t tx_cap = 0;
     std::mutex one_mu;       // single-frame (drop-in ether_fcs) staging
     hipStream_t one_stream = nullptr;
@@ -513,6 +518,51 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t stride, const uint32_
     return 0;
 }
 
+// Small RX verify batches in fcs_host_alloc memory (the RX queue's arena): the kernel reads the
+// frames and writes the ok flags and the bad count through mapped memory, one launch and a
+// completion word, as run_tx_zero_copy does for TX. Returns the bad count or -errno.
+int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena_bytes, const uint64_t *off,
+                             const uint32_t *len, uint8_t *ok, uint64_t n) {
+    std::lock_guard<std::mutex> lk(ds->tx_mu);
+    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    if (!ds->tx_stream) {
+        HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
+        HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dflag, ds->tx_flag, 0), "hipHostGetDevicePointer(flag)");
+        *ds->tx_flag = 0;
+    }
+    if (n > ds->vz_cap) {
+        if (ds->vz_off) hipHostFree(ds->vz_off);
+        if (ds->vz_len) hipHostFree(ds->vz_len);
+        if (ds->vz_ok) hipHostFree(ds->vz_ok);
+        if (!ds->vz_dbad) HIPTRY(hipMalloc(&ds->vz_dbad, 64), "hipMalloc(verify bad scratch)");
+        ds->vz_off = nullptr;
+        ds->vz_len = nullptr;
+        ds->vz_ok = nullptr;
+        ds->vz_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(n, 4096);
+        HIPTRY(hipHostMalloc(&ds->vz_off, cap * 8, hipHostMallocMapped), "hipHostMalloc(verify off)");
+        HIPTRY(hipHostMalloc(&ds->vz_len, cap * 4, hipHostMallocMapped), "hipHostMalloc(verify len)");
+        HIPTRY(hipHostMalloc(&ds->vz_ok, cap, hipHostMallocMapped), "hipHostMalloc(verify ok)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->vz_doff, ds->vz_off, 0), "hipHostGetDevicePointer(off)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->vz_dlen, ds->vz_len, 0), "hipHostGetDevicePointer(len)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->vz_dok, ds->vz_ok, 0), "hipHostGetDevicePointer(ok)");
+        ds->vz_cap = cap;
+    }
+    std::memcpy(ds->vz_off, off, n * 8);
+    std::memcpy(ds->vz_len, len, n * 4);
+    int rc = launch_var(ds, darena, arena_bytes, ds->vz_doff, ds->vz_dlen, nullptr, n, ds->tx_stream, ds->vz_dok,
+                        ds->vz_dbad);
+    if (rc) return rc;
+    const uint64_t v = ++ds->tx_seq;
+    HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
+    if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small verify batch"))) return rc;
+    std::memcpy(ok, ds->vz_ok, n);
+    int64_t bad = 0;
+    for (uint64_t i = 0; i < n; i++) bad += ok[i] == 0;
+    return bad;
+}
+
 int engine_devices(std::vector<DevState *> *out) {
     {
         std::lock_guard<std::mutex> lk(g_mu);
@@ -667,6 +717,10 @@ void fcs_engine_fini(void) {
         if (ds->tx_len) hipHostFree(ds->tx_len);
         if (ds->tx_out) hipHostFree(ds->tx_out);
         if (ds->tx_flag) hipHostFree(ds->tx_flag);
+        if (ds->vz_off) hipHostFree(ds->vz_off);
+        if (ds->vz_len) hipHostFree(ds->vz_len);
+        if (ds->vz_ok) hipHostFree(ds->vz_ok);
+        if (ds->vz_dbad) hipFree(ds->vz_dbad);
         if (ds->one_stream) hipStreamDestroy(ds->one_stream);
         if (ds->one_h) hipHostFree(ds->one_h);
         if (ds->one_hout) hipHostFree(ds->one_hout);
@@ -787,6 +841,14 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
         if (off[i] > arena_bytes || len[i] > arena_bytes - off[i])
             return fail(EINVAL, "frame %llu [%llu, +%u) outside the %llu-byte arena", (unsigned long long)i,
                         (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    if (arena_bytes <= kZeroCopyMaxBytes) {
+        if (const uint8_t *darena = pinned_dev_ptr(arena, arena_bytes)) {   // the RX queue's arena
+            std::vector<DevState *> devs;
+            const int rc = engine_devices(&devs);
+            if (rc) return rc;
+            return run_verify_zero_copy(devs[0], darena, arena_bytes, off, len, ok, n);
+        }
+    }
     std::atomic<uint64_t> bad{0};
     HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, nullptr, nullptr, 0, n, ok, &bad};
     const int rc = run_host_sharded(job, n);
