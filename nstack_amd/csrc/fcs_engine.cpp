@@ -310,26 +310,6 @@ int wait_flag(hipStream_t st, const uint64_t *flag, uint64_t v, const char *what
     }
 }
 
-// Pageable host frames are copied into pinned staging before their DMA; one core copies
-// ~28 GB/s, below PCIe Gen5 x16, so large spans are split over a few threads.
-constexpr uint64_t kCopySplitBytes = 16ull << 20;
-constexpr int kCopyThreads = 4;
-
-void staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes) {
-    if (bytes < kCopySplitBytes) {
-        std::memcpy(dst, src, bytes);
-        return;
-    }
-    const uint64_t part = ((bytes + kCopyThreads - 1) / kCopyThreads + 4095) & ~4095ull;
-    std::thread th[kCopyThreads - 1];
-    for (int t = 1; t < kCopyThreads; t++) {
-        const uint64_t a = std::min(bytes, part * t), z = std::min(bytes, part * (t + 1));
-        th[t - 1] = std::thread([=] { if (z > a) std::memcpy(dst + a, src + a, z - a); });
-    }
-    std::memcpy(dst, src, std::min(bytes, part));
-    for (auto &x : th) x.join();
-}
-
 bool is_pinned(const void *p) {
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) != hipSuccess) {
@@ -450,7 +430,7 @@ int run_host_job(DevState *ds, const HostJob &job) {
                 }
             }
             if (!src_pinned) {
-                staging_copy(pp.h_in[b], src, span);
+                fcs::staging_copy(pp.h_in[b], src, span);
                 src = pp.h_in[b];
             }
         }
@@ -636,6 +616,25 @@ int run_host_sharded(HostJob job, uint64_t n) {
 }
 
 }  // namespace
+
+// Pageable host bytes are copied into pinned staging before their DMA; one core copies
+// ~28 GB/s, below PCIe Gen5 x16, so large spans are split over a few threads.
+void fcs::staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes) {
+    constexpr uint64_t kCopySplitBytes = 16ull << 20;
+    constexpr int kCopyThreads = 4;
+    if (bytes < kCopySplitBytes) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const uint64_t part = ((bytes + kCopyThreads - 1) / kCopyThreads + 4095) & ~4095ull;
+    std::thread th[kCopyThreads - 1];
+    for (int t = 1; t < kCopyThreads; t++) {
+        const uint64_t a = std::min(bytes, part * t), z = std::min(bytes, part * (t + 1));
+        th[t - 1] = std::thread([=] { if (z > a) std::memcpy(dst + a, src + a, z - a); });
+    }
+    std::memcpy(dst, src, std::min(bytes, part));
+    for (auto &x : th) x.join();
+}
 
 int fcs::current_device(int *dev, int *cus) {
     DevState *ds = nullptr;

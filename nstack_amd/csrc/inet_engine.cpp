@@ -141,7 +141,7 @@ int run_host(int mode, const uint8_t *arena, const uint64_t *off, const uint32_t
         if (hi - lo <= kChunkBytes) {   // dense: one span copy, offsets rebased (alignment kept mod 16)
             const uint64_t pad = lo & 15;
             span = pad + (hi - lo);
-            std::memcpy(s.h_in + pad, arena + lo, hi - lo);
+            fcs::staging_copy(s.h_in + pad, arena + lo, hi - lo);
             for (uint64_t q = 0; q < np; q++) s.h_off[q] = off[i + q] - lo + pad;
         } else {                        // sparse: gather back to back (any start alignment is fine)
             uint64_t w = 0;

@@ -101,6 +101,24 @@ def main():
                             "metadata_bytes": m * 12,
                             "spot_bad": spot("ip", arena, off.cpu().numpy(), ln_np, None, got)}
         print("imix_128M", json.dumps(res["imix_128M"]), flush=True)
+    if "host" not in a.skip:   # host-inclusive: packets in pageable host memory, results back to host
+        m = (4 << 30) // S
+        host = np.random.default_rng(3).integers(0, 256, m * S + 64, dtype=np.uint8)
+        off = (14 + np.arange(m, dtype=np.uint64) * S).astype(np.uint64)
+        ln = np.full(m, 1500, dtype=np.uint32)
+        out = np.zeros(m, dtype=np.uint16)
+        na.inet_batch_host("ip", host, host.nbytes, off[:1024], ln[:1024], None, out, 1024)   # warm
+        import time
+        t0 = time.perf_counter()
+        na.inet_batch_host("ip", host, host.nbytes, off, ln, None, out, m)
+        dt = time.perf_counter() - t0
+        bad = 0
+        for i in rng.integers(0, m, 48):
+            o = int(off[i])
+            bad += int(witness("ip", host[o:o + 1500].tobytes()) != int(out[i]))
+        res["host_ip_1500_pageable"] = {"packets": m, "bytes": m * 1500, "s": dt, "GB_s": m * 1500 / dt / 1e9,
+                                        "Mpkt_s": m / dt / 1e6, "spot_bad": bad}
+        print("host_ip_1500_pageable", json.dumps(res["host_ip_1500_pageable"]), flush=True)
     print(json.dumps(res, indent=1), flush=True)
 
 
