@@ -125,12 +125,16 @@ int run_host(int mode, const uint8_t *arena, const uint64_t *off, const uint32_t
         Slot &s = hp->slot[b];
         int rc = drain(s);
         if (rc) return rc;
-        // the chunk [i, e): at most kChunkPkts packets and kChunkBytes of packet bytes
+        // the chunk [i, e): at most kChunkPkts packets, kChunkBytes of packet bytes, and (so that
+        // densely packed packets go over as one span copy) a span of at most kChunkBytes unless
+        // the packets are sparse (span > 2x their bytes), which are gathered instead
         uint64_t e = i, sum = 0, lo = UINT64_MAX, hi = 0;
         while (e < n && e - i < kChunkPkts && sum + len[e] <= kChunkBytes) {
+            const uint64_t nlo = std::min(lo, off[e]), nhi = std::max(hi, off[e] + len[e]);
+            if (e > i && nhi - nlo > kChunkBytes && nhi - nlo <= 2 * (sum + len[e])) break;
             sum += len[e];
-            lo = std::min(lo, off[e]);
-            hi = std::max(hi, off[e] + len[e]);
+            lo = nlo;
+            hi = nhi;
             e++;
         }
         if (e == i)
