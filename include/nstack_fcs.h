@@ -15,6 +15,7 @@
  *   ether_fcs_tx_host()         TX mode of the same call site: computes the FCS over the first
  *                               len bytes of each frame and stores it little-endian right after
  *                               them, exactly as src/linux/ether.c:262-263 does per frame.
+ *   ether_fcs_tx_batch_host()   the same over arena + offsets (the TX queue's batches).
  *   ether_fcs_*_dev()           device-resident forms (frames already in HBM).
  *
  * Semantics (all entry points): out[i] == ether_fcs(frame_i, len_i) of the reference, i.e.
@@ -78,6 +79,12 @@ int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64
  * first len[i] bytes is written little-endian at base[i*stride + len[i] .. +4). Requires
  * len[i] + 4 <= stride. Frames are modified in place in host memory. */
 int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n);
+/* TX mode over the packed-arena layout: frame i is arena[off[i] .. +len[i]) and
+ * its FCS goes to arena[off[i] + len[i] .. +4), which must lie inside [arena, arena +
+ * arena_bytes). Frames must not overlap each other's FCS bytes. Batches of up to 64 MiB in
+ * fcs_host_alloc memory are read and answered in place (no staging copies). */
+int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *off,
+                            const uint32_t *len, uint64_t n);
 
 /* ---- RX verification (new behaviour: the reference's ether_receive,
  *      src/linux/ether.c:180-212, checks no FCS) ----
@@ -95,7 +102,7 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
                               const uint32_t *len, uint8_t *ok, uint64_t n);
 
 /* ---- pinned host memory for zero-copy-staging callers (optional) ----
- * Pinned, device-mapped, portable host memory. Small TX batches in it (ether_fcs_tx_host) are
+ * Pinned, device-mapped, portable host memory. TX and verify batches of up to 64 MiB in it are
  * read by the kernel in place. Release it with fcs_host_free only (the engine keeps the range's
  * device address until then). */
 void *fcs_host_alloc(uint64_t bytes);

@@ -16,14 +16,14 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fcs.so")
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
-           "batch_host", "tx_host", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
+           "batch_host", "tx_host", "tx_batch_host", "host_buffer", "host_free", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
            "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
     "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
-    "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_verify_dev",
+    "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
     "fcs_tables_blob",
@@ -77,6 +77,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "ether_fcs_batch_host": (i32, [vp, u64, vp, vp, vp, u64]),
         "ether_fcs_fixed_host": (i32, [vp, u64, u32, u64, vp]),
         "ether_fcs_tx_host": (i32, [vp, u64, vp, u64]),
+        "ether_fcs_tx_batch_host": (i32, [vp, u64, vp, vp, u64]),
         "ether_fcs_verify_dev": (i32, [vp, u64, vp, vp, vp, vp, u64, vp]),
         "ether_fcs_verify_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, vp]),
         "ether_fcs_verify_host": (c.c_int64, [vp, u64, vp, vp, vp, u64]),
@@ -201,6 +202,25 @@ def batch_host(arena, arena_bytes: int, off, length, out, n: int) -> None:
 
 def tx_host(base, stride: int, length, n: int) -> None:
     _check(load().ether_fcs_tx_host(_ptr(base), stride, _ptr(length), n), "ether_fcs_tx_host")
+
+
+def tx_batch_host(arena, arena_bytes: int, off, length, n: int) -> None:
+    """TX mode over arena + offsets: the FCS of arena[off[i], +len[i]) lands at off[i] + len[i]."""
+    _check(load().ether_fcs_tx_batch_host(_ptr(arena), arena_bytes, _ptr(off), _ptr(length), n),
+           "ether_fcs_tx_batch_host")
+
+
+def host_buffer(nbytes: int):
+    """fcs_host_alloc'd (pinned, device-mapped) bytes as a numpy uint8 array; free with host_free."""
+    import numpy as np
+    p = load().fcs_host_alloc(nbytes)
+    if not p:
+        raise FcsError(f"fcs_host_alloc({nbytes}): {load().fcs_last_error().decode()}")
+    return np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+
+
+def host_free(arr) -> None:
+    load().fcs_host_free(arr.ctypes.data)
 
 
 def verify_dev(arena, arena_bytes: int, off, length, ok, bad, n: int, stream=None) -> None:

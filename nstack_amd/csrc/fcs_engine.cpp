@@ -84,6 +84,7 @@ struct DevState {
     hipStream_t tx_stream = nullptr;
     uint32_t *tx_len = nullptr, *tx_out = nullptr;   // pinned, device-mapped
     uint32_t *tx_dlen = nullptr, *tx_dout = nullptr; //   ... their device addresses
+    uint64_t *tx_off = nullptr, *tx_doff = nullptr;  // frame offsets (ether_fcs_tx_batch_host)
     uint64_t *tx_flag = nullptr, *tx_dflag = nullptr; // completion word (signal_kernel), mapped
     uint64_t tx_seq = 0;
     uint64_t *vz_off = nullptr, *vz_doff = nullptr;  // small RX verify batches (same stream and lock):
@@ -362,7 +363,7 @@ int run_host_job(DevState *ds, const HostJob &job) {
                 if (c != kResidue) job.bad->fetch_add(1, std::memory_order_relaxed);
             }
             if (job.tx_base) {   // src/linux/ether.c:263 — memcpy of the host-order u32
-                uint8_t *dst = job.tx_base + i * job.stride + job.len[i];
+                uint8_t *dst = job.tx_base + (job.off ? job.off[i] : i * job.stride) + job.len[i];
                 std::memcpy(dst, &c, 4);
             }
         }
@@ -459,9 +460,13 @@ int run_host_job(DevState *ds, const HostJob &job) {
 // Small TX batches in pinned memory (the TX queue's arenas): no staging copies — the kernel reads
 // the frames and writes the FCSs through device-mapped pinned memory, one launch, one sync; the
 // host then stores each FCS little-endian after its covered bytes (src/linux/ether.c:263).
-constexpr uint64_t kZeroCopyMaxBytes = 8ull << 20;
+#ifndef FCS_ZC_MAX_MB   // measurement builds (tools/variants.sh) move the limit
+#define FCS_ZC_MAX_MB 64
+#endif
+constexpr uint64_t kZeroCopyMaxBytes = (uint64_t)FCS_ZC_MAX_MB << 20;
 
-int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t stride, const uint32_t *len, uint64_t n) {
+int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t stride, const uint64_t *off,
+                     const uint32_t *len, uint64_t n) {
     std::lock_guard<std::mutex> lk(ds->tx_mu);
     HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
     if (!ds->tx_stream) {
@@ -473,28 +478,33 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t stride, const uint32_
     if (n > ds->tx_cap) {
         if (ds->tx_len) hipHostFree(ds->tx_len);
         if (ds->tx_out) hipHostFree(ds->tx_out);
+        if (ds->tx_off) hipHostFree(ds->tx_off);
         ds->tx_len = ds->tx_out = nullptr;
+        ds->tx_off = nullptr;
         ds->tx_cap = 0;
         const uint64_t cap = std::max<uint64_t>(n, 4096);
         HIPTRY(hipHostMalloc(&ds->tx_len, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx len)");
         HIPTRY(hipHostMalloc(&ds->tx_out, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx out)");
+        HIPTRY(hipHostMalloc(&ds->tx_off, cap * 8, hipHostMallocMapped), "hipHostMalloc(tx off)");
         HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dlen, ds->tx_len, 0), "hipHostGetDevicePointer(len)");
         HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dout, ds->tx_out, 0), "hipHostGetDevicePointer(out)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_doff, ds->tx_off, 0), "hipHostGetDevicePointer(off)");
         ds->tx_cap = cap;
     }
     std::memcpy(ds->tx_len, len, n * 4);
-    void *dbase = pinned_dev_ptr(base, n * stride);   // our own arenas: no HIP query
+    if (off) std::memcpy(ds->tx_off, off, n * 8);
+    void *dbase = pinned_dev_ptr(base, bytes);   // our own arenas: no HIP query
     if (!dbase && hipHostGetDevicePointer(&dbase, base, 0) != hipSuccess) {   // pinned but not mapped
         (void)hipGetLastError();
         return 1;
     }
-    int rc = launch_var(ds, dbase, n * stride, nullptr, ds->tx_dlen, ds->tx_dout, n, ds->tx_stream, nullptr, nullptr,
-                        stride);
+    int rc = launch_var(ds, dbase, bytes, off ? ds->tx_doff : nullptr, ds->tx_dlen, ds->tx_dout, n, ds->tx_stream,
+                        nullptr, nullptr, off ? 0 : stride);
     if (rc) return rc;
     const uint64_t v = ++ds->tx_seq;
     HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
     if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small TX batch"))) return rc;
-    for (uint64_t i = 0; i < n; i++) std::memcpy(base + i * stride + len[i], &ds->tx_out[i], 4);
+    for (uint64_t i = 0; i < n; i++) std::memcpy(base + (off ? off[i] : i * stride) + len[i], &ds->tx_out[i], 4);
     return 0;
 }
 
@@ -797,11 +807,31 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
         std::vector<DevState *> devs;
         int rc = engine_devices(&devs);
         if (rc) return rc;
-        rc = run_tx_zero_copy(devs[0], (uint8_t *)base, stride, len, n);
+        rc = run_tx_zero_copy(devs[0], (uint8_t *)base, n * stride, stride, nullptr, len, n);
         if (rc <= 0) return rc;   // 1: the frames are not device-mapped; take the staged pipeline
     }
     HostJob job{(const uint8_t *)base, n * stride, nullptr, len, stride, 0, nullptr, (uint8_t *)base, 0, n,
                 nullptr, nullptr};
+    return run_host_sharded(job, n);
+}
+
+int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
+                            uint64_t n) {
+    if (n == 0) return 0;
+    if (!arena || !off || !len) return fail(EINVAL, "null pointer");
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i] > arena_bytes || (uint64_t)len[i] + 4 > arena_bytes - off[i])
+            return fail(EINVAL, "frame %llu [%llu, +%u) and its FCS outside the %llu-byte arena",
+                        (unsigned long long)i, (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    if (arena_bytes <= kZeroCopyMaxBytes && (pinned_dev_ptr(arena, arena_bytes) || is_pinned(arena))) {
+        std::vector<DevState *> devs;
+        int rc = engine_devices(&devs);
+        if (rc) return rc;
+        rc = run_tx_zero_copy(devs[0], (uint8_t *)arena, arena_bytes, 0, off, len, n);
+        if (rc <= 0) return rc;
+    }
+    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, nullptr, (uint8_t *)arena, 0, n, nullptr,
+                nullptr};
     return run_host_sharded(job, n);
 }
 

@@ -4,6 +4,12 @@
 // (:257-263), -EMSGSIZE rule (:222-224, :234-237), per-call return value (:265-269) — while the
 // FCS of every frame queued by any thread is computed in one GPU batch (ether_fcs_tx_host) and
 // the batch is handed to the sink at once (sendmmsg). The CRC itself is never computed here.
+//
+// Producers reserve slots with one atomic add on a reservation word, and the open batch is split
+// into up to 16 shards, each with its own word on its own cache line: a thread reserves in its
+// home shard (threads are dealt homes round-robin) and moves to higher shards only when that one
+// is full, so producers on different threads do not bounce one line between cores. Frames leave
+// in shard order, which keeps every thread's own frames in the order it sent them (see enqueue).
 #include <arpa/inet.h>
 #include <linux/if_packet.h>
 #include <sys/socket.h>
@@ -58,22 +64,38 @@ struct alignas(64) SlotMeta {
 };
 
 struct Batch {
-    uint8_t *arena = nullptr;            // cap slots of kStride bytes (pinned when possible)
-    bool pinned = false;
+    uint8_t *arena = nullptr;            // cap slots of kStride bytes (pinned when possible);
+    bool pinned = false;                 //   shard k owns slots [k * per, (k + 1) * per)
     std::vector<SlotMeta> meta;          // per slot, one cache line each (written by its producer)
-    std::vector<uint32_t> covered;       // FCS-covered bytes (frame_size - 4) per slot (flusher)
-    std::vector<uint32_t> sizes;         // frame_size per slot
+    // the frames that leave, in shard order (filled by the flusher)
+    std::vector<uint32_t> slot;          // arena slot of each
+    std::vector<uint64_t> off;           // its byte offset in the arena
+    std::vector<uint32_t> covered;       // FCS-covered bytes (frame_size - 4)
+    std::vector<uint32_t> sizes;         // frame_size
     std::vector<uint8_t *> frames;
     std::vector<int> res;
-    std::atomic<int64_t> first_ns{0};    // when slot 0 was reserved (0: not yet stamped)
+    std::atomic<int64_t> first_ns{0};    // when the batch's first frame was reserved (0: not yet)
 };
 
-// The open batch and its fill level in one word, so producers reserve slots with one atomic add
-// and no lock: bits 63..32 = batch sequence number (the batch lives in b[seq & 1]), 31..0 = slots
-// reserved. The flusher closes a batch by swapping in (seq + 1, 0).
+// A shard's open batch and its fill level in one word, so producers reserve slots with one atomic
+// add and no lock: bits 63..32 = batch sequence number (the batch lives in b[seq & 1]), 31..0 =
+// slots reserved. The flusher closes a batch by swapping (seq + 1, 0) into every shard.
 inline uint64_t st_pack(uint64_t seq, uint32_t r) { return (seq << 32) | r; }
 inline uint64_t st_seq(uint64_t s) { return s >> 32; }
 inline uint32_t st_res(uint64_t s) { return (uint32_t)s; }
+
+constexpr uint32_t kMaxShards = 16;
+constexpr uint32_t kMinShardSlots = 64;
+struct alignas(64) Shard {
+    std::atomic<uint64_t> st{0};
+};
+
+// Home shard of the calling thread: threads are numbered in the order they first send.
+std::atomic<uint32_t> g_thread_count{0};
+uint32_t thread_number() {
+    thread_local const uint32_t t = g_thread_count.fetch_add(1, std::memory_order_relaxed);
+    return t;
+}
 
 }  // namespace
 
@@ -82,9 +104,11 @@ struct fcs_txq {
     uint32_t cap = 0, flush_usec = 0;
     fcs_txq_sink_fn sink = nullptr;
     void *ctx = nullptr;
+    uint32_t nsh = 1, per = 0;            // shards, slots per shard (cap = nsh * per)
     Batch b[2];
-    std::atomic<uint64_t> st{0};          // (open batch seq, slots reserved): see st_pack
+    Shard sh[kMaxShards];                 // (open batch seq, slots reserved) per shard: see st_pack
     std::atomic<bool> idle{false};        // flusher asleep waiting for a first frame
+    std::atomic<bool> blocked{false};     // a producer found every shard it may use full
     std::atomic<bool> stop_req{false};
     // slow paths (sleeping, flush(), statistics) take mu
     std::mutex mu;
@@ -105,44 +129,64 @@ uint64_t flush_target(fcs_txq *q) {
     return q->flush_target;
 }
 
-// Wait until the open batch has a frame to leave with; returns false when stopping with nothing
-// left. Decides like the locked version did: leave when full, when flush() asks, at once when
-// flush_usec == 0, else after the oldest frame has lingered flush_usec.
-bool wait_for_batch(fcs_txq *q, uint64_t seq) {
+// Slots reserved in the open batch over all shards (each capped at its size).
+uint32_t reserved(fcs_txq *q, std::memory_order mo) {
+    uint32_t r = 0;
+    for (uint32_t k = 0; k < q->nsh; k++) r += std::min(st_res(q->sh[k].st.load(mo)), q->per);
+    return r;
+}
+
+enum class Leave { kStop, kSend };
+
+// Wait until the open batch has a frame to leave with; kStop when stopping with nothing left.
+// Leaves when full (or a producer is stuck behind a full home shard), when flush() asks, at once
+// when flush_usec == 0, else after the oldest frame has lingered flush_usec. *closed_empty gets
+// the shards the stop path sealed while still empty (they hold no frames).
+Leave wait_for_batch(fcs_txq *q, uint64_t seq, uint32_t *closed_empty) {
+    *closed_empty = 0;
     for (;;) {
-        uint64_t s = q->st.load(std::memory_order_seq_cst);
-        uint32_t r = st_res(s);
+        uint32_t r = reserved(q, std::memory_order_seq_cst);
         const bool stop = q->stop_req.load(std::memory_order_acquire);
         if (r == 0) {
-            // stopping: mark the empty batch full so no producer can slip a frame in after we
-            // leave (it then sees stop_req and returns -ESHUTDOWN); lost the race: send it
+            // stopping: mark every empty shard full so no producer can slip a frame in after we
+            // leave (it then sees stop_req and returns -ESHUTDOWN); lost a race: send what came
             if (stop) {
-                if (q->st.compare_exchange_strong(s, st_pack(seq, q->cap), std::memory_order_seq_cst)) return false;
-                continue;
+                bool all = true;
+                for (uint32_t k = 0; k < q->nsh; k++) {
+                    uint64_t s = st_pack(seq, 0);
+                    if (q->sh[k].st.compare_exchange_strong(s, st_pack(seq, q->per), std::memory_order_seq_cst))
+                        *closed_empty |= 1u << k;
+                    else
+                        all = false;
+                }
+                if (all) return Leave::kStop;
+                return Leave::kSend;
             }
             // idle: spin a little for the next frame, then sleep until a producer, flush() or
-            // destroy wakes us (a producer taking slot 0 notifies when it sees idle set)
+            // destroy wakes us (a producer taking a shard's slot 0 notifies when it sees idle set)
             const auto until = Clock::now() + kSpin;
-            while (st_res(q->st.load(std::memory_order_acquire)) == 0 && Clock::now() < until &&
+            while (reserved(q, std::memory_order_acquire) == 0 && Clock::now() < until &&
                    !q->stop_req.load(std::memory_order_acquire))
                 cpu_relax();
             std::unique_lock<std::mutex> lk(q->mu);
             q->idle.store(true, std::memory_order_seq_cst);
-            while (st_res(q->st.load(std::memory_order_seq_cst)) == 0 && !q->stop_req.load(std::memory_order_seq_cst))
+            while (reserved(q, std::memory_order_seq_cst) == 0 && !q->stop_req.load(std::memory_order_seq_cst))
                 q->cv_flusher.wait(lk);
             q->idle.store(false, std::memory_order_relaxed);
             continue;
         }
-        if (r >= q->cap || stop || q->flush_usec == 0 || flush_target(q) >= seq) return true;
+        if (r >= q->cap || stop || q->flush_usec == 0 || q->blocked.load(std::memory_order_acquire) ||
+            flush_target(q) >= seq)
+            return Leave::kSend;
         // linger for company. Short lingers spin: a timed futex sleep is rounded up by the kernel's
         // timer slack (50 us by default), longer than the whole GPU step.
         Batch &B = q->b[seq & 1];
         int64_t f = B.first_ns.load(std::memory_order_acquire);
-        if (f == 0) f = now_ns();   // slot 0's producer has not stamped it yet
+        if (f == 0) f = now_ns();   // the first frame's producer has not stamped it yet
         const int64_t deadline = f + (int64_t)q->flush_usec * 1000;
         if (q->flush_usec <= 1000) {
-            while (now_ns() < deadline && st_res(q->st.load(std::memory_order_acquire)) < q->cap &&
-                   !q->stop_req.load(std::memory_order_acquire))
+            while (now_ns() < deadline && reserved(q, std::memory_order_acquire) < q->cap &&
+                   !q->blocked.load(std::memory_order_acquire) && !q->stop_req.load(std::memory_order_acquire))
                 cpu_relax();
         } else {
             std::unique_lock<std::mutex> lk(q->mu);
@@ -153,26 +197,33 @@ bool wait_for_batch(fcs_txq *q, uint64_t seq) {
             q->cv_flusher.wait_for(lk, left);
 #endif
         }
-        if (now_ns() >= deadline) return true;
+        if (now_ns() >= deadline) return Leave::kSend;
     }
 }
 
 void flusher(fcs_txq *q) {
     for (;;) {
-        const uint64_t seq = st_seq(q->st.load(std::memory_order_acquire));
-        if (!wait_for_batch(q, seq)) {   // stopping, nothing queued
+        const uint64_t seq = st_seq(q->sh[0].st.load(std::memory_order_acquire));
+        uint32_t closed_empty = 0;
+        if (wait_for_batch(q, seq, &closed_empty) == Leave::kStop) {   // stopping, nothing queued
             std::lock_guard<std::mutex> lk(q->mu);
             q->seq_done = seq - 1;
             q->cv_prod.notify_all();
             return;
         }
         // close batch seq: producers move on to b[(seq + 1) & 1], which the previous iteration
-        // finished with (its results were delivered before we got here)
+        // finished with (its results were delivered before we got here). Shards are closed from
+        // the highest down, so a thread climbing from its home shard never finds a closed shard
+        // below an open one (enqueue relies on it for per-thread order).
         Batch *B = &q->b[seq & 1];
         Batch &N = q->b[(seq + 1) & 1];
         N.first_ns.store(0, std::memory_order_relaxed);
-        const uint64_t old = q->st.exchange(st_pack(seq + 1, 0), std::memory_order_acq_rel);
-        const uint32_t n = std::min(st_res(old), q->cap);   // producers past cap got no slot
+        uint32_t nk[kMaxShards];
+        for (uint32_t k = q->nsh; k-- > 0;) {
+            const uint64_t old = q->sh[k].st.exchange(st_pack(seq + 1, 0), std::memory_order_acq_rel);
+            nk[k] = (closed_empty >> k) & 1 ? 0 : std::min(st_res(old), q->per);   // past per: no slot
+        }
+        q->blocked.store(false, std::memory_order_release);
         {
             std::lock_guard<std::mutex> lk(q->mu);   // producers waiting for a free slot
             q->cv_prod.notify_all();
@@ -181,17 +232,26 @@ void flusher(fcs_txq *q) {
         const uint64_t pickup = f ? (uint64_t)std::max<int64_t>(0, now_ns() - f) : 0;
 
         const auto t0 = Clock::now();
-        for (uint32_t i = 0; i < n; i++) {   // every reserved slot assembled by its producer
-            while (B->meta[i].ready.load(std::memory_order_acquire) != seq) std::this_thread::yield();
-            B->covered[i] = B->meta[i].covered;
+        uint32_t n = 0;
+        for (uint32_t k = 0; k < q->nsh; k++) {
+            for (uint32_t j = 0; j < nk[k]; j++, n++) {   // every reserved slot assembled by its producer
+                const uint32_t slot = k * q->per + j;
+                SlotMeta &m = B->meta[slot];
+                while (m.ready.load(std::memory_order_acquire) != seq) std::this_thread::yield();
+                B->slot[n] = slot;
+                B->off[n] = (uint64_t)slot * kStride;
+                B->covered[n] = m.covered;
+            }
         }
         const auto t1 = Clock::now();
         // FCS of every frame, written little-endian after its covered bytes (ether.c:262-263)
-        const int rc = ether_fcs_tx_host(B->arena, kStride, B->covered.data(), n);
+        // the span the frames occupy (not the whole arena): it decides the engine's in-place path
+        const uint64_t span = n ? B->off[n - 1] + kStride : 0;
+        const int rc = ether_fcs_tx_batch_host(B->arena, span, B->off.data(), B->covered.data(), n);
         const auto t2 = Clock::now();
         if (rc == 0) {
             for (uint32_t i = 0; i < n; i++) {
-                B->frames[i] = B->arena + (uint64_t)i * kStride;
+                B->frames[i] = B->arena + B->off[i];
                 B->sizes[i] = B->covered[i] + kFcsLen;
                 B->res[i] = -EIO;   // a sink that forgets a frame reports it as failed
             }
@@ -210,7 +270,7 @@ void flusher(fcs_txq *q) {
         q->ns_pickup += pickup;
         for (uint32_t i = 0; i < n; i++) {
             if (B->res[i] != (int)(B->covered[i] + kFcsLen)) q->n_errors++;
-            if (Waiter *w = B->meta[i].w) {   // null: fcs_txq_send_async
+            if (Waiter *w = B->meta[B->slot[i]].w) {   // null: fcs_txq_send_async
                 w->result = B->res[i];
                 w->done.store(true, std::memory_order_release);   // last touch: w may vanish now
             }
@@ -233,6 +293,12 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
     if (!q) return nullptr;
     std::memcpy(q->mac, src_mac, 6);
     q->cap = max_batch;
+    // as many shards (a power of two, at most 16) as split the batch into equal parts of at
+    // least kMinShardSlots slots
+    q->nsh = 1;
+    while (q->nsh < kMaxShards && max_batch % (2 * q->nsh) == 0 && max_batch / (2 * q->nsh) >= kMinShardSlots)
+        q->nsh *= 2;
+    q->per = max_batch / q->nsh;
     q->flush_usec = flush_usec;
     q->sink = sink;
     q->ctx = sink_ctx;
@@ -247,12 +313,14 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
             return nullptr;
         }
         B.meta = std::vector<SlotMeta>(max_batch);
+        B.slot.assign(max_batch, 0);
+        B.off.assign(max_batch, 0);
         B.covered.assign(max_batch, 0);
         B.sizes.assign(max_batch, 0);
         B.frames.assign(max_batch, nullptr);
         B.res.assign(max_batch, 0);
     }
-    q->st.store(st_pack(1, 0));
+    for (uint32_t k = 0; k < q->nsh; k++) q->sh[k].st.store(st_pack(1, 0));
     q->th = std::thread(flusher, q);
     return q;
 }
@@ -260,44 +328,62 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
 }  // extern "C"
 
 namespace {
-// Reserve a slot in the open batch (one fetch_add, no lock), assemble the frame there and mark it
-// ready.
+// Reserve a slot in the open batch (one fetch_add on the home shard's word, no lock), assemble the
+// frame there and mark it ready.
 // w == nullptr: fire-and-forget (the result only feeds the error counter).
+//
+// Per-thread order: a thread only climbs from its home shard to higher ones, and the flusher
+// closes shards from the highest down, so every shard a thread can still reserve in after a slot in
+// shard k of batch s is either shard >= k of batch s or a shard of a later batch. Batches leave in
+// sequence and a batch's frames leave in (shard, slot) order, so a thread's frames leave in the
+// order it queued them.
 int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize, Waiter *w) {
     if (!q || !dst || (!buf && bsize)) return -EINVAL;
     const size_t frame_size = kHeaderLen + std::max<size_t>(bsize, kMinPayload) + kFcsLen;   // :222-224
     if (frame_size > kSlot) return -EMSGSIZE;                                                // :234-237
-    uint64_t s;
+    const uint32_t home = thread_number() % q->nsh;
+    uint64_t s = 0;
+    uint32_t k = home;
     for (;;) {
         if (q->stop_req.load(std::memory_order_acquire)) return -ESHUTDOWN;
-        s = q->st.load(std::memory_order_acquire);
-        if (st_res(s) < q->cap) {
-            // one fetch_add; a producer that overshoots the full batch got no slot and retries
-            // after the swap (the flusher takes min(reserved, cap))
-            s = q->st.fetch_add(1, std::memory_order_seq_cst);
-            if (st_res(s) < q->cap) break;
+        const uint64_t seq0 = st_seq(q->sh[home].st.load(std::memory_order_acquire));
+        bool got = false;
+        for (k = home; k < q->nsh && !got; k++) {
+            s = q->sh[k].st.load(std::memory_order_acquire);
+            if (st_res(s) < q->per) {
+                // one fetch_add; a producer that overshoots a full shard got no slot and moves on
+                // (the flusher takes min(reserved, per))
+                s = q->sh[k].st.fetch_add(1, std::memory_order_seq_cst);
+                got = st_res(s) < q->per;
+            }
         }
-        // batch full: wait for the flusher to swap in the next one
-        const uint64_t seq = st_seq(s);
+        if (got) {
+            k--;
+            break;
+        }
+        // every shard from home up is full: have the flusher close the batch and wait for it
+        q->blocked.store(true, std::memory_order_release);
         const auto until = Clock::now() + kSpin;
-        while (st_seq(q->st.load(std::memory_order_acquire)) == seq && Clock::now() < until) cpu_relax();
+        while (st_seq(q->sh[home].st.load(std::memory_order_acquire)) == seq0 && Clock::now() < until) cpu_relax();
         std::unique_lock<std::mutex> lk(q->mu);
-        while (st_seq(q->st.load(std::memory_order_acquire)) == seq && !q->stop_req.load(std::memory_order_acquire)) {
+        while (st_seq(q->sh[home].st.load(std::memory_order_acquire)) == seq0 &&
+               !q->stop_req.load(std::memory_order_acquire)) {
             q->cv_flusher.notify_one();
             q->cv_prod.wait(lk);
         }
     }
     const uint64_t seq = st_seq(s);
-    const uint32_t slot = st_res(s);
+    const uint32_t slot = k * q->per + st_res(s);
     Batch &B = q->b[seq & 1];
-    if (slot == 0) {
-        B.first_ns.store(now_ns(), std::memory_order_release);
+    if (st_res(s) == 0) {
+        int64_t zero = 0;
+        B.first_ns.compare_exchange_strong(zero, now_ns(), std::memory_order_acq_rel);
         if (q->idle.load(std::memory_order_seq_cst)) {   // the flusher went to sleep: wake it
             std::lock_guard<std::mutex> lk(q->mu);
             q->cv_flusher.notify_one();
         }
     }
-    if (slot + 1 == q->cap && q->flush_usec > 1000) {   // a long linger sleeps: a full batch ends it
+    if (st_res(s) + 1 == q->per && q->flush_usec > 1000) {   // a long linger sleeps: a full shard may end it
         std::lock_guard<std::mutex> lk(q->mu);
         q->cv_flusher.notify_one();
     }
@@ -340,8 +426,14 @@ int fcs_txq_send_async(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const
 
 int fcs_txq_flush(fcs_txq_t *q) {
     if (!q) return -EINVAL;
-    const uint64_t s = q->st.load(std::memory_order_seq_cst);
-    const uint64_t target = st_res(s) ? st_seq(s) : st_seq(s) - 1;   // the open batch, else the one in flight
+    // per shard: the open batch if it holds frames, else the one before it; the latest of these.
+    // A frame this thread queued is in a shard whose word now names its batch with res > 0, or a
+    // later batch: either way the target covers it, even while a close is half way through.
+    uint64_t target = 0;
+    for (uint32_t k = 0; k < q->nsh; k++) {
+        const uint64_t s = q->sh[k].st.load(std::memory_order_seq_cst);
+        target = std::max(target, st_res(s) ? st_seq(s) : st_seq(s) - 1);
+    }
     std::unique_lock<std::mutex> lk(q->mu);
     q->flush_target = std::max(q->flush_target, target);
     q->cv_flusher.notify_one();

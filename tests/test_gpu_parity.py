@@ -271,6 +271,43 @@ def test_tx_mode_matches_ether_send_layout(dev, var_kernel, oracle):
         assert oracle.oracle_ether_fcs(frames[i].ctypes.data, fs) == 0x2144DF1C
 
 
+@pytest.mark.parametrize("where,count", [("pageable", 3000), ("pinned", 3000), ("pageable", 12000)])
+def test_tx_batch_host_offsets(dev, oracle, where, count):
+    """ether_fcs_tx_batch_host: ether_send's FCS placement (src/linux/ether.c:262-263) over the
+    packed-arena layout: frames at arbitrary offsets with gaps, the FCS written
+    at off + len, nothing else touched. "pinned" runs the in-place (zero-copy) path of
+    fcs_host_alloc memory up to 8 MiB; 12000 frames of up to 1514 B take the staged pipeline."""
+    rng = np.random.default_rng(40 + count)
+    ln = rng.integers(0, 1515, count).astype(np.uint32)
+    gap = rng.integers(4, 40, count).astype(np.uint64)       # room for the FCS plus slack
+    off = np.zeros(count, dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gap[:-1])
+    nbytes = int(off[-1] + ln[-1] + gap[-1])
+    data = rng.integers(0, 256, nbytes, dtype=np.uint8)
+    arena = na.host_buffer(nbytes) if where == "pinned" else np.empty(nbytes, dtype=np.uint8)
+    try:
+        arena[:] = data
+        na.tx_batch_host(arena, nbytes, off, ln, count)
+        want = data.copy()
+        for i in range(count):
+            o, L = int(off[i]), int(ln[i])
+            c = oracle.oracle_ether_fcs(data[o:o + L].ctypes.data, L) if L else 0
+            want[o + L:o + L + 4] = np.frombuffer(struct.pack("<I", c), dtype=np.uint8)
+        bad = np.flatnonzero(arena != want)
+        assert bad.size == 0, f"{bad.size} bytes differ, first at {bad[:8]}"
+    finally:
+        if where == "pinned":
+            na.host_free(arena)
+
+
+def test_tx_batch_host_rejects_fcs_past_arena(dev):
+    """The FCS of the last frame must fit inside arena_bytes (-EINVAL, nothing written)."""
+    arena = np.zeros(100, dtype=np.uint8)
+    with pytest.raises(na.FcsError):
+        na.tx_batch_host(arena, 100, np.array([40], dtype=np.uint64), np.array([57], dtype=np.uint32), 1)
+    assert not arena.any()
+
+
 def test_concurrent_callers(dev, oracle):
     """ether_fcs is called from 3-4 threads in the reference."""
     errs = []

@@ -12,6 +12,12 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
     std::this_thread::sleep_for(std::chrono::microseconds(20));
     return 0;
 }
+int ether_fcs_tx_batch_host(void *arena, uint64_t bytes, const uint64_t *off, const uint32_t *len, uint64_t n) {
+    (void)bytes;
+    for (uint64_t i = 0; i < n; i++) { uint32_t c = 0xA5A5A5A5u ^ len[i]; std::memcpy((uint8_t*)arena + off[i] + len[i], &c, 4); }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    return 0;
+}
 void *fcs_host_alloc(uint64_t b) { return std::malloc(b); }
 void fcs_host_free(void *p) { std::free(p); }
 }

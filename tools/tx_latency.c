@@ -19,14 +19,15 @@ static double now(void) {
 
 int main(void) {
     if (fcs_engine_init(1) < 0) return fprintf(stderr, "%s\n", fcs_last_error()), 1;
-    const int ns[] = {1, 16, 128, 1024, 4096};
+    const int ns[] = {1, 16, 128, 1024, 4096, 8192, 16384, 32768};
+    const int NMAX = 32768;
     const uint64_t stride = 1518;
-    uint8_t *pin = fcs_host_alloc(4096 * stride);
-    uint8_t *pag = malloc(4096 * stride);
-    uint32_t *len = malloc(4096 * 4);
-    for (int i = 0; i < 4096; i++) len[i] = 1514;
-    memset(pin, 7, 4096 * stride);
-    memset(pag, 7, 4096 * stride);
+    uint8_t *pin = fcs_host_alloc((uint64_t)NMAX * stride);
+    uint8_t *pag = malloc((uint64_t)NMAX * stride);
+    uint32_t *len = malloc((uint64_t)NMAX * 4);
+    for (int i = 0; i < NMAX; i++) len[i] = 1514;
+    memset(pin, 7, (uint64_t)NMAX * stride);
+    memset(pag, 7, (uint64_t)NMAX * stride);
     for (unsigned k = 0; k < sizeof ns / sizeof ns[0]; k++) {
         const int n = ns[k];
         const int reps = 200;
