@@ -358,7 +358,7 @@ def pcap_read(path: str):
     """Load a pcap into the batch layout: (arena u8, off u64, len u32, link type) as numpy arrays."""
     import numpy as np
     n, b, lt, _ = pcap_scan(path)
-    arena = np.zeros(max(b, 1), dtype=np.uint8)
+    arena = np.empty(max(b, 1), dtype=np.uint8)   # every byte of [0, b) is written by the read
     off = np.zeros(max(n, 1), dtype=np.uint64)
     ln = np.zeros(max(n, 1), dtype=np.uint32)
     got = _check(load().fcs_pcap_read(os.fsencode(path), arena.ctypes.data, arena.size, off.ctypes.data,

@@ -1,10 +1,18 @@
 // fcs_pcap.cpp — classic libpcap files <-> the engine's batch layout (include/nstack_pcap.h;
 // fixtures and captured traffic driving the GPU engine reproducibly).
 // Host code only: parsing and packing; no CRC is computed here.
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
 #include <cerrno>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <thread>
+#include <vector>
 
 #include "../../include/nstack_pcap.h"
 #include "fcs_error.hpp"
@@ -25,33 +33,71 @@ using File = std::unique_ptr<FILE, FileCloser>;
 
 inline uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// Opens `path`, validates the 24-byte global header; returns 0 or -errno.
-int open_pcap(const char *path, File *out, bool *swapped, uint32_t *linktype, uint32_t *snaplen) {
+// A pcap file mapped read-only, global header validated. Records are parsed straight from the
+// mapping: no per-record read or seek calls.
+struct Mapped {
+    const uint8_t *p = nullptr;
+    uint64_t size = 0;
+    bool swapped = false;
+    uint32_t linktype = 0;
+    ~Mapped() {
+        if (p && size) munmap((void *)p, size);
+    }
+    uint32_t u32(uint64_t at) const {
+        uint32_t v;
+        std::memcpy(&v, p + at, 4);
+        return swapped ? bswap32(v) : v;
+    }
+};
+
+int map_pcap(const char *path, Mapped *m) {
     if (!path) return fcs::set_error(EINVAL, "null path");
-    File f(std::fopen(path, "rb"));
-    if (!f) return fcs::set_error(errno ? errno : EIO, "%s: %s", path, std::strerror(errno));
-    uint32_t h[6];
-    if (std::fread(h, 4, 6, f.get()) != 6) return fcs::set_error(EINVAL, "%s: short pcap header", path);
-    const uint32_t m = h[0];
-    if (m == kMagicPcapng) return fcs::set_error(EPROTONOSUPPORT, "%s: pcapng is not supported", path);
-    if (m != kMagicUs && m != kMagicNs && m != kMagicUsSwapped && m != kMagicNsSwapped)
-        return fcs::set_error(EINVAL, "%s: not a pcap file (magic 0x%08X)", path, m);
-    *swapped = (m == kMagicUsSwapped || m == kMagicNsSwapped);
-    *snaplen = *swapped ? bswap32(h[4]) : h[4];
-    *linktype = *swapped ? bswap32(h[5]) : h[5];
-    *out = std::move(f);
+    const int fd = open(path, O_RDONLY | O_CLOEXEC);
+    if (fd < 0) return fcs::set_error(errno ? errno : EIO, "%s: %s", path, std::strerror(errno));
+    struct stat st;
+    if (fstat(fd, &st) != 0) {
+        const int e = errno;
+        close(fd);
+        return fcs::set_error(e ? e : EIO, "%s: %s", path, std::strerror(e));
+    }
+    m->size = (uint64_t)st.st_size;
+    if (m->size < 24) {
+        close(fd);
+        m->size = 0;
+        return fcs::set_error(EINVAL, "%s: short pcap header", path);
+    }
+    void *p = mmap(nullptr, m->size, PROT_READ, MAP_PRIVATE, fd, 0);
+    const int e = errno;
+    close(fd);
+    if (p == MAP_FAILED) {
+        m->size = 0;
+        return fcs::set_error(e ? e : EIO, "%s: mmap: %s", path, std::strerror(e));
+    }
+    m->p = (const uint8_t *)p;
+    madvise(p, m->size, MADV_SEQUENTIAL);
+    uint32_t magic;
+    std::memcpy(&magic, m->p, 4);
+    if (magic == kMagicPcapng) return fcs::set_error(EPROTONOSUPPORT, "%s: pcapng is not supported", path);
+    if (magic != kMagicUs && magic != kMagicNs && magic != kMagicUsSwapped && magic != kMagicNsSwapped)
+        return fcs::set_error(EINVAL, "%s: not a pcap file (magic 0x%08X)", path, magic);
+    m->swapped = (magic == kMagicUsSwapped || magic == kMagicNsSwapped);
+    m->linktype = m->u32(20);
     return 0;
 }
 
-// Reads the next 16-byte record header: 1 = got one, 0 = clean end of file, <0 = -errno.
-int next_record(FILE *f, bool swapped, const char *path, uint32_t *incl, uint32_t *orig) {
-    uint32_t r[4];
-    const size_t got = std::fread(r, 4, 4, f);
-    if (got == 0 && std::feof(f)) return 0;
-    if (got != 4) return fcs::set_error(EINVAL, "%s: truncated record header", path);
-    *incl = swapped ? bswap32(r[2]) : r[2];
-    *orig = swapped ? bswap32(r[3]) : r[3];
+// Record header at *pos: 1 = got one (*pos moves past header and data), 0 = clean end of file,
+// <0 = -errno.
+int next_record(const Mapped &m, const char *path, uint64_t n, uint64_t *pos, uint64_t *data, uint32_t *incl,
+                uint32_t *orig) {
+    if (*pos == m.size) return 0;
+    if (m.size - *pos < 16) return fcs::set_error(EINVAL, "%s: truncated record header", path);
+    *incl = m.u32(*pos + 8);
+    *orig = m.u32(*pos + 12);
     if (*incl > kMaxRecord) return fcs::set_error(EINVAL, "%s: record of %u bytes", path, *incl);
+    *data = *pos + 16;
+    if (*incl > m.size - *data)
+        return fcs::set_error(EINVAL, "%s: truncated record %llu", path, (unsigned long long)n);
+    *pos = *data + *incl;
     return 1;
 }
 
@@ -61,25 +107,23 @@ extern "C" {
 
 int fcs_pcap_scan(const char *path, uint64_t *frames, uint64_t *bytes, uint32_t *linktype,
                   uint64_t *truncated) {
-    File f;
-    bool sw = false;
-    uint32_t lt = 0, snap = 0;
-    int rc = open_pcap(path, &f, &sw, &lt, &snap);
+    Mapped m;
+    int rc = map_pcap(path, &m);
     if (rc) return rc;
-    uint64_t n = 0, b = 0, tr = 0;
+    uint64_t n = 0, b = 0, tr = 0, pos = 24;
     for (;;) {
+        uint64_t data = 0;
         uint32_t incl = 0, orig = 0;
-        rc = next_record(f.get(), sw, path, &incl, &orig);
+        rc = next_record(m, path, n, &pos, &data, &incl, &orig);
         if (rc < 0) return rc;
         if (rc == 0) break;
-        if (std::fseek(f.get(), incl, SEEK_CUR) != 0) return fcs::set_error(EIO, "%s: seek failed", path);
         n++;
         b += incl;
         tr += incl < orig;
     }
     if (frames) *frames = n;
     if (bytes) *bytes = b;
-    if (linktype) *linktype = lt;
+    if (linktype) *linktype = m.linktype;
     if (truncated) *truncated = tr;
     return 0;
 }
@@ -87,26 +131,48 @@ int fcs_pcap_scan(const char *path, uint64_t *frames, uint64_t *bytes, uint32_t 
 int64_t fcs_pcap_read(const char *path, uint8_t *arena, uint64_t arena_bytes, uint64_t *off,
                       uint32_t *len, uint64_t max_frames) {
     if (max_frames && (!arena || !off || !len)) return fcs::set_error(EINVAL, "null pointer");
-    File f;
-    bool sw = false;
-    uint32_t lt = 0, snap = 0;
-    int rc = open_pcap(path, &f, &sw, &lt, &snap);
+    Mapped m;
+    int rc = map_pcap(path, &m);
     if (rc) return rc;
-    uint64_t n = 0, pos = 0;
+    // pass 1: where every record's bytes are and where they go (packed in file order)
+    std::vector<uint64_t> src;
+    uint64_t n = 0, pos = 24, dst = 0;
     while (n < max_frames) {
+        uint64_t data = 0;
         uint32_t incl = 0, orig = 0;
-        rc = next_record(f.get(), sw, path, &incl, &orig);
+        rc = next_record(m, path, n, &pos, &data, &incl, &orig);
         if (rc < 0) return rc;
         if (rc == 0) break;
-        if (incl > arena_bytes - pos)
+        if (incl > arena_bytes - dst)
             return fcs::set_error(ENOSPC, "%s: record %llu (%u B) does not fit the %llu-byte arena", path,
                                   (unsigned long long)n, incl, (unsigned long long)arena_bytes);
-        if (incl && std::fread(arena + pos, 1, incl, f.get()) != incl)
-            return fcs::set_error(EINVAL, "%s: truncated record %llu", path, (unsigned long long)n);
-        off[n] = pos;
+        src.push_back(data);
+        off[n] = dst;
         len[n] = incl;
-        pos += incl;
+        dst += incl;
         n++;
+    }
+    // pass 2: copy, split by bytes over a few threads for large captures (one core copies far
+    // below the rate the GPU takes the batch at)
+    const uint64_t kPerThread = 64ull << 20;
+    const unsigned nth = (unsigned)std::min<uint64_t>(8, std::max<uint64_t>(1, dst / kPerThread));
+    auto copy = [&](uint64_t i0, uint64_t i1) {
+        for (uint64_t i = i0; i < i1; i++)
+            if (len[i]) std::memcpy(arena + off[i], m.p + src[i], len[i]);
+    };
+    if (nth == 1) {
+        copy(0, n);
+    } else {
+        std::vector<std::thread> th;
+        uint64_t i = 0;
+        for (unsigned t = 0; t < nth; t++) {
+            const uint64_t goal = dst * (t + 1) / nth;   // records until this many bytes are covered
+            uint64_t e = i;
+            while (e < n && (t + 1 == nth || off[e] < goal)) e++;
+            th.emplace_back(copy, i, e);
+            i = e;
+        }
+        for (auto &x : th) x.join();
     }
     return (int64_t)n;
 }
