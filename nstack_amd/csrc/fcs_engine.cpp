@@ -78,6 +78,7 @@ struct DevState {
     int dev = -1;
     int cus = 0;
     uint32_t *d_blob = nullptr;
+    uint32_t *d_one_blob = nullptr;   // tables of the single-frame kernel (drop-in ether_fcs)
     std::mutex pipe_mu;      // one host pipeline at a time per device
     Pipe pipe;
     std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
@@ -100,6 +101,7 @@ struct DevState {
     uint64_t *one_flag = nullptr, *one_dflag = nullptr;
     uint64_t one_seq = 0;
     uint64_t one_cap = 0;
+    uint32_t one_seq32 = 0;   // single-frame kernel: sequence number in the result word's high half
 };
 
 std::mutex g_mu;
@@ -134,6 +136,9 @@ int dev_state(int dev, DevState **out) {
         const std::vector<uint32_t> blob = tables().blob();
         hipError_t ae = hipMalloc(&st->d_blob, blob.size() * 4);
         if (ae == hipSuccess) ae = hipMemcpy(st->d_blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice);
+        const std::vector<uint32_t> one = tables().one_blob();
+        if (ae == hipSuccess) ae = hipMalloc(&st->d_one_blob, one.size() * 4);
+        if (ae == hipSuccess) ae = hipMemcpy(st->d_one_blob, one.data(), one.size() * 4, hipMemcpyHostToDevice);
         hipSetDevice(cur);
         if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
         g_dev[dev] = std::move(st);
@@ -735,6 +740,7 @@ void fcs_engine_fini(void) {
         if (ds->one_hout) hipHostFree(ds->one_hout);
         if (ds->one_flag) hipHostFree(ds->one_flag);
         if (ds->d_blob) hipFree(ds->d_blob);
+        if (ds->d_one_blob) hipFree(ds->d_one_blob);
     }
     g_dev.clear();
     g_engine_devs.clear();
@@ -915,7 +921,7 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
         if ((e = hipHostGetDevicePointer((void **)&ds->one_dout, ds->one_hout, 0)) != hipSuccess) die("map", e);
         if ((e = hipHostMalloc(&ds->one_flag, 64, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
         if ((e = hipHostGetDevicePointer((void **)&ds->one_dflag, ds->one_flag, 0)) != hipSuccess) die("map", e);
-        *ds->one_flag = 0;
+        ds->one_flag[0] = ds->one_flag[1] = 0;
     }
     if (bsize > ds->one_cap) {
         if (ds->one_h) hipHostFree(ds->one_h);
@@ -923,6 +929,41 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
         if ((e = hipHostMalloc(&ds->one_h, cap, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
         if ((e = hipHostGetDevicePointer((void **)&ds->one_hd, ds->one_h, 0)) != hipSuccess) die("map", e);
         ds->one_cap = cap - 64;
+    }
+    if (bsize <= fcs::kOneBytes) {   // every Ethernet frame: one launch carrying the frame itself
+        static const std::vector<uint32_t> kinit = [] {   // A_L(0xFFFFFFFF), L = 0 .. kOneBytes
+            std::vector<uint32_t> k(fcs::kOneBytes + 1);
+            k[0] = 0xFFFFFFFFu;
+            for (uint32_t L = 1; L <= fcs::kOneBytes; L++) k[L] = tables().zstep(k[L - 1]);
+            return k;
+        }();
+        fcs::OneArgs a;
+        a.flag = ds->one_dflag + 1;   // word 0 is the staged path's completion signal
+        a.blob = ds->d_one_blob;
+        if (++ds->one_seq32 == 0) ds->one_seq32 = 1;   // 0 never names a completion
+        a.seq = ds->one_seq32;
+        a.kinit = kinit[bsize];
+        uint8_t *win = reinterpret_cast<uint8_t *>(a.data);
+        std::memset(win, 0, fcs::kOneBytes - bsize);
+        std::memcpy(win + fcs::kOneBytes - bsize, data, bsize);
+        if ((e = fcs::launch_one(a, ds->one_stream)) != hipSuccess) die("launching the single-frame kernel", e);
+        const auto t0 = std::chrono::steady_clock::now();
+        for (uint32_t i = 1;; i++) {
+            const uint64_t v = __atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE);
+            if ((uint32_t)(v >> 32) == a.seq) {
+                hipSetDevice(cur);
+                return (uint32_t)v;
+            }
+            __builtin_ia32_pause();
+            if ((i & 4095) == 0) {
+                const hipError_t q = hipStreamQuery(ds->one_stream);
+                if (q == hipSuccess && (uint32_t)(__atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE) >> 32) != a.seq)
+                    die("single-frame kernel finished without a result", hipErrorUnknown);
+                if (q != hipSuccess && q != hipErrorNotReady) die("single-frame kernel", q);
+                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                    die("no result after 10 s", hipErrorUnknown);
+            }
+        }
     }
     std::memcpy(ds->one_h, data, bsize);
     rc = launch_fixed(ds, ds->one_hd, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);

@@ -1100,6 +1100,53 @@ __global__ void signal_kernel(uint64_t *flag, uint64_t v) {
     }
 }
 
+// Drop-in ether_fcs for one frame (fcs_launch.hpp OneArgs). The frame arrives in the kernel
+// arguments, right-aligned in a 1536-byte window with zeros in front: from a zero register,
+// leading zeros change nothing, and the all-ones start of the real CRC is added back as
+// kinit = A_len(0xFFFFFFFF) (the register update is affine: R(s, M) = A_len(s) ^ R(0, M)).
+// Lane j runs six slice-by-4 steps over window bytes [24j, 24j + 24) from a zero register; a
+// six-level tree then joins neighbouring lane groups, the earlier one advanced by A_{24 * 2^k}.
+// Lane 0 stores (seq << 32) | FCS into a mapped host word with one system-scope store, which
+// is also the completion signal the host spins on: no staging copy, no second launch.
+__device__ __forceinline__ uint32_t one_step(const uint32_t *t, uint32_t x, uint32_t wn) {
+    return xor3(xor3(t[768 + (x & 0xFFu)], t[512 + ((x >> 8) & 0xFFu)], t[256 + ((x >> 16) & 0xFFu)]),
+                t[x >> 24], wn);
+}
+
+__global__ __launch_bounds__(64) void fcs_one_kernel(OneArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t t[kOneBlobWords];
+    const int lane = threadIdx.x;
+    for (int i = lane; i < (int)kOneBlobWords / 4; i += 64)
+        reinterpret_cast<u32x4a4 *>(t)[i] = reinterpret_cast<const u32x4a4 *>(a.blob)[i];
+    // the window words straight from the kernel-argument segment (no private copy of `a`)
+    typedef const __attribute__((address_space(4))) uint32_t karg_u32;
+    karg_u32 *dw = reinterpret_cast<karg_u32 *>(
+        (const __attribute__((address_space(4))) uint8_t *)__builtin_amdgcn_kernarg_segment_ptr() +
+        offsetof(OneArgs, data));
+    uint32_t w[6];
+#pragma unroll
+    for (int q = 0; q < 6; q++) w[q] = dw[lane * 6 + q];
+    __syncthreads();
+    uint32_t x = w[0];
+#pragma unroll
+    for (int i = 0; i < 6; i++) x = one_step(t, x, i < 5 ? w[i + 1] : 0u);
+#pragma unroll
+    for (int k = 0; k < 6; k++) {
+        const uint32_t *nt = t + 1024 + k * 128;
+        uint32_t y = x;
+        if (!(lane & (1 << k))) {   // the earlier group: advance it past the later one's bytes
+            uint32_t r[8];
+#pragma unroll
+            for (int q = 0; q < 8; q++) r[q] = nt[q * 16 + ((x >> (4 * q)) & 15u)];
+            y = xor9(r, 0u);
+        }
+        x = y ^ (uint32_t)__shfl_xor((int)y, 1 << k);
+    }
+    if (lane == 0)
+        __hip_atomic_store(a.flag, ((uint64_t)a.seq << 32) | (uint64_t)(uint32_t)~(x ^ a.kinit), __ATOMIC_RELEASE,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // TX mode helper: after the FCS kernel wrote crc[i], store it little-endian after each frame.
 __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t stride,
                                                        const uint32_t *len, const uint32_t *crc,
@@ -1175,6 +1222,11 @@ hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hip
 
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st) {
     hipLaunchKernelGGL(read_stream_kernel, dim3(8192), dim3(256), 0, st, (const u32x4 *)p, bytes / 16, sink);
+    return hipGetLastError();
+}
+
+hipError_t launch_one(const OneArgs &a, hipStream_t st) {
+    hipLaunchKernelGGL(fcs_one_kernel, dim3(1), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

@@ -24,9 +24,24 @@ struct KParams {
 
 constexpr int kWgThreads = 1024;
 
+// Single-frame kernel of the drop-in ether_fcs (fcs_one_kernel): the frame travels inside the
+// kernel arguments, right-aligned in a 1536-byte window (zeros before it), one wave of 64 lanes
+// takes 24 bytes each. Tables: the four slice-by-4 tables, then nibble tables of A_{24 * 2^k},
+// k = 0..5, for the lane tree (kOneBlobWords words).
+constexpr uint32_t kOneBytes = 1536;
+constexpr uint32_t kOneBlobWords = 1024 + 6 * 128;
+struct OneArgs {
+    uint64_t *flag;          // device address of a mapped host word: (seq << 32) | FCS
+    const uint32_t *blob;    // kOneBlobWords
+    uint32_t seq;
+    uint32_t kinit;          // A_len(0xFFFFFFFF): the all-ones start carried over the frame
+    uint32_t data[kOneBytes / 4];
+};
+
 
 hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st);
 hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st);
+hipError_t launch_one(const OneArgs &a, hipStream_t st);
 hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hipStream_t st);
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st);
 hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,

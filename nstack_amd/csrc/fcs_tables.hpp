@@ -138,6 +138,18 @@ struct Tables {
         }
         return b;
     }
+    // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.
+    std::vector<uint32_t> one_blob() const {
+        std::vector<uint32_t> b(1024 + 6 * 128, 0u);
+        for (int k = 0; k < 4; k++) std::memcpy(&b[256 * k], T[k], 1024);
+        uint32_t nt[8][16];
+        for (int k = 0; k < 6; k++) {
+            nibble_table(24L << k, nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[1024 + k * 128 + t * 16 + e] = nt[t][e];
+        }
+        return b;
+    }
 };
 
 }  // namespace fcs

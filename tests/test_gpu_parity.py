@@ -99,6 +99,25 @@ def test_dropin_ether_fcs(dev, golden):
         assert na.ether_fcs(arena[f["off"]:f["off"] + f["len"]]) == f["crc"]
 
 
+def test_dropin_every_length(dev, golden):
+    """The drop-in takes frames of up to 1536 B through the single-frame kernel (the frame rides in
+    the kernel arguments) and longer ones through the staged path: every length 0..1600 from
+    several source alignments, the golden known answers, and the residue of a frame with its
+    own FCS appended, all against zlib (= the reference ether_fcs)."""
+    rng = np.random.default_rng(77)
+    buf = rng.integers(0, 256, 1700, dtype=np.uint8).tobytes()
+    for L in range(0, 1601):
+        a = (L * 7) % 13
+        b = buf[a:a + L]
+        assert na.ether_fcs(b) == zlib.crc32(b), L
+    for case in golden["kat"]["cases"]:
+        b = bytes.fromhex(case["hex"]) if case["hex"] is not None else bytes([case["fill"]]) * case["len"]
+        assert na.ether_fcs(b) == case["crc"], case["name"]
+    for L in (60, 1514, 1532):
+        f = buf[:L]
+        assert na.ether_fcs(f + struct.pack("<I", zlib.crc32(f))) == 0x2144DF1C
+
+
 # ---------------------------------------------------------------- edge lengths / alignment
 EDGE = [0, 1, 3, 4, 59, 60, 61, 63, 64, 65, 69, 70, 71, 575, 576, 577, 1487, 1488, 1489,
         1513, 1514, 1515, 1516, 1517, 1518, 1535, 1536, 1537, 3071, 3072, 3073, 8999, 9000]
