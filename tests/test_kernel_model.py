@@ -5,6 +5,8 @@ addressing, front-lane init/masking, segment jumps and lane shifts — without a
 import random
 import zlib
 
+import numpy as np
+
 import pytest
 
 import kernel_model as km  # noqa: E402
@@ -64,3 +66,52 @@ def test_flat_kernel_chunk_shift_tables():
             for t in range(8):
                 v ^= int(blob[flat + c * 136 + t * 16 + ((s >> (4 * t)) & 15)])
             assert v == _shift(s, 96 * c), (c, hex(s))
+
+
+def test_single_frame_kernel_decomposition():
+    """fcs_one_kernel (drop-in ether_fcs, frames <= 1536 B): the frame right-aligned in a 1536-B
+    window with zeros in front, 64 lanes x 24 B from a zero register, a six-level lane tree with
+    A_{24*2^k}, and the all-ones start added back as A_len(0xFFFFFFFF). Replayed here with tables
+    built from the polynomial alone, against zlib (= the reference ether_fcs)."""
+    import zlib
+    poly = 0xEDB88320
+    t0 = []
+    for b in range(256):
+        r = b
+        for _ in range(8):
+            r = (r >> 1) ^ (poly if r & 1 else 0)
+        t0.append(r)
+    T = [t0]
+    for k in range(1, 4):
+        T.append([(T[k - 1][b] >> 8) ^ t0[T[k - 1][b] & 0xFF] for b in range(256)])
+
+    def zshift(s, n):
+        for _ in range(n):
+            s = (s >> 8) ^ t0[s & 0xFF]
+        return s
+
+    nib = [[[zshift(e << (4 * t), 24 << k) for e in range(16)] for t in range(8)] for k in range(6)]
+
+    def a_shift(k, x):
+        v = 0
+        for t in range(8):
+            v ^= nib[k][t][(x >> (4 * t)) & 15]
+        return v
+
+    rng = np.random.default_rng(3)
+    for L in (0, 1, 5, 60, 64, 333, 1514, 1518, 1535, 1536):
+        frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+        win = np.frombuffer(bytes(1536 - L) + frame, dtype="<u4")
+        x = []
+        for j in range(64):
+            w = [int(v) for v in win[6 * j:6 * j + 6]]
+            s = w[0]
+            for i in range(6):
+                s = T[3][s & 0xFF] ^ T[2][(s >> 8) & 0xFF] ^ T[1][(s >> 16) & 0xFF] ^ T[0][s >> 24] ^ (w[i + 1] if i < 5 else 0)
+            x.append(s)
+        for k in range(6):
+            d = 1 << k
+            y = [x[j] if j & d else a_shift(k, x[j]) for j in range(64)]
+            x = [y[j] ^ y[j ^ d] for j in range(64)]
+        got = ~(x[0] ^ zshift(0xFFFFFFFF, L)) & 0xFFFFFFFF
+        assert got == zlib.crc32(frame), L
