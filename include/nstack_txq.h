@@ -61,6 +61,9 @@ void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint
  * sum plus bookkeeping), and pickup (a batch's first frame queued -> the flusher closing it). */
 void fcs_txq_timing(const fcs_txq_t *q, uint64_t *ns_ready, uint64_t *ns_gpu, uint64_t *ns_sink,
                     uint64_t *ns_busy, uint64_t *ns_pickup);
+/* Text of the most recent failed GPU step (fcs_last_error() of the flusher thread when its
+ * ether_fcs_tx_batch_host call failed); "" when no batch has failed. Valid until the next call. */
+const char *fcs_txq_last_error(const fcs_txq_t *q);
 
 /* ---- provided sinks ---- */
 /* ctx = pointer to an int file descriptor of a CONNECTED socket (e.g. a socketpair or a

@@ -28,7 +28,7 @@ EXPORTS = [
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
     "fcs_tables_blob",
     # include/nstack_txq.h — batched TX call site
-    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing",
+    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
@@ -94,6 +94,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_txq_send_async": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
         "fcs_txq_stats": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
         "fcs_txq_timing": (None, [vp] + [c.POINTER(u64)] * 5),
+        "fcs_txq_last_error": (c.c_char_p, [vp]),
         "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
         "fcs_txq_sink_packet": (None, [vp, vp, vp, vp, u32]),
         "fcs_pcap_scan": (i32, [c.c_char_p, c.POINTER(u64), c.POINTER(u64), c.POINTER(u32), c.POINTER(u64)]),

@@ -88,6 +88,8 @@ struct DevState {
     uint64_t *tx_off = nullptr, *tx_doff = nullptr;  // frame offsets (ether_fcs_tx_batch_host)
     uint64_t *tx_flag = nullptr, *tx_dflag = nullptr; // completion word (signal_kernel), mapped
     uint64_t tx_seq = 0;
+    unsigned long long *tx_dcount = nullptr;        // small-batch kernel: frames done (device memory)
+    uint64_t tx_count = 0;                           //   ... its value once every launch so far is done
     uint64_t *vz_off = nullptr, *vz_doff = nullptr;  // small RX verify batches (same stream and lock):
     uint32_t *vz_len = nullptr, *vz_dlen = nullptr;  //   offsets, lengths, ok flags and the bad count,
     uint8_t *vz_ok = nullptr, *vz_dok = nullptr;     //   pinned and device-mapped; the kernel's bad
@@ -110,6 +112,18 @@ std::vector<int> g_engine_devs;                  // devices used by the host bat
 const fcs::Tables &tables() {
     static const fcs::Tables t;
     return t;
+}
+
+// A_L(0xFFFFFFFF) for L = 0 .. kOneBytes: the all-ones CRC start carried over L bytes (the
+// single-frame kernels start from a zero register and add this back).
+const std::vector<uint32_t> &kinit_table() {
+    static const std::vector<uint32_t> k = [] {
+        std::vector<uint32_t> v(fcs::kOneBytes + 1);
+        v[0] = 0xFFFFFFFFu;
+        for (uint32_t L = 1; L <= fcs::kOneBytes; L++) v[L] = tables().zstep(v[L - 1]);
+        return v;
+    }();
+    return k;
 }
 
 int dev_state(int dev, DevState **out) {
@@ -481,9 +495,9 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
         *ds->tx_flag = 0;
     }
     if (n > ds->tx_cap) {
-        if (ds->tx_len) hipHostFree(ds->tx_len);
-        if (ds->tx_out) hipHostFree(ds->tx_out);
-        if (ds->tx_off) hipHostFree(ds->tx_off);
+        if (ds->tx_len) HIPTRY(hipHostFree(ds->tx_len), "hipHostFree(tx len)");
+        if (ds->tx_out) HIPTRY(hipHostFree(ds->tx_out), "hipHostFree(tx out)");
+        if (ds->tx_off) HIPTRY(hipHostFree(ds->tx_off), "hipHostFree(tx off)");
         ds->tx_len = ds->tx_out = nullptr;
         ds->tx_off = nullptr;
         ds->tx_cap = 0;
@@ -496,13 +510,40 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
         HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_doff, ds->tx_off, 0), "hipHostGetDevicePointer(off)");
         ds->tx_cap = cap;
     }
-    std::memcpy(ds->tx_len, len, n * 4);
-    if (off) std::memcpy(ds->tx_off, off, n * 8);
     void *dbase = pinned_dev_ptr(base, bytes);   // our own arenas: no HIP query
     if (!dbase && hipHostGetDevicePointer(&dbase, base, 0) != hipSuccess) {   // pinned but not mapped
         (void)hipGetLastError();
         return 1;
     }
+    bool small = n <= fcs::kTxSmallMax;
+    for (uint64_t i = 0; small && i < n; i++) small = len[i] <= fcs::kOneBytes;
+    if (small && !ds->tx_dcount) {
+        HIPTRY(hipMalloc(&ds->tx_dcount, 64), "hipMalloc(small TX counter)");
+        HIPTRY(hipMemset(ds->tx_dcount, 0, 64), "hipMemset(small TX counter)");
+        ds->tx_count = 0;
+    }
+    if (small) {   // everything the kernel needs rides in its arguments; it writes the FCSs itself
+        const std::vector<uint32_t> &kinit = kinit_table();
+        fcs::TxSmallArgs a;
+        a.flag = ds->tx_dflag;
+        a.count = ds->tx_dcount;
+        a.count_base = ds->tx_count;
+        a.blob = ds->d_one_blob;
+        a.base = (uint8_t *)dbase;
+        a.seq = ++ds->tx_seq;
+        a.n = (uint32_t)n;
+        a.pad = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            a.off[i] = off ? off[i] : i * stride;
+            a.len[i] = len[i];
+            a.kinit[i] = kinit[len[i]];
+        }
+        HIPTRY(fcs::launch_tx_small(a, ds->tx_stream), "launching the small TX kernel");
+        ds->tx_count += n;
+        return wait_flag(ds->tx_stream, ds->tx_flag, a.seq, "small TX batch");
+    }
+    std::memcpy(ds->tx_len, len, n * 4);
+    if (off) std::memcpy(ds->tx_off, off, n * 8);
     int rc = launch_var(ds, dbase, bytes, off ? ds->tx_doff : nullptr, ds->tx_dlen, ds->tx_dout, n, ds->tx_stream,
                         nullptr, nullptr, off ? 0 : stride);
     if (rc) return rc;
@@ -511,6 +552,54 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
     if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small TX batch"))) return rc;
     for (uint64_t i = 0; i < n; i++) std::memcpy(base + (off ? off[i] : i * stride) + len[i], &ds->tx_out[i], 4);
     return 0;
+}
+
+// One frame of at most kOneBytes through fcs_one_kernel: the frame rides in the kernel arguments
+// and the FCS comes back in the high-sequenced mapped word (one_flag[1]). Any host memory.
+int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
+    std::lock_guard<std::mutex> lk(ds->one_mu);
+    int cur = 0;
+    HIPTRY(hipGetDevice(&cur), "hipGetDevice");
+    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    struct Restore {
+        int d;
+        ~Restore() { hipSetDevice(d); }
+    } restore{cur};
+    if (!ds->one_stream) {
+        HIPTRY(hipStreamCreateWithFlags(&ds->one_stream, hipStreamNonBlocking), "hipStreamCreate");
+        HIPTRY(hipHostMalloc(&ds->one_hout, 64, hipHostMallocMapped), "hipHostMalloc(result)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->one_dout, ds->one_hout, 0), "hipHostGetDevicePointer(result)");
+        HIPTRY(hipHostMalloc(&ds->one_flag, 64, hipHostMallocMapped), "hipHostMalloc(flag)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->one_dflag, ds->one_flag, 0), "hipHostGetDevicePointer(flag)");
+        ds->one_flag[0] = ds->one_flag[1] = 0;
+    }
+    fcs::OneArgs a;
+    a.flag = ds->one_dflag + 1;   // word 0 is the staged path's completion signal
+    a.blob = ds->d_one_blob;
+    if (++ds->one_seq32 == 0) ds->one_seq32 = 1;   // 0 never names a completion
+    a.seq = ds->one_seq32;
+    a.kinit = kinit_table()[bsize];
+    uint8_t *win = reinterpret_cast<uint8_t *>(a.data);
+    std::memset(win, 0, fcs::kOneBytes - bsize);
+    if (bsize) std::memcpy(win + fcs::kOneBytes - bsize, data, bsize);
+    HIPTRY(fcs::launch_one(a, ds->one_stream), "launching the single-frame kernel");
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 1;; i++) {
+        const uint64_t v = __atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE);
+        if ((uint32_t)(v >> 32) == a.seq) {
+            *crc = (uint32_t)v;
+            return 0;
+        }
+        __builtin_ia32_pause();
+        if ((i & 4095) == 0) {
+            const hipError_t q = hipStreamQuery(ds->one_stream);
+            if (q == hipSuccess && (uint32_t)(__atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE) >> 32) != a.seq)
+                return fail(EIO, "single-frame kernel finished without a result");
+            if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "single-frame kernel");
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+                return fail(ETIMEDOUT, "single-frame kernel: no result after 10 s");
+        }
+    }
 }
 
 // Small RX verify batches in fcs_host_alloc memory (the RX queue's arena): the kernel reads the
@@ -582,6 +671,19 @@ int engine_devices(std::vector<DevState *> *out) {
     }
     return 0;
 }
+
+// A TX batch of one frame (a sync ether_send caller on its own): the single-frame kernel, from any
+// host memory, and the FCS stored here (src/linux/ether.c:263).
+int tx_one(uint8_t *frame, uint32_t len) {
+    std::vector<DevState *> devs;
+    int rc = engine_devices(&devs);
+    if (rc) return rc;
+    uint32_t c = 0;
+    if ((rc = run_one(devs[0], frame, len, &c))) return rc;
+    std::memcpy(frame + len, &c, 4);
+    return 0;
+}
+
 
 // Shard [0, n) over the engine devices (contiguous ranges, byte-balanced when lengths are known).
 int run_host_sharded(HostJob job, uint64_t n) {
@@ -730,7 +832,9 @@ void fcs_engine_fini(void) {
         if (ds->tx_stream) hipStreamDestroy(ds->tx_stream);
         if (ds->tx_len) hipHostFree(ds->tx_len);
         if (ds->tx_out) hipHostFree(ds->tx_out);
+        if (ds->tx_off) hipHostFree(ds->tx_off);
         if (ds->tx_flag) hipHostFree(ds->tx_flag);
+        if (ds->tx_dcount) hipFree(ds->tx_dcount);
         if (ds->vz_off) hipHostFree(ds->vz_off);
         if (ds->vz_len) hipHostFree(ds->vz_len);
         if (ds->vz_ok) hipHostFree(ds->vz_ok);
@@ -809,6 +913,7 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
         if ((uint64_t)len[i] + 4 > stride)
             return fail(EINVAL, "frame %llu: len %u + FCS does not fit stride %llu", (unsigned long long)i,
                         len[i], (unsigned long long)stride);
+    if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)base, len[0]);
     if (n * stride <= kZeroCopyMaxBytes && (pinned_dev_ptr(base, n * stride) || is_pinned(base))) {
         std::vector<DevState *> devs;
         int rc = engine_devices(&devs);
@@ -829,6 +934,7 @@ int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *o
         if (off[i] > arena_bytes || (uint64_t)len[i] + 4 > arena_bytes - off[i])
             return fail(EINVAL, "frame %llu [%llu, +%u) and its FCS outside the %llu-byte arena",
                         (unsigned long long)i, (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)arena + off[0], len[0]);
     if (arena_bytes <= kZeroCopyMaxBytes && (pinned_dev_ptr(arena, arena_bytes) || is_pinned(arena))) {
         std::vector<DevState *> devs;
         int rc = engine_devices(&devs);
@@ -905,6 +1011,14 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
         std::fprintf(stderr, "nstack_fcs: ether_fcs: no usable GPU engine: %s\n", g_last_error.c_str());
         std::abort();
     }
+    if (bsize <= fcs::kOneBytes) {   // every Ethernet frame: one launch carrying the frame itself
+        uint32_t c = 0;
+        if ((rc = run_one(ds, data, bsize, &c))) {
+            std::fprintf(stderr, "nstack_fcs: ether_fcs: %s\n", g_last_error.c_str());
+            std::abort();
+        }
+        return c;
+    }
     dev = ds->dev;
     std::lock_guard<std::mutex> lk(ds->one_mu);
     auto die = [](const char *what, hipError_t e) {
@@ -929,41 +1043,6 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
         if ((e = hipHostMalloc(&ds->one_h, cap, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
         if ((e = hipHostGetDevicePointer((void **)&ds->one_hd, ds->one_h, 0)) != hipSuccess) die("map", e);
         ds->one_cap = cap - 64;
-    }
-    if (bsize <= fcs::kOneBytes) {   // every Ethernet frame: one launch carrying the frame itself
-        static const std::vector<uint32_t> kinit = [] {   // A_L(0xFFFFFFFF), L = 0 .. kOneBytes
-            std::vector<uint32_t> k(fcs::kOneBytes + 1);
-            k[0] = 0xFFFFFFFFu;
-            for (uint32_t L = 1; L <= fcs::kOneBytes; L++) k[L] = tables().zstep(k[L - 1]);
-            return k;
-        }();
-        fcs::OneArgs a;
-        a.flag = ds->one_dflag + 1;   // word 0 is the staged path's completion signal
-        a.blob = ds->d_one_blob;
-        if (++ds->one_seq32 == 0) ds->one_seq32 = 1;   // 0 never names a completion
-        a.seq = ds->one_seq32;
-        a.kinit = kinit[bsize];
-        uint8_t *win = reinterpret_cast<uint8_t *>(a.data);
-        std::memset(win, 0, fcs::kOneBytes - bsize);
-        std::memcpy(win + fcs::kOneBytes - bsize, data, bsize);
-        if ((e = fcs::launch_one(a, ds->one_stream)) != hipSuccess) die("launching the single-frame kernel", e);
-        const auto t0 = std::chrono::steady_clock::now();
-        for (uint32_t i = 1;; i++) {
-            const uint64_t v = __atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE);
-            if ((uint32_t)(v >> 32) == a.seq) {
-                hipSetDevice(cur);
-                return (uint32_t)v;
-            }
-            __builtin_ia32_pause();
-            if ((i & 4095) == 0) {
-                const hipError_t q = hipStreamQuery(ds->one_stream);
-                if (q == hipSuccess && (uint32_t)(__atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE) >> 32) != a.seq)
-                    die("single-frame kernel finished without a result", hipErrorUnknown);
-                if (q != hipSuccess && q != hipErrorNotReady) die("single-frame kernel", q);
-                if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
-                    die("no result after 10 s", hipErrorUnknown);
-            }
-        }
     }
     std::memcpy(ds->one_h, data, bsize);
     rc = launch_fixed(ds, ds->one_hd, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);

@@ -22,6 +22,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -119,6 +120,7 @@ struct fcs_txq {
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
     uint64_t ns_ready = 0, ns_gpu = 0, ns_sink = 0, ns_busy = 0;   // flusher time split
     uint64_t ns_pickup = 0;               // first frame of a batch queued -> batch closed
+    std::string last_error;               // fcs_last_error() of the latest failed GPU step
     std::thread th;
 };
 
@@ -258,6 +260,9 @@ void flusher(fcs_txq *q) {
             q->sink(q->ctx, B->frames.data(), B->sizes.data(), B->res.data(), n);
         } else {
             for (uint32_t i = 0; i < n; i++) B->res[i] = rc;   // nothing leaves unchecked
+            const char *why = fcs_last_error();
+            std::lock_guard<std::mutex> lk(q->mu);
+            q->last_error = why ? why : "";
         }
         const auto t3 = Clock::now();
 
@@ -469,6 +474,15 @@ void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint
     if (frames) *frames = m->n_frames;
     if (batches) *batches = m->n_batches;
     if (errors) *errors = m->n_errors;
+}
+
+const char *fcs_txq_last_error(const fcs_txq_t *q) {
+    if (!q) return "";
+    fcs_txq *m = const_cast<fcs_txq *>(q);
+    static thread_local std::string copy;
+    std::lock_guard<std::mutex> lk(m->mu);
+    copy = m->last_error;
+    return copy.c_str();
 }
 
 void fcs_txq_timing(const fcs_txq_t *q, uint64_t *ns_ready, uint64_t *ns_gpu, uint64_t *ns_sink,

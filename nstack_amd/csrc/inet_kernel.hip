@@ -287,6 +287,7 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
 }
 
 hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, hipStream_t st) {
+    (void)hipGetLastError();   // report this launch's own error, not an earlier call's
     if (p.n > flat_min) {
         const uint64_t windows = (p.n + 63) / 64, per_block = kThreads / 64;
         const uint64_t want = (windows + per_block - 1) / per_block, cap = (uint64_t)cus * 8;

@@ -290,14 +290,20 @@ def test_tx_mode_matches_ether_send_layout(dev, var_kernel, oracle):
         assert oracle.oracle_ether_fcs(frames[i].ctypes.data, fs) == 0x2144DF1C
 
 
-@pytest.mark.parametrize("where,count", [("pageable", 3000), ("pinned", 3000), ("pageable", 12000)])
-def test_tx_batch_host_offsets(dev, oracle, where, count):
+@pytest.mark.parametrize("where,count,maxlen", [("pageable", 3000, 1514), ("pinned", 3000, 1514),
+                                               ("pageable", 12000, 1514), ("pinned", 1, 1514), ("pageable", 1, 1536),
+                                               ("pinned", 17, 1536), ("pinned", 64, 1536),
+                                               ("pinned", 64, 2000), ("pinned", 65, 1536)])
+def test_tx_batch_host_offsets(dev, oracle, where, count, maxlen):
     """ether_fcs_tx_batch_host: ether_send's FCS placement (src/linux/ether.c:262-263) over the
-    packed-arena layout: frames at arbitrary offsets with gaps, the FCS written
-    at off + len, nothing else touched. "pinned" runs the in-place (zero-copy) path of
-    fcs_host_alloc memory up to 8 MiB; 12000 frames of up to 1514 B take the staged pipeline."""
-    rng = np.random.default_rng(40 + count)
-    ln = rng.integers(0, 1515, count).astype(np.uint32)
+    packed-arena layout: frames at arbitrary offsets with gaps, the first at the
+    arena's first byte, the FCS written at off + len, nothing else touched. "pinned" runs the
+    in-place paths of fcs_host_alloc memory: up to 64 frames of up to 1536 B in the small-batch
+    kernel (frame list in its arguments), more frames or longer ones through the mapped-memory
+    batch kernel; pageable memory takes the staged pipeline."""
+    rng = np.random.default_rng(40 + count + maxlen)
+    ln = rng.integers(0, maxlen + 1, count).astype(np.uint32)
+    ln[:min(count, 3)] = [maxlen, 0, 1][:min(count, 3)]
     gap = rng.integers(4, 40, count).astype(np.uint64)       # room for the FCS plus slack
     off = np.zeros(count, dtype=np.uint64)
     off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + gap[:-1])
@@ -317,6 +323,28 @@ def test_tx_batch_host_offsets(dev, oracle, where, count):
     finally:
         if where == "pinned":
             na.host_free(arena)
+
+
+def test_tx_in_place_buffers_grow(dev):
+    """The in-place TX path keeps mapped length/offset/result arrays sized to the largest batch
+    so far; batches that outgrow them (4097 and 9000 frames after 100) must reallocate cleanly,
+    with offsets and with a stride, and the next batch must still run."""
+    for n in (100, 4097, 9000, 9000, 20):
+        a = na.host_buffer(n * 1536)
+        try:
+            data = np.random.default_rng(n).integers(0, 256, n * 1536, dtype=np.uint8)
+            a[:] = data
+            ln = np.full(n, 1514, dtype=np.uint32)
+            na.tx_batch_host(a, n * 1536, np.arange(n, dtype=np.uint64) * 1536, ln, n)
+            for i in (0, n // 2, n - 1):
+                f = data[i * 1536:i * 1536 + 1514].tobytes()
+                assert a[i * 1536 + 1514:i * 1536 + 1518].tobytes() == struct.pack("<I", zlib.crc32(f)), (n, i)
+            a[:] = data
+            na.tx_host(a, 1536, ln, n)
+            assert a[(n - 1) * 1536 + 1514:(n - 1) * 1536 + 1518].tobytes() == \
+                struct.pack("<I", zlib.crc32(data[(n - 1) * 1536:(n - 1) * 1536 + 1514].tobytes()))
+        finally:
+            na.host_free(a)
 
 
 def test_tx_batch_host_rejects_fcs_past_arena(dev):

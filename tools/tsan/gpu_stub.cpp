@@ -18,6 +18,7 @@ int ether_fcs_tx_batch_host(void *arena, uint64_t bytes, const uint64_t *off, co
     std::this_thread::sleep_for(std::chrono::microseconds(20));
     return 0;
 }
+const char *fcs_last_error(void) { return "stub"; }
 void *fcs_host_alloc(uint64_t b) { return std::malloc(b); }
 void fcs_host_free(void *p) { std::free(p); }
 }

@@ -155,6 +155,7 @@ int main(int argc, char **argv) {
            (unsigned long long)errors, batches ? nr / 1e3 / batches : 0.0, batches ? ng / 1e3 / batches : 0.0,
            batches ? ns / 1e3 / batches : 0.0, batches ? nb / 1e3 / batches : 0.0, batches ? np_ / 1e3 / batches : 0.0,
            batches ? dt * 1e6 / batches : 0.0);
+    if (Q && errors) fprintf(stderr, "txq: %llu frames failed: %s\n", (unsigned long long)errors, fcs_txq_last_error(Q));
     if (Q) fcs_txq_destroy(Q);
     return (atomic_load(&bad_results) || errors) ? 2 : 0;
 }
