@@ -79,6 +79,7 @@ struct DevState {
     int cus = 0;
     uint32_t *d_blob = nullptr;
     uint32_t *d_one_blob = nullptr;   // tables of the single-frame kernel (drop-in ether_fcs)
+    uint32_t *d_kinit = nullptr;      // kinit_table() in device memory (mapped-list kernel)
     std::mutex pipe_mu;      // one host pipeline at a time per device
     Pipe pipe;
     std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
@@ -153,6 +154,9 @@ int dev_state(int dev, DevState **out) {
         const std::vector<uint32_t> one = tables().one_blob();
         if (ae == hipSuccess) ae = hipMalloc(&st->d_one_blob, one.size() * 4);
         if (ae == hipSuccess) ae = hipMemcpy(st->d_one_blob, one.data(), one.size() * 4, hipMemcpyHostToDevice);
+        const std::vector<uint32_t> &ki = kinit_table();
+        if (ae == hipSuccess) ae = hipMalloc(&st->d_kinit, ki.size() * 4);
+        if (ae == hipSuccess) ae = hipMemcpy(st->d_kinit, ki.data(), ki.size() * 4, hipMemcpyHostToDevice);
         hipSetDevice(cur);
         if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
         g_dev[dev] = std::move(st);
@@ -312,15 +316,17 @@ uint8_t *pinned_dev_ptr(const void *p, uint64_t bytes) {
 // mapped completion word: the host spins on that word (a stream synchronisation costs ~3 us more
 // per round trip, tools/microbench/launch_lat.hip). Errors and stalls are still caught by
 // polling the stream now and then.
+// Completion words only grow: every launch that stores one is numbered under its stream's lock
+// in stream order, so a later launch may already have overwritten `v` with a larger value.
 int wait_flag(hipStream_t st, const uint64_t *flag, uint64_t v, const char *what) {
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1;; i++) {
-        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+        if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) >= v) return 0;
         __builtin_ia32_pause();
         if ((i & 4095) == 0) {
             const hipError_t q = hipStreamQuery(st);
             if (q == hipSuccess) {
-                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) == v) return 0;
+                if (__atomic_load_n(flag, __ATOMIC_ACQUIRE) >= v) return 0;
                 return fail(EIO, "%s: stream idle but no completion signal", what);
             }
             if (q != hipErrorNotReady) return hip_fail(q, what);
@@ -484,6 +490,24 @@ int run_host_job(DevState *ds, const HostJob &job) {
 #endif
 constexpr uint64_t kZeroCopyMaxBytes = (uint64_t)FCS_ZC_MAX_MB << 20;
 
+// Small-batch resources on the TX/verify stream (caller holds tx_mu).
+int ensure_small(DevState *ds) {
+    if (!ds->tx_stream) {
+        HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
+        HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dflag, ds->tx_flag, 0), "hipHostGetDevicePointer(flag)");
+        *ds->tx_flag = 0;
+    }
+    if (!ds->tx_dcount) {
+        HIPTRY(hipMalloc(&ds->tx_dcount, 64), "hipMalloc(small batch counter)");
+        HIPTRY(hipMemset(ds->tx_dcount, 0, 64), "hipMemset(small batch counter)");
+        HIPTRY(hipDeviceSynchronize(), "hipDeviceSynchronize");   // zeroed before any launch on tx_stream
+        ds->tx_count = 0;
+    }
+    return 0;
+}
+
+
 int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t stride, const uint64_t *off,
                      const uint32_t *len, uint64_t n) {
     std::lock_guard<std::mutex> lk(ds->tx_mu);
@@ -517,15 +541,15 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
     }
     bool small = n <= fcs::kTxSmallMax;
     for (uint64_t i = 0; small && i < n; i++) small = len[i] <= fcs::kOneBytes;
-    if (small && !ds->tx_dcount) {
-        HIPTRY(hipMalloc(&ds->tx_dcount, 64), "hipMalloc(small TX counter)");
-        HIPTRY(hipMemset(ds->tx_dcount, 0, 64), "hipMemset(small TX counter)");
-        ds->tx_count = 0;
+    if (small) {
+        const int e = ensure_small(ds);
+        if (e) return e;
     }
     if (small) {   // everything the kernel needs rides in its arguments; it writes the FCSs itself
         const std::vector<uint32_t> &kinit = kinit_table();
         fcs::TxSmallArgs a;
         a.flag = ds->tx_dflag;
+        a.ok = nullptr;
         a.count = ds->tx_dcount;
         a.count_base = ds->tx_count;
         a.blob = ds->d_one_blob;
@@ -616,9 +640,9 @@ int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena
         *ds->tx_flag = 0;
     }
     if (n > ds->vz_cap) {
-        if (ds->vz_off) hipHostFree(ds->vz_off);
-        if (ds->vz_len) hipHostFree(ds->vz_len);
-        if (ds->vz_ok) hipHostFree(ds->vz_ok);
+        if (ds->vz_off) HIPTRY(hipHostFree(ds->vz_off), "hipHostFree(verify off)");
+        if (ds->vz_len) HIPTRY(hipHostFree(ds->vz_len), "hipHostFree(verify len)");
+        if (ds->vz_ok) HIPTRY(hipHostFree(ds->vz_ok), "hipHostFree(verify ok)");
         if (!ds->vz_dbad) HIPTRY(hipMalloc(&ds->vz_dbad, 64), "hipMalloc(verify bad scratch)");
         ds->vz_off = nullptr;
         ds->vz_len = nullptr;
@@ -633,14 +657,40 @@ int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena
         HIPTRY(hipHostGetDevicePointer((void **)&ds->vz_dok, ds->vz_ok, 0), "hipHostGetDevicePointer(ok)");
         ds->vz_cap = cap;
     }
-    std::memcpy(ds->vz_off, off, n * 8);
-    std::memcpy(ds->vz_len, len, n * 4);
-    int rc = launch_var(ds, darena, arena_bytes, ds->vz_doff, ds->vz_dlen, nullptr, n, ds->tx_stream, ds->vz_dok,
+    bool small = n <= fcs::kTxSmallMax;
+    for (uint64_t i = 0; small && i < n; i++) small = len[i] <= fcs::kOneBytes;
+    int rc = 0;
+    if (small) {   // the small-batch kernel in verify mode: frame list in its arguments
+        if ((rc = ensure_small(ds))) return rc;
+        const std::vector<uint32_t> &kinit = kinit_table();
+        fcs::TxSmallArgs a;
+        a.flag = ds->tx_dflag;
+        a.blob = ds->d_one_blob;
+        a.base = (uint8_t *)darena;
+        a.ok = ds->vz_dok;
+        a.count = ds->tx_dcount;
+        a.count_base = ds->tx_count;
+        a.seq = ++ds->tx_seq;
+        a.n = (uint32_t)n;
+        a.pad = 0;
+        for (uint64_t i = 0; i < n; i++) {
+            a.off[i] = off[i];
+            a.len[i] = len[i];
+            a.kinit[i] = kinit[len[i]];
+        }
+        HIPTRY(fcs::launch_tx_small(a, ds->tx_stream), "launching the small verify kernel");
+        ds->tx_count += n;
+        if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, a.seq, "small verify batch"))) return rc;
+    } else {
+        std::memcpy(ds->vz_off, off, n * 8);
+        std::memcpy(ds->vz_len, len, n * 4);
+        rc = launch_var(ds, darena, arena_bytes, ds->vz_doff, ds->vz_dlen, nullptr, n, ds->tx_stream, ds->vz_dok,
                         ds->vz_dbad);
-    if (rc) return rc;
-    const uint64_t v = ++ds->tx_seq;
-    HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
-    if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small verify batch"))) return rc;
+        if (rc) return rc;
+        const uint64_t v = ++ds->tx_seq;
+        HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
+        if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small verify batch"))) return rc;
+    }
     std::memcpy(ok, ds->vz_ok, n);
     int64_t bad = 0;
     for (uint64_t i = 0; i < n; i++) bad += ok[i] == 0;
@@ -736,6 +786,50 @@ int run_host_sharded(HostJob job, uint64_t n) {
 
 // Pageable host bytes are copied into pinned staging before their DMA; one core copies
 // ~28 GB/s, below PCIe Gen5 x16, so large spans are split over a few threads.
+int fcs::verify_mapped_submit(const uint8_t *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
+                              uint8_t *ok, uint64_t n, uint64_t *ticket) {
+    if (!arena || !off || !len || !ok || !ticket || n == 0) return fail(EINVAL, "verify_mapped_submit: bad arguments");
+    for (uint64_t i = 0; i < n; i++)
+        if (len[i] > fcs::kOneBytes || off[i] > arena_bytes || len[i] > arena_bytes - off[i])
+            return fail(EINVAL, "verify_mapped_submit: frame %llu out of range", (unsigned long long)i);
+    const uint8_t *da = pinned_dev_ptr(arena, arena_bytes);
+    const uint8_t *doff = pinned_dev_ptr(off, n * 8), *dlen = pinned_dev_ptr(len, n * 4);
+    uint8_t *dok = pinned_dev_ptr(ok, n);
+    if (!da || !doff || !dlen || !dok) return fail(EINVAL, "verify_mapped_submit: buffers not from fcs_host_alloc");
+    std::vector<DevState *> devs;
+    int rc = engine_devices(&devs);
+    if (rc) return rc;
+    DevState *ds = devs[0];
+    std::lock_guard<std::mutex> lk(ds->tx_mu);
+    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    if ((rc = ensure_small(ds))) return rc;
+    fcs::ListArgs a;
+    a.flag = ds->tx_dflag;
+    a.blob = ds->d_one_blob;
+    a.kinit = ds->d_kinit;
+    a.base = (uint8_t *)da;
+    a.off = (const uint64_t *)doff;
+    a.len = (const uint32_t *)dlen;
+    a.ok = dok;
+    a.count = ds->tx_dcount;
+    a.count_base = ds->tx_count;
+    a.seq = ds->tx_seq + 1;
+    a.n = (uint32_t)n;
+    a.pad = 0;
+    HIPTRY(fcs::launch_small_list(a, ds->tx_stream), "launching the mapped-list verify kernel");
+    ds->tx_seq++;
+    ds->tx_count += n;
+    *ticket = a.seq;
+    return 0;
+}
+
+int fcs::verify_mapped_wait(uint64_t ticket) {
+    std::vector<DevState *> devs;
+    int rc = engine_devices(&devs);
+    if (rc) return rc;
+    return wait_flag(devs[0]->tx_stream, devs[0]->tx_flag, ticket, "mapped-list verify");
+}
+
 void fcs::staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes) {
     constexpr uint64_t kCopySplitBytes = 16ull << 20;
     constexpr int kCopyThreads = 4;
@@ -845,6 +939,7 @@ void fcs_engine_fini(void) {
         if (ds->one_flag) hipHostFree(ds->one_flag);
         if (ds->d_blob) hipFree(ds->d_blob);
         if (ds->d_one_blob) hipFree(ds->d_one_blob);
+        if (ds->d_kinit) hipFree(ds->d_kinit);
     }
     g_dev.clear();
     g_engine_devs.clear();

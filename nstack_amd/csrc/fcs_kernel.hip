@@ -1151,8 +1151,9 @@ __global__ __launch_bounds__(64) void fcs_one_kernel(OneArgs a) {
 // (mapped) memory: the same window, lane chain and tree as fcs_one_kernel. The wave first copies
 // the 16-byte blocks that hold the frame into its LDS window with coalesced 16-byte loads (host
 // memory over PCIe wants few, wide requests), then every lane takes its 24 bytes from there.
-// Blocks start no earlier than the one holding `start` (the frame may open its allocation) and
-// end with the one holding end + 3 (the realignment reads into the FCS slot after the frame).
+// Blocks start with the one holding `start` and end with the one holding end - 1: no byte of
+// another page is touched (the frame may open or close its allocation). The realignment's last
+// LDS dword may reach past the copied bytes; those bytes lie beyond the lane's 24 and are unused.
 constexpr uint32_t kOneWinBytes = kOneBytes + 32;   // per-wave LDS window (16-B aligned base)
 
 __device__ __forceinline__ uint32_t one_frame_reg(const uint32_t *t, uint8_t *win, uint64_t start, uint64_t end,
@@ -1160,7 +1161,7 @@ __device__ __forceinline__ uint32_t one_frame_reg(const uint32_t *t, uint8_t *wi
     const uint64_t wbase = end - kOneBytes;            // window byte 0 (may precede the frame)
     const uint64_t g0 = wbase & ~15ull;                // LDS byte 0 <-> this address
     const uint64_t b0 = (start > wbase ? start : wbase) & ~15ull;
-    const uint64_t b1 = (end + 3 + 16) & ~15ull;       // one past the last block to load
+    const uint64_t b1 = (end + 15) & ~15ull;           // one past the last block to load
     for (uint64_t a = b0 + 16 * (uint64_t)lane; a < b1; a += 16 * 64)
         *reinterpret_cast<u32x4a4 *>(win + (a - g0)) = gload<u32x4a4>(a);
     __builtin_amdgcn_wave_barrier();
@@ -1200,6 +1201,25 @@ __device__ __forceinline__ uint32_t one_frame_reg(const uint32_t *t, uint8_t *wi
     return x;
 }
 
+// A small-batch frame's result: RX verify writes ok[f] (the frame carries its trailer; it checks
+// iff the residue shows), TX writes the FCS little-endian right after the frame
+// (src/linux/ether.c:263). Then the frame counts itself done; the batch's last frame stores seq.
+__device__ __forceinline__ void small_finish(uint32_t fcs, uint8_t *ok, uint32_t f, uint64_t start, uint32_t L,
+                                             int lane, unsigned long long *count, uint64_t count_base, uint32_t n,
+                                             uint64_t *flag, uint64_t seq) {
+    if (ok) {
+        if (lane == 0) ok[f] = (L >= 4 && fcs == 0x2144DF1Cu) ? 1 : 0;
+    } else if (lane < 4) {
+        *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(start + L + lane) = (uint8_t)(fcs >> (8 * lane));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this frame's result has reached host memory
+    if (lane == 0) {
+        const uint64_t done = __hip_atomic_fetch_add(count, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+        if (done == count_base + n - 1)   // the batch's last frame
+            __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
 // One workgroup (one wave) per frame, so the frames' PCIe reads come from as many CUs: one CU
 // reading 16 frames of host memory took 17.7 us, against 10.6 us for one. Each wave writes its
 // FCS into the frame, makes it visible system-wide and counts itself done on a device counter;
@@ -1219,16 +1239,23 @@ __global__ __launch_bounds__(64) void fcs_tx_small_kernel(TxSmallArgs a) {
     const uint32_t ki = *(const __attribute__((address_space(4))) uint32_t *)(ka + offsetof(TxSmallArgs, kinit) + 4 * f);
     const uint64_t start = (uint64_t)a.base + o;
     const uint32_t x = one_frame_reg(t, win, start, start + L, lane);
-    if (lane < 4) {   // src/linux/ether.c:263: the FCS little-endian right after the frame
-        const uint32_t fcs = ~(x ^ ki);
-        *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(start + L + lane) = (uint8_t)(fcs >> (8 * lane));
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this frame's FCS has reached host memory
-    if (lane == 0) {
-        const uint64_t done = __hip_atomic_fetch_add(a.count, 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-        if (done == a.count_base + a.n - 1)   // the batch's last frame
-            __hip_atomic_store(a.flag, a.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    small_finish(~(x ^ ki), a.ok, f, start, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
+}
+
+__global__ __launch_bounds__(64) void fcs_small_list_kernel(ListArgs a) {
+    __shared__ __attribute__((aligned(16))) uint32_t t[kOneBlobWords];
+    __shared__ __attribute__((aligned(16))) uint8_t win[kOneWinBytes];
+    const int lane = threadIdx.x;
+    const uint32_t f = blockIdx.x;
+    const uint64_t o = a.off[f];      // one mapped read each (uniform address)
+    const uint32_t L = a.len[f];
+    for (int i = lane; i < (int)kOneBlobWords / 4; i += 64)
+        reinterpret_cast<u32x4a4 *>(t)[i] = reinterpret_cast<const u32x4a4 *>(a.blob)[i];
+    const uint32_t ki = a.kinit[L < kOneBytes ? L : kOneBytes];
+    __syncthreads();
+    const uint64_t start = (uint64_t)a.base + o;
+    const uint32_t x = one_frame_reg(t, win, start, start + L, lane);
+    small_finish(~(x ^ ki), a.ok, f, start, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
 }
 
 // TX mode helper: after the FCS kernel wrote crc[i], store it little-endian after each frame.
@@ -1322,6 +1349,12 @@ hipError_t launch_one(const OneArgs &a, hipStream_t st) {
 hipError_t launch_tx_small(const TxSmallArgs &a, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
     hipLaunchKernelGGL(fcs_tx_small_kernel, dim3(a.n), dim3(64), 0, st, a);
+    return hipGetLastError();
+}
+
+hipError_t launch_small_list(const ListArgs &a, hipStream_t st) {
+    (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    hipLaunchKernelGGL(fcs_small_list_kernel, dim3(a.n), dim3(64), 0, st, a);
     return hipGetLastError();
 }
 

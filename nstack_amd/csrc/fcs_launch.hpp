@@ -38,16 +38,32 @@ struct OneArgs {
     uint32_t data[kOneBytes / 4];
 };
 
-// Small TX batches in mapped host memory (fcs_tx_small_kernel): 1..kTxSmallMax frames of up to
-// kOneBytes covered bytes each, their offsets, lengths and A_len(0xFFFFFFFF) in the kernel
+// Small TX (or RX verify) batches in mapped host memory (fcs_tx_small_kernel): 1..kTxSmallMax
+// frames of up to kOneBytes bytes each, their offsets, lengths and A_len(0xFFFFFFFF) in the kernel
 // arguments. One workgroup per frame writes its FCS into the frame in host memory; the last one
 // done (device counter `count`, which has reached count_base when the launch starts) stores
 // `seq` into `flag`.
+// The same kernel body with the frame list in (mapped) memory instead of the arguments, for any
+// batch size (fcs_small_list_kernel): RX batches checked while the next recvmmsg runs.
+struct ListArgs {
+    uint64_t *flag;
+    const uint32_t *blob;    // kOneBlobWords
+    const uint32_t *kinit;   // A_L(0xFFFFFFFF), L = 0 .. kOneBytes (device memory)
+    uint8_t *base;           // device address of the (mapped) arena
+    const uint64_t *off;     // device addresses of mapped arrays of n entries
+    const uint32_t *len;
+    uint8_t *ok;             // null: TX (write each FCS); else RX verify
+    unsigned long long *count;
+    uint64_t count_base;
+    uint64_t seq;
+    uint32_t n, pad;
+};
 constexpr uint32_t kTxSmallMax = 64;
 struct TxSmallArgs {
     uint64_t *flag;
     const uint32_t *blob;    // kOneBlobWords
     uint8_t *base;           // device address of the (mapped) arena
+    uint8_t *ok;             // null: TX (write each FCS); else RX verify: ok[i] (mapped) per frame
     unsigned long long *count;
     uint64_t count_base;
     uint64_t seq;
@@ -62,6 +78,7 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st);
 hipError_t launch_one(const OneArgs &a, hipStream_t st);
 hipError_t launch_tx_small(const TxSmallArgs &a, hipStream_t st);
+hipError_t launch_small_list(const ListArgs &a, hipStream_t st);
 hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hipStream_t st);
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st);
 hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,

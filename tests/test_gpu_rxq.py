@@ -60,3 +60,55 @@ def test_rx_verify_drops_corrupted_frames(max_batch):
     assert got == good
     assert frames == len(sent) and dropped == 0
     assert bad + echoes + len(good) == len(sent) and bad > 0 and echoes > 0
+
+
+@pytest.mark.parametrize("max_batch", [16, 64])
+def test_rx_pipeline_with_live_sender(max_batch):
+    """Frames arriving while batches are checked: the queue overlaps the GPU check of one batch
+    with the recvmmsg of the next (two buffers). A sender thread pushes bursts with pauses, so
+    the receiver meets full, partial and empty queues; every good frame must come out once, in
+    order, and no corrupted one."""
+    import threading
+    import time
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    b.setblocking(False)
+    rng = random.Random(1000 + max_batch)
+    frames, good = [], []
+    for i in range(3000):
+        pl = i.to_bytes(4, "little") + bytes(rng.randrange(256) for _ in range(rng.choice([0, 60, 700, 1400])))
+        f = bytearray(ether_send_frame(pl))
+        if rng.random() < 0.05:
+            f[rng.randrange(len(f))] ^= 0x10
+        else:
+            good.append(pl + bytes(max(0, 56 - len(pl))))
+        frames.append(bytes(f))
+
+    def sender():
+        for k in range(0, len(frames), 97):
+            for f in frames[k:k + 97]:
+                a.send(f)
+            time.sleep(0.0005 * (k % 3))
+
+    th = threading.Thread(target=sender)
+    th.start()
+    got = []
+    deadline = time.time() + 60
+    with na.RxQueue(b.fileno(), OWN, max_batch=max_batch, trailer=True) as q:
+        while len(got) < len(good) and time.time() < deadline:
+            n, dst, src, proto, pl = q.receive()
+            assert n >= 0, n
+            if n:
+                got.append(pl)
+        th.join()
+        while True:   # the corrupted frames after the last good one
+            n, *_ = q.receive()
+            assert n >= 0, n
+            if n == 0:
+                break
+            got.append(None)
+        st = q.stats()
+    a.close(), b.close()
+    assert got == good
+    assert st[1] == len(frames) - len(good)

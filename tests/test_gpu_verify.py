@@ -104,6 +104,34 @@ def test_verify_host_matches_device(dev, var_kernel, oracle):
     assert nbad == int((exp == 0).sum())
 
 
+@pytest.mark.parametrize("n", [1, 5, 64, 65, 300])
+def test_verify_host_in_place_small_batches(dev, oracle, n):
+    """RX-queue-sized batches in fcs_host_alloc memory take the in-place paths (up to 64 frames of
+    up to 1536 B: the small-batch kernel with the frame list in its arguments). Frames of 0..3
+    bytes never check, the last frame ends on the allocation's last byte (a page boundary), and
+    a fifth of the frames carry a flipped bit."""
+    rng = np.random.default_rng(500 + n)
+    lens = [int(x) for x in rng.integers(64, 1519, n)]
+    lens[:min(n, 4)] = [0, 3, 4, 1536][:min(n, 4)]
+    arena, off, ln = build_rx_batch(oracle, rng, lens)
+    last = int(off[-1] + ln[-1])
+    size = (last + 4095) // 4096 * 4096
+    shift = size - last                                # move the frames so the last one ends the buffer
+    buf = na.host_buffer(size)
+    try:
+        buf[:] = 0
+        buf[shift:shift + last] = arena[:last]
+        off2 = off + np.uint64(shift)
+        exp = expected_ok(oracle, buf, off2, ln)
+        ok = np.zeros(n, dtype=np.uint8)
+        nbad = na.verify_host(buf, size, off2, ln, ok, n)
+        assert np.array_equal(ok, exp)
+        assert nbad == int((exp == 0).sum())
+        assert exp[0] == 0 and (n < 2 or exp[1] == 0)
+    finally:
+        na.host_free(buf)
+
+
 @pytest.mark.parametrize("L", [74, 1518, 9018])
 def test_verify_fixed_single_and_multi_segment(dev, oracle, L):
     """Fixed stride: the single-segment kernel (<= 1536 B) and the generic multi-segment one."""
