@@ -1100,6 +1100,18 @@ __global__ void signal_kernel(uint64_t *flag, uint64_t v) {
     }
 }
 
+// The single-frame tables (7 KiB) into LDS: every load issued before the first store, so the
+// wave waits for one memory latency instead of seven in a row.
+__device__ __forceinline__ void stage_one_blob(uint32_t *t, const uint32_t *blob, int lane) {
+    constexpr int kIters = kOneBlobWords / 4 / 64;
+    static_assert(kOneBlobWords % 256 == 0, "one 16-byte piece per lane per step");
+    u32x4a4 v[kIters];
+#pragma unroll
+    for (int k = 0; k < kIters; k++) v[k] = reinterpret_cast<const u32x4a4 *>(blob)[lane + 64 * k];
+#pragma unroll
+    for (int k = 0; k < kIters; k++) reinterpret_cast<u32x4a4 *>(t)[lane + 64 * k] = v[k];
+}
+
 // Drop-in ether_fcs for one frame (fcs_launch.hpp OneArgs). The frame arrives in the kernel
 // arguments, right-aligned in a 1536-byte window with zeros in front: from a zero register,
 // leading zeros change nothing, and the all-ones start of the real CRC is added back as
@@ -1116,16 +1128,23 @@ __device__ __forceinline__ uint32_t one_step(const uint32_t *t, uint32_t x, uint
 __global__ __launch_bounds__(64) void fcs_one_kernel(OneArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t t[kOneBlobWords];
     const int lane = threadIdx.x;
-    for (int i = lane; i < (int)kOneBlobWords / 4; i += 64)
-        reinterpret_cast<u32x4a4 *>(t)[i] = reinterpret_cast<const u32x4a4 *>(a.blob)[i];
+#ifndef FCS_ONE_NOBLOB   // measurement-only build: tables not staged (wrong FCS; timing only)
+    stage_one_blob(t, a.blob, lane);
+#endif
     // the window words straight from the kernel-argument segment (no private copy of `a`)
     typedef const __attribute__((address_space(4))) uint32_t karg_u32;
     karg_u32 *dw = reinterpret_cast<karg_u32 *>(
         (const __attribute__((address_space(4))) uint8_t *)__builtin_amdgcn_kernarg_segment_ptr() +
         offsetof(OneArgs, data));
     uint32_t w[6];
+#ifdef FCS_ONE_NOARG   // measurement-only build: the frame words not read (wrong FCS; timing only)
+#pragma unroll
+    for (int q = 0; q < 6; q++) w[q] = lane * 6 + q;
+    (void)dw;
+#else
 #pragma unroll
     for (int q = 0; q < 6; q++) w[q] = dw[lane * 6 + q];
+#endif
     __syncthreads();
     uint32_t x = w[0];
 #pragma unroll
@@ -1156,15 +1175,32 @@ __global__ __launch_bounds__(64) void fcs_one_kernel(OneArgs a) {
 // LDS dword may reach past the copied bytes; those bytes lie beyond the lane's 24 and are unused.
 constexpr uint32_t kOneWinBytes = kOneBytes + 32;   // per-wave LDS window (16-B aligned base)
 
-__device__ __forceinline__ uint32_t one_frame_reg(const uint32_t *t, uint8_t *win, uint64_t start, uint64_t end,
-                                                  int lane) {
+// The tables (blob, staged into t) and the frame are fetched together: every load of both is
+// issued before the first LDS store, so the table latency hides under the frame's PCIe reads.
+__device__ __forceinline__ uint32_t one_frame_reg(uint32_t *t, const uint32_t *blob, uint8_t *win, uint64_t start,
+                                                  uint64_t end, int lane) {
     const uint64_t wbase = end - kOneBytes;            // window byte 0 (may precede the frame)
     const uint64_t g0 = wbase & ~15ull;                // LDS byte 0 <-> this address
     const uint64_t b0 = (start > wbase ? start : wbase) & ~15ull;
     const uint64_t b1 = (end + 15) & ~15ull;           // one past the last block to load
-    for (uint64_t a = b0 + 16 * (uint64_t)lane; a < b1; a += 16 * 64)
-        *reinterpret_cast<u32x4a4 *>(win + (a - g0)) = gload<u32x4a4>(a);
-    __builtin_amdgcn_wave_barrier();
+    constexpr int kTab = kOneBlobWords / 4 / 64;
+    constexpr int kBlk = (kOneWinBytes / 16 + 63) / 64;
+    u32x4a4 tv[kTab], fv[kBlk];
+#pragma unroll
+    for (int k = 0; k < kTab; k++) tv[k] = reinterpret_cast<const u32x4a4 *>(blob)[lane + 64 * k];
+#pragma unroll
+    for (int k = 0; k < kBlk; k++) {
+        const uint64_t a = b0 + 16 * (uint64_t)(lane + 64 * k);
+        if (a < b1) fv[k] = gload<u32x4a4>(a);
+    }
+#pragma unroll
+    for (int k = 0; k < kTab; k++) reinterpret_cast<u32x4a4 *>(t)[lane + 64 * k] = tv[k];
+#pragma unroll
+    for (int k = 0; k < kBlk; k++) {
+        const uint64_t a = b0 + 16 * (uint64_t)(lane + 64 * k);
+        if (a < b1) *reinterpret_cast<u32x4a4 *>(win + (a - g0)) = fv[k];
+    }
+    __syncthreads();
     const int64_t c = (int64_t)wbase + 24 * lane;      // this lane's window bytes [c, c + 24)
     uint32_t w[6] = {0, 0, 0, 0, 0, 0};
     if (c + 24 > (int64_t)start) {
@@ -1228,9 +1264,6 @@ __global__ __launch_bounds__(64) void fcs_tx_small_kernel(TxSmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t t[kOneBlobWords];
     __shared__ __attribute__((aligned(16))) uint8_t win[kOneWinBytes];
     const int lane = threadIdx.x;
-    for (int i = lane; i < (int)kOneBlobWords / 4; i += 64)
-        reinterpret_cast<u32x4a4 *>(t)[i] = reinterpret_cast<const u32x4a4 *>(a.blob)[i];
-    __syncthreads();
     const uint32_t f = blockIdx.x;
     typedef const __attribute__((address_space(4))) uint8_t karg_u8;
     karg_u8 *ka = (karg_u8 *)__builtin_amdgcn_kernarg_segment_ptr();
@@ -1238,7 +1271,7 @@ __global__ __launch_bounds__(64) void fcs_tx_small_kernel(TxSmallArgs a) {
     const uint32_t L = *(const __attribute__((address_space(4))) uint32_t *)(ka + offsetof(TxSmallArgs, len) + 4 * f);
     const uint32_t ki = *(const __attribute__((address_space(4))) uint32_t *)(ka + offsetof(TxSmallArgs, kinit) + 4 * f);
     const uint64_t start = (uint64_t)a.base + o;
-    const uint32_t x = one_frame_reg(t, win, start, start + L, lane);
+    const uint32_t x = one_frame_reg(t, a.blob, win, start, start + L, lane);
     small_finish(~(x ^ ki), a.ok, f, start, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
 }
 
@@ -1249,12 +1282,9 @@ __global__ __launch_bounds__(64) void fcs_small_list_kernel(ListArgs a) {
     const uint32_t f = blockIdx.x;
     const uint64_t o = a.off[f];      // one mapped read each (uniform address)
     const uint32_t L = a.len[f];
-    for (int i = lane; i < (int)kOneBlobWords / 4; i += 64)
-        reinterpret_cast<u32x4a4 *>(t)[i] = reinterpret_cast<const u32x4a4 *>(a.blob)[i];
     const uint32_t ki = a.kinit[L < kOneBytes ? L : kOneBytes];
-    __syncthreads();
     const uint64_t start = (uint64_t)a.base + o;
-    const uint32_t x = one_frame_reg(t, win, start, start + L, lane);
+    const uint32_t x = one_frame_reg(t, a.blob, win, start, start + L, lane);
     small_finish(~(x ^ ki), a.ok, f, start, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
 }
 
