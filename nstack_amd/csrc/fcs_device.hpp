@@ -10,12 +10,14 @@ __attribute__((visibility("hidden"))) int current_device(int *dev, int *cus);
 __attribute__((visibility("hidden"))) int engine_device0(int *dev, int *cus);
 // memcpy into pinned staging, split over a few threads for large spans (host pipelines).
 __attribute__((visibility("hidden"))) void staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes);
-// Asynchronous RX residue check (the small-batch kernel reading its frame list from mapped
-// memory): arena, off, len and ok must all lie in fcs_host_alloc ranges, every len <= 1536.
-// Launches and returns a ticket, or -errno (nothing launched). ok[i] is valid once
-// verify_mapped_wait(ticket) returned 0.
-__attribute__((visibility("hidden"))) int verify_mapped_submit(const uint8_t *arena, uint64_t arena_bytes,
-                                                               const uint64_t *off, const uint32_t *len,
-                                                               uint8_t *ok, uint64_t n, uint64_t *ticket);
-__attribute__((visibility("hidden"))) int verify_mapped_wait(uint64_t ticket);
+// Asynchronous batch over frames in fcs_host_alloc memory (the small-batch kernel reading its frame
+// list from mapped memory): arena, off, len (and ok) must all lie in fcs_host_alloc ranges, every
+// len <= 1536. ok == nullptr: TX, each frame's FCS written little-endian after it (len + 4 must
+// fit the arena); else RX residue check, ok[i] = 1 / 0. Launches and returns a ticket, or -errno
+// (nothing launched). Results are in place once mapped_wait(ticket) returned 0; tickets complete
+// in the order they were issued.
+__attribute__((visibility("hidden"))) int mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off,
+                                                        const uint32_t *len, uint8_t *ok, uint64_t n,
+                                                        uint64_t *ticket);
+__attribute__((visibility("hidden"))) int mapped_wait(uint64_t ticket);
 }  // namespace fcs

@@ -786,16 +786,17 @@ int run_host_sharded(HostJob job, uint64_t n) {
 
 // Pageable host bytes are copied into pinned staging before their DMA; one core copies
 // ~28 GB/s, below PCIe Gen5 x16, so large spans are split over a few threads.
-int fcs::verify_mapped_submit(const uint8_t *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
-                              uint8_t *ok, uint64_t n, uint64_t *ticket) {
-    if (!arena || !off || !len || !ok || !ticket || n == 0) return fail(EINVAL, "verify_mapped_submit: bad arguments");
+int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len, uint8_t *ok,
+                       uint64_t n, uint64_t *ticket) {
+    if (!arena || !off || !len || !ticket || n == 0) return fail(EINVAL, "mapped_submit: bad arguments");
+    const uint64_t tail = ok ? 0 : 4;   // TX writes the FCS after each frame
     for (uint64_t i = 0; i < n; i++)
-        if (len[i] > fcs::kOneBytes || off[i] > arena_bytes || len[i] > arena_bytes - off[i])
-            return fail(EINVAL, "verify_mapped_submit: frame %llu out of range", (unsigned long long)i);
+        if (len[i] > fcs::kOneBytes || off[i] > arena_bytes || len[i] + tail > arena_bytes - off[i])
+            return fail(EINVAL, "mapped_submit: frame %llu out of range", (unsigned long long)i);
     const uint8_t *da = pinned_dev_ptr(arena, arena_bytes);
     const uint8_t *doff = pinned_dev_ptr(off, n * 8), *dlen = pinned_dev_ptr(len, n * 4);
-    uint8_t *dok = pinned_dev_ptr(ok, n);
-    if (!da || !doff || !dlen || !dok) return fail(EINVAL, "verify_mapped_submit: buffers not from fcs_host_alloc");
+    uint8_t *dok = ok ? pinned_dev_ptr(ok, n) : nullptr;
+    if (!da || !doff || !dlen || (ok && !dok)) return fail(EINVAL, "mapped_submit: buffers not from fcs_host_alloc");
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
     if (rc) return rc;
@@ -816,18 +817,18 @@ int fcs::verify_mapped_submit(const uint8_t *arena, uint64_t arena_bytes, const 
     a.seq = ds->tx_seq + 1;
     a.n = (uint32_t)n;
     a.pad = 0;
-    HIPTRY(fcs::launch_small_list(a, ds->tx_stream), "launching the mapped-list verify kernel");
+    HIPTRY(fcs::launch_small_list(a, ds->tx_stream), "launching the mapped-list kernel");
     ds->tx_seq++;
     ds->tx_count += n;
     *ticket = a.seq;
     return 0;
 }
 
-int fcs::verify_mapped_wait(uint64_t ticket) {
+int fcs::mapped_wait(uint64_t ticket) {
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
     if (rc) return rc;
-    return wait_flag(devs[0]->tx_stream, devs[0]->tx_flag, ticket, "mapped-list verify");
+    return wait_flag(devs[0]->tx_stream, devs[0]->tx_flag, ticket, "mapped-list batch");
 }
 
 void fcs::staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes) {

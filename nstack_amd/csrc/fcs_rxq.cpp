@@ -122,7 +122,7 @@ int start_check(fcs_rxq *q, RxBuf &B) {
         return 0;
     }
     if (q->pipelined) {
-        const int rc = fcs::verify_mapped_submit(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n, &B.ticket);
+        const int rc = fcs::mapped_submit(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n, &B.ticket);
         if (rc) {
             B.state = RxBuf::kEmpty;
             return rc;
@@ -141,7 +141,7 @@ int start_check(fcs_rxq *q, RxBuf &B) {
 
 int finish_check(RxBuf &B) {
     if (B.state != RxBuf::kInFlight) return 0;
-    const int rc = fcs::verify_mapped_wait(B.ticket);
+    const int rc = fcs::mapped_wait(B.ticket);
     B.state = rc ? RxBuf::kEmpty : RxBuf::kReady;
     return rc;
 }

@@ -6,6 +6,8 @@
 #include <cstring>
 #include <thread>
 #include <chrono>
+#include <mutex>
+#include <deque>
 extern "C" {
 int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n) {
     for (uint64_t i = 0; i < n; i++) { uint32_t c = 0xA5A5A5A5u ^ len[i]; std::memcpy((uint8_t*)base + i*stride + len[i], &c, 4); }
@@ -22,3 +24,38 @@ const char *fcs_last_error(void) { return "stub"; }
 void *fcs_host_alloc(uint64_t b) { return std::malloc(b); }
 void fcs_host_free(void *p) { std::free(p); }
 }
+
+// Asynchronous form (fcs_device.hpp): the "GPU step" completes 20 us after its submission,
+// tickets in order.
+namespace fcs {
+static std::mutex g_mu;
+static uint64_t g_next = 0;
+static std::deque<std::pair<uint64_t, std::chrono::steady_clock::time_point>> g_due;
+int mapped_submit(uint8_t *arena, uint64_t, const uint64_t *off, const uint32_t *len, uint8_t *ok, uint64_t n,
+                  uint64_t *ticket) {
+    for (uint64_t i = 0; i < n; i++) {
+        if (ok) { ok[i] = 1; continue; }
+        uint32_t c = 0xA5A5A5A5u ^ len[i];
+        std::memcpy(arena + off[i] + len[i], &c, 4);
+    }
+    std::lock_guard<std::mutex> lk(g_mu);
+    *ticket = ++g_next;
+    g_due.emplace_back(*ticket, std::chrono::steady_clock::now() + std::chrono::microseconds(20));
+    return 0;
+}
+int mapped_wait(uint64_t ticket) {
+    for (;;) {
+        std::chrono::steady_clock::time_point t;
+        {
+            std::lock_guard<std::mutex> lk(g_mu);
+            while (!g_due.empty() && g_due.front().first < ticket) g_due.pop_front();
+            if (g_due.empty() || g_due.front().first != ticket) return 0;
+            t = g_due.front().second;
+        }
+        std::this_thread::sleep_until(t);
+        std::lock_guard<std::mutex> lk(g_mu);
+        if (!g_due.empty() && g_due.front().first == ticket) g_due.pop_front();
+        return 0;
+    }
+}
+}  // namespace fcs
