@@ -965,8 +965,14 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
             issue_any<TINY>(p, cstart, it.valid && it.zr < kChunkBytes, it.ch);
         };
         auto finish = [&](const FlatItem &it) {
+#ifdef FCS_FLAT_NOCRC   // measurement-only build: loads and dealing without the CRC work (wrong FCS)
+            uint32_t v = it.ch.x6 ^ it.c;
+#pragma unroll
+            for (int q = 0; q < 6; q++) v ^= it.ch.x[q].x ^ it.ch.x[q].y ^ it.ch.x[q].z ^ it.ch.x[q].w;
+#else
             const uint32_t own = chunk_value<TINY>(lds, it.ch, it.zr, it.valid ? inv_start(lds, it.zr) : 0u, base0, base1);
             const uint32_t v = chunk_shift(lds, own, it.c & 15u);
+#endif
             if (it.valid && v) atomicXor(&acc[it.src], v);
         };
 #ifdef FCS_FLAT_PIPE   // measurement-only build: the next item's loads in flight during this one
