@@ -78,3 +78,33 @@ def test_errors(tmp_path):
     p = tmp_path / "big.pcap"
     p.write_bytes(build_pcap([b"\x07" * 64]))
     assert lib.fcs_pcap_read(os.fsencode(str(p)), small.ctypes.data, 10, off.ctypes.data, ln.ctypes.data, 1) == -28
+
+
+def test_edge_files(tmp_path):
+    """Empty file, header only, and a record header cut short (the mmap parser's bounds)."""
+    lib = na.load()
+    e = tmp_path / "empty.pcap"
+    e.write_bytes(b"")
+    assert lib.fcs_pcap_scan(os.fsencode(str(e)), None, None, None, None) == -22
+    h = tmp_path / "hdr.pcap"
+    h.write_bytes(build_pcap([]))
+    assert na.pcap_scan(str(h)) == (0, 0, 1, 0)
+    c = tmp_path / "cuthdr.pcap"
+    c.write_bytes(build_pcap([b"\x01" * 30]) + b"\x00" * 10)
+    assert lib.fcs_pcap_scan(os.fsencode(str(c)), None, None, None, None) == -22
+
+
+def test_large_capture_parallel_copy(tmp_path):
+    """Over 64 MiB of records the read copies them on several threads, split by bytes: every
+    record must land at its packed offset intact (158 MB, lengths 60..1518: two threads)."""
+    rng = np.random.default_rng(9)
+    n = 200000
+    lens = rng.integers(60, 1519, n).astype(np.uint32)
+    off = np.zeros(n, dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1], dtype=np.uint64)
+    arena = rng.integers(0, 256, int(off[-1] + lens[-1]), dtype=np.uint8)
+    p = tmp_path / "large.pcap"
+    na.pcap_write(str(p), arena, off, lens)
+    got, o2, l2, lt = na.pcap_read(str(p))
+    assert lt == 1 and np.array_equal(l2, lens) and np.array_equal(o2, off)
+    assert np.array_equal(got, arena)
