@@ -30,8 +30,8 @@ sub(r'not, goes through the drop-in.s single-frame kernel below: [0-9.]+ µs \(w
     f"not, goes through the drop-in's single-frame kernel below: {pin[1]['us_per_call']:.1f} µs (was 13.5). The TX\n  queue's lone sync producer now sends {g('txq','null',1)['Mframes_s']*1000:.0f} k frames/s")
 sub(r'as well\. Per call: [0-9.]+ µs median, [0-9.]+ µs p99 for 1514 B; [0-9.]+ µs for 64 B',
     f"as well. Per call: {dro[1514]['p50_us']:.1f} µs median, {dro[1514]['p99_us']:.1f} µs p99 for 1514 B; {dro[64]['p50_us']:.1f} µs for 64 B")
-sub(r'\{?[0-9.]+ µs for 4000 B; 8\.4–9\.0 µs median over three boxes\)',
-    f"{dro[4000]['p50_us']:.1f} µs for 4000 B; 8.2–9.0 µs median over four boxes)")
+sub(r'[0-9.]+ µs for 4000 B; ([0-9.]+–[0-9.]+ µs median over [a-z]+ boxes\))',
+    f"{dro[4000]['p50_us']:.1f} µs for 4000 B; \\1")
 i=s.index('| TX queue, 1 sync producer, 1500-B payloads |'); j=s.index('\n',i)
 s=s[:i]+f"| TX queue, 1 sync producer, 1500-B payloads | {g('txq','null',1)['Mframes_s']*1000:.0f} k frames/s ({1e3/g('txq','null',1)['Mframes_s']/1000:.1f} µs per frame; was 65 k) | per-frame drop-in `ether_fcs`: {dro[1514]['p50_us']:.1f} µs median per 1514-B call (`profiles/r01_tx_latency.jsonl`) |"+s[j:]
 s16=g('txq','null',16); s16s=g('txq','socketpair',16)
