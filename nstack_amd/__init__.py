@@ -294,6 +294,10 @@ class TxQueue:
         load().fcs_txq_stats(self._q, ctypes.byref(f), ctypes.byref(b), ctypes.byref(e))
         return int(f.value), int(b.value), int(e.value)
 
+    def last_error(self) -> str:
+        """Text of the most recent failed GPU step ("" if none)."""
+        return (load().fcs_txq_last_error(self._q) or b"").decode()
+
     def close(self) -> None:
         if self._q:
             load().fcs_txq_destroy(self._q)

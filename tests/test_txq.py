@@ -50,7 +50,9 @@ def test_no_gpu_fails_every_frame_and_sends_nothing():
             t.join()
         q.flush()
         frames, batches, errors = q.stats()
+        why = q.last_error()
     assert res == [-19] * 10                                     # -ENODEV for every caller
+    assert why                                                   # the failing step's reason
     assert frames == 10 and batches >= 3 and errors == 10       # batches of at most 4
     with pytest.raises(BlockingIOError):
         b.recv(2048)
