@@ -49,7 +49,7 @@ int check_mode(int mode, const uint32_t *addr) {
 }
 
 // ---- host pipeline ----
-constexpr uint64_t kChunkBytes = 64ull << 20;
+constexpr uint64_t kChunkBytes = 128ull << 20;
 constexpr uint64_t kChunkPkts = 1ull << 20;
 constexpr int kDepth = 2;
 
