@@ -1,7 +1,7 @@
 // inet_engine.cpp — the C ABI of include/nstack_inet.h around inet_kernel.hip.
 //
 // Device forms validate and launch; the host form runs a double-buffered H2D -> kernel -> D2H
-// pipeline of 64 MiB chunks on the engine's first GPU (packets of a chunk are copied as one span
+// pipeline of 128 MiB chunks on the engine's first GPU (packets of a chunk are copied as one span
 // when they lie densely, gathered into the pinned staging buffer otherwise). The single-packet
 // forms keep the reference functions' signatures (src/ip.c:39, src/tcp.c:167, src/udp.c:136) and,
 // like them, have no error channel: on an engine failure they abort with the reason.
