@@ -112,3 +112,24 @@ def test_rx_pipeline_with_live_sender(max_batch):
     a.close(), b.close()
     assert got == good
     assert st[1] == len(frames) - len(good)
+
+
+def test_rx_destroy_with_batches_in_flight():
+    """Closing the queue while a batch's check is still on the GPU (the pipeline launches the
+    next batch before handing out the current one) waits for it and frees cleanly; a new queue
+    on the same socket then receives the rest."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+    b.setblocking(False)
+    for i in range(200):
+        a.send(ether_send_frame(i.to_bytes(4, "little") * 20))
+    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True) as q:
+        n, *_rest, pl = q.receive()
+        assert n > 0 and pl[:4] == (0).to_bytes(4, "little")
+    got = 0
+    with na.RxQueue(b.fileno(), OWN, max_batch=64, trailer=True) as q:
+        while q.receive()[0] > 0:
+            got += 1
+    a.close(), b.close()
+    assert 0 < got <= 199 - 15   # the first queue took at least its first two batches
