@@ -62,3 +62,33 @@ def test_capture_with_fcs_verifies(dev, oracle, tmp_path):
     ok = np.zeros(len(l2), dtype=np.uint8)
     assert na.verify_host(a2, a2.nbytes, o2, l2, ok, len(l2)) == len(bad)
     assert set(np.nonzero(ok == 0)[0].tolist()) == bad
+
+
+def test_add_fcs_to_a_capture(dev, oracle, tmp_path):
+    """tools/pcap_fcs.py --add-fcs: a capture without trailers (as veth delivers it) becomes the
+    capture the wire would carry: every frame followed by ether_send's FCS (GPU TX mode), which
+    the residue check then accepts and which matches the oracle byte for byte."""
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "pcap_fcs", os.path.join(os.path.dirname(__file__), "..", "tools", "pcap_fcs.py"))
+    tool = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(tool)
+    rng = np.random.default_rng(21)
+    ln = rng.integers(60, 1515, 500).astype(np.uint32)
+    off = np.zeros(len(ln), dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    arena = rng.integers(0, 256, int(off[-1] + ln[-1]), dtype=np.uint8)
+    src, dst = tmp_path / "plain.pcap", tmp_path / "fcs.pcap"
+    na.pcap_write(str(src), arena, off, ln)
+    a1, o1, l1, lt = na.pcap_read(str(src))
+    tool.add_fcs(a1, o1, l1, str(dst), lt)
+    a2, o2, l2, _ = na.pcap_read(str(dst))
+    assert np.array_equal(l2, ln + 4)
+    ok = np.zeros(len(l2), dtype=np.uint8)
+    assert na.verify_host(a2, a2.nbytes, o2, l2, ok, len(l2)) == 0 and ok.all()
+    for i in rng.integers(0, len(ln), 40):
+        o, L = int(o2[i]), int(ln[i])
+        assert a2[o:o + L].tobytes() == arena[int(off[i]):int(off[i]) + L].tobytes()
+        c = oracle.oracle_ether_fcs(arena[int(off[i]):].ctypes.data, L)
+        assert a2[o + L:o + L + 4].tobytes() == struct.pack("<I", c)
