@@ -106,6 +106,19 @@ def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
         if tag == "O2":   # secondary figure: the same loop on the 16 host cores a GPU box grants
             secs16 = o.oracle_time_fixed(buf.ctypes.data, L, L, frames, out.ctypes.data, 0, 16)
             res["all"] = {"gibs": frames * L / secs16 / GIB, "threads": 16}
+    # the reference's own src/ether_fcs.c (oracle/_ref, built from /root/reference at the reference
+    # Makefile's flags -O0 -g -std=gnu99), called once per frame by the oracle's timing loop
+    ref_path = os.path.join(ROOT, "oracle", "_ref", "libref_fcs.so")
+    if "O2" in res and os.path.exists(ref_path):
+        r = ctypes.CDLL(ref_path)
+        o = ctypes.CDLL(os.path.join(here, "liboracle.so"))
+        FN = ctypes.CFUNCTYPE(ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t)
+        o.oracle_time_calls.restype = ctypes.c_double
+        o.oracle_time_calls.argtypes = [FN, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint32, ctypes.c_size_t,
+                                        ctypes.c_void_p]
+        fn = ctypes.cast(r.ether_fcs, FN)
+        secs = o.oracle_time_calls(fn, buf.ctypes.data, L, L, frames, out.ctypes.data)
+        res["ref"] = {"gibs": frames * L / secs / GIB, "secs": secs, "xor": int(np.bitwise_xor.reduce(out))}
     if "O2" not in res:
         return None
     cpu_model = ""
@@ -123,6 +136,17 @@ def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
                  if "O0" in res else "")
               + f"; XOR of CRCs 0x{res['O2']['xor']:08X} ({'ok' if ok else 'MISMATCH'}); host CPU: {cpu_model}; "
               f"nproc {os.cpu_count()}")
+    if "ref" in res:   # the reference itself is the baseline; the port's figures stay beside it
+        ref_ok = res["ref"]["xor"] == 0x600A585E
+        sample = (f"{frames} x {L}-B frames (xorshift64 seed 42, SURVEY §8d), the reference's own "
+                  f"src/ether_fcs.c compiled at its Makefile flags (-O0 -g -std=gnu99; oracle/_ref), one "
+                  f"ether_fcs call per frame on 1 host thread: {res['ref']['secs']:.2f} s; XOR of CRCs "
+                  f"0x{res['ref']['xor']:08X} ({'ok' if ref_ok else 'MISMATCH'}). Beside it, the oracle port: "
+                  + sample)
+        return {"value": round(res["ref"]["gibs"], 4), "unit": "GiB/s", "cores": 1, "kind": "reference",
+                "sample": sample, "value_port_O2": round(res["O2"]["gibs"], 4),
+                "value_port_O0": round(res["O0"]["gibs"], 4) if "O0" in res else None,
+                "value_port_16_threads": round(res["all"]["gibs"], 4)}
     return {"value": round(res["O2"]["gibs"], 4), "unit": "GiB/s", "cores": 1, "kind": "port",
             "sample": sample, "value_O0": round(res["O0"]["gibs"], 4) if "O0" in res else None,
             "value_16_threads": round(res["all"]["gibs"], 4)}

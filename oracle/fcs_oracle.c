@@ -165,6 +165,19 @@ double oracle_time_fixed(const uint8_t *base, size_t stride, uint32_t len, size_
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
 
+/* Wall-clock seconds of `n` calls fcs(base + i*stride, len) of an ether_fcs-shaped function: the
+ * reference's own compiled src/ether_fcs.c (oracle/_ref) for bench.py's cpu_baseline leg, called
+ * once per frame exactly as ether_send calls it (src/linux/ether.c:262). */
+typedef uint32_t (*fcs_fn)(const void *, size_t);
+double oracle_time_calls(fcs_fn fcs, const uint8_t *base, size_t stride, uint32_t len, size_t n, uint32_t *out)
+{
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (size_t i = 0; i < n; i++) out[i] = fcs(base + i * stride, len);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}
+
 /* SURVEY §8c dataset: xorshift64, one output byte per step; *state carries across calls. */
 void oracle_xorshift64_fill(uint8_t *buf, size_t n, uint64_t *state)
 {
