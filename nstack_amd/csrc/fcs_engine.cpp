@@ -104,7 +104,17 @@ struct DevState {
     uint64_t *one_flag = nullptr, *one_dflag = nullptr;
     uint64_t one_seq = 0;
     uint64_t one_cap = 0;
-    uint32_t one_seq32 = 0;   // single-frame kernel: sequence number in the result word's high half
+    // Single-frame kernel (drop-in ether_fcs, one-frame TX): a few independent lanes, each with its
+    // own stream and result word, so concurrent callers (nstack calls ether_fcs from its main,
+    // ingress, egress and timer threads) do not queue behind one another. A thread keeps its lane.
+    struct OneLane {
+        std::mutex mu;
+        hipStream_t st = nullptr;
+        uint64_t *flag = nullptr, *dflag = nullptr;   // mapped result word: (seq << 32) | FCS
+        uint32_t seq = 0;
+    };
+    static constexpr int kOneLanes = 4;   // HIP maps streams onto 4 hardware queues per process
+    OneLane one_lane[kOneLanes];
 };
 
 std::mutex g_mu;
@@ -579,9 +589,12 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
 }
 
 // One frame of at most kOneBytes through fcs_one_kernel: the frame rides in the kernel arguments
-// and the FCS comes back in the high-sequenced mapped word (one_flag[1]). Any host memory.
+// and the FCS comes back in the calling thread's lane's mapped result word. Any host memory.
 int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
-    std::lock_guard<std::mutex> lk(ds->one_mu);
+    static std::atomic<uint32_t> next_thread{0};
+    thread_local const uint32_t me = next_thread.fetch_add(1, std::memory_order_relaxed);
+    DevState::OneLane &L = ds->one_lane[me % DevState::kOneLanes];
+    std::lock_guard<std::mutex> lk(L.mu);
     int cur = 0;
     HIPTRY(hipGetDevice(&cur), "hipGetDevice");
     HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
@@ -589,35 +602,33 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
         int d;
         ~Restore() { hipSetDevice(d); }
     } restore{cur};
-    if (!ds->one_stream) {
-        HIPTRY(hipStreamCreateWithFlags(&ds->one_stream, hipStreamNonBlocking), "hipStreamCreate");
-        HIPTRY(hipHostMalloc(&ds->one_hout, 64, hipHostMallocMapped), "hipHostMalloc(result)");
-        HIPTRY(hipHostGetDevicePointer((void **)&ds->one_dout, ds->one_hout, 0), "hipHostGetDevicePointer(result)");
-        HIPTRY(hipHostMalloc(&ds->one_flag, 64, hipHostMallocMapped), "hipHostMalloc(flag)");
-        HIPTRY(hipHostGetDevicePointer((void **)&ds->one_dflag, ds->one_flag, 0), "hipHostGetDevicePointer(flag)");
-        ds->one_flag[0] = ds->one_flag[1] = 0;
+    if (!L.st) {
+        HIPTRY(hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking), "hipStreamCreate");
+        HIPTRY(hipHostMalloc(&L.flag, 64, hipHostMallocMapped), "hipHostMalloc(result word)");
+        HIPTRY(hipHostGetDevicePointer((void **)&L.dflag, L.flag, 0), "hipHostGetDevicePointer(result word)");
+        *L.flag = 0;
     }
     fcs::OneArgs a;
-    a.flag = ds->one_dflag + 1;   // word 0 is the staged path's completion signal
+    a.flag = L.dflag;
     a.blob = ds->d_one_blob;
-    if (++ds->one_seq32 == 0) ds->one_seq32 = 1;   // 0 never names a completion
-    a.seq = ds->one_seq32;
+    if (++L.seq == 0) L.seq = 1;   // 0 never names a completion
+    a.seq = L.seq;
     a.kinit = kinit_table()[bsize];
     uint8_t *win = reinterpret_cast<uint8_t *>(a.data);
     std::memset(win, 0, fcs::kOneBytes - bsize);
     if (bsize) std::memcpy(win + fcs::kOneBytes - bsize, data, bsize);
-    HIPTRY(fcs::launch_one(a, ds->one_stream), "launching the single-frame kernel");
+    HIPTRY(fcs::launch_one(a, L.st), "launching the single-frame kernel");
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1;; i++) {
-        const uint64_t v = __atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE);
+        const uint64_t v = __atomic_load_n(L.flag, __ATOMIC_ACQUIRE);
         if ((uint32_t)(v >> 32) == a.seq) {
             *crc = (uint32_t)v;
             return 0;
         }
         __builtin_ia32_pause();
         if ((i & 4095) == 0) {
-            const hipError_t q = hipStreamQuery(ds->one_stream);
-            if (q == hipSuccess && (uint32_t)(__atomic_load_n(ds->one_flag + 1, __ATOMIC_ACQUIRE) >> 32) != a.seq)
+            const hipError_t q = hipStreamQuery(L.st);
+            if (q == hipSuccess && (uint32_t)(__atomic_load_n(L.flag, __ATOMIC_ACQUIRE) >> 32) != a.seq)
                 return fail(EIO, "single-frame kernel finished without a result");
             if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "single-frame kernel");
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
@@ -961,6 +972,10 @@ void fcs_engine_fini(void) {
         if (ds->one_h) hipHostFree(ds->one_h);
         if (ds->one_hout) hipHostFree(ds->one_hout);
         if (ds->one_flag) hipHostFree(ds->one_flag);
+        for (DevState::OneLane &L : ds->one_lane) {
+            if (L.st) hipStreamDestroy(L.st);
+            if (L.flag) hipHostFree(L.flag);
+        }
         if (ds->d_blob) hipFree(ds->d_blob);
         if (ds->d_one_blob) hipFree(ds->d_one_blob);
         if (ds->d_kinit) hipFree(ds->d_kinit);
