@@ -32,7 +32,11 @@ namespace fcs {
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
-constexpr int kSlotsPerWg = kWgThreads / kGroup;   // 64 frame slots; LDS (145 KiB) -> 1 WG per CU
+// Frame slots (quarter-waves) per workgroup of NT threads; LDS (150 KiB) -> 1 WG per CU.
+template <int NT> constexpr int kSlotsPerWg = NT / kGroup;
+// fcs_kernel's thread count: small variable-length batches keep kWgThreads (every frame in flight
+// at once), fixed-length batches run kFixedWgThreads.
+template <bool VAR> constexpr int kBodyThreads = VAR ? kWgThreads : kFixedWgThreads;
 constexpr int kSingleMaskWords = 8;                // SINGLE variant: front-lane masks for words < 8
 #ifndef FCS_CHAINS
 #define FCS_CHAINS 2                               // independent chains per lane (2 or 4)
@@ -383,10 +387,11 @@ struct Lane {
 };
 
 // Stage the constant tables into LDS (once per workgroup; grids are persistent).
+template <int NT>
 __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
     const int tid = threadIdx.x;
     // data: 8192 x 16 B; each b128 store = 4 replicas of one entry
-    for (int i = tid; i < 8192; i += kWgThreads) {
+    for (int i = tid; i < 8192; i += NT) {
         const int h = i >> 12;            // 64 KiB half
         const int b = (i >> 4) & 255;     // entry
         const int odd = (i >> 3) & 1;     // +128 slot
@@ -398,7 +403,7 @@ __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
     }
     const uint32_t *src = p.blob + kBlobLane;
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
-    for (int i = tid; i < (int)(kBlobFlat - kBlobLane); i += kWgThreads) dst[i] = src[i];
+    for (int i = tid; i < (int)(kBlobFlat - kBlobLane); i += NT) dst[i] = src[i];
     __syncthreads();
 }
 
@@ -426,10 +431,10 @@ __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, u
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg};
+    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<kBodyThreads<VAR>>};
 
     typename Lane<VAR, TINY, SINGLE>::Pos A, B;
-    A.f = ((uint64_t)blk * kSlotsPerWg) + (threadIdx.x / kGroup);
+    A.f = ((uint64_t)blk * kSlotsPerWg<kBodyThreads<VAR>>) + (threadIdx.x / kGroup);
     A.k = 0;
     A.act = A.f < p.n;
     A.it = (SINGLE || A.act) ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
@@ -475,9 +480,9 @@ __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, u
 }
 
 template <bool VAR, bool TINY, bool SINGLE>
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_kernel(KParams p) {
+__global__ __launch_bounds__(kBodyThreads<VAR>, 1) void fcs_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    stage_tables(p, lds);
+    stage_tables<kBodyThreads<VAR>>(p, lds);
     init_bad(lds);
     fcs_body<VAR, TINY, SINGLE>(p, lds, blockIdx.x, gridDim.x);
     flush_bad(p, lds);
@@ -561,7 +566,7 @@ struct SingleLane {
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts2 = stamp();
         if (dbg != nullptr && (threadIdx.x & 63) == 0) {
-            const uint32_t wv = blockIdx.x * (kWgThreads / 64) + (threadIdx.x >> 6);
+            const uint32_t wv = blockIdx.x * (kFixedWgThreads / 64) + (threadIdx.x >> 6);
             atomicAdd((unsigned long long *)&dbg[wv * 4 + 0], (unsigned long long)(ts1 - ts0));
             atomicAdd((unsigned long long *)&dbg[wv * 4 + 1], (unsigned long long)(ts2 - ts0));
             atomicAdd((unsigned long long *)&dbg[wv * 4 + 2], 1ull);
@@ -578,9 +583,9 @@ __device__ __forceinline__ void issue_raw(uint64_t a, uint32_t r, Raw &c) {
     c.x6 = gload<uint32_t>(a + (r ? 96 : 92));   // 25th dword only matters when r != 0
 }
 
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
+__global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    stage_tables(p, lds);
+    stage_tables<kFixedWgThreads>(p, lds);
     init_bad(lds);
 
     const int lane = threadIdx.x & 63;
@@ -609,8 +614,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_single_kernel(KParams p) {
         S.x0 = (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
     }
 
-    const uint64_t Q = (uint64_t)gridDim.x * kSlotsPerWg;
-    const uint64_t f0 = (uint64_t)blockIdx.x * kSlotsPerWg + threadIdx.x / kGroup;
+    const uint64_t Q = (uint64_t)gridDim.x * kSlotsPerWg<kFixedWgThreads>;
+    const uint64_t f0 = (uint64_t)blockIdx.x * kSlotsPerWg<kFixedWgThreads> + threadIdx.x / kGroup;
     int rem = f0 < p.n ? (int)((p.n - 1 - f0) / Q) + 1 : 0;   // items left for this frame slot
     uint64_t end = p.base + f0 * p.stride + p.flen;
     const uint64_t dend = Q * p.stride;
@@ -798,7 +803,7 @@ __device__ __forceinline__ void unit_finish(const KParams &p, const uint8_t *lds
 template <bool TINY>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    stage_tables(p, lds);
+    stage_tables<kWgThreads>(p, lds);
     init_bad(lds);
 
     const int lane = threadIdx.x & 63;
@@ -1318,7 +1323,7 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
     const bool single = !var && p.fseg == 1 && p.zmax <= 4 * kSingleMaskWords;
 #endif
 #define FCS_LAUNCH(V, T, S) \
-    hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kWgThreads), 0, st, p)
+    hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kBodyThreads<V>), 0, st, p)
     if (var) {
         // windowed: throughput form (64-frame windows per wave, chunks dealt flat to the lanes);
         // otherwise one quarter-wave per frame, every frame in flight at once (small batches)
@@ -1345,7 +1350,7 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #ifdef FCS_OLD_SINGLE   // measurement-only build: generic kernel's SINGLE instantiation
         FCS_LAUNCH(false, false, true);
 #else
-        hipLaunchKernelGGL(fcs_single_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
+        hipLaunchKernelGGL(fcs_single_kernel, dim3(grid), dim3(kFixedWgThreads), 0, st, p);
 #endif
     } else {
         FCS_LAUNCH(false, false, false);

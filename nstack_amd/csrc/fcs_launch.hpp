@@ -22,7 +22,20 @@ struct KParams {
     unsigned long long *bad;//   ... and *bad += number of frames that do not (else both null)
 };
 
-constexpr int kWgThreads = 1024;
+// Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). Fixed-length
+// kernels run 8 waves per CU: 2 per SIMD beat 4 per SIMD by 1-7 % on 1518-B and 9000-B frames
+// (tools/ab.py); 4, 6, 12 and 14 waves were slower or equal. The variable-length
+// kernels keep 16 waves (the flat kernel on IMIX: 4358 vs 3728 GB/s at 8 waves).
+#ifndef FCS_WG_THREADS   // measurement-only overrides (tools/variants.sh)
+#define FCS_WG_THREADS 1024
+#endif
+#ifndef FCS_FIXED_WG_THREADS
+#define FCS_FIXED_WG_THREADS 512
+#endif
+constexpr int kWgThreads = FCS_WG_THREADS;             // variable-length kernels
+constexpr int kFixedWgThreads = FCS_FIXED_WG_THREADS;  // fixed-length kernels
+static_assert(kWgThreads % 64 == 0 && kWgThreads <= 1024, "workgroup = 1..16 waves (LDS scratch holds 16)");
+static_assert(kFixedWgThreads % 64 == 0 && kFixedWgThreads <= 1024, "workgroup = 1..16 waves");
 
 // Single-frame kernel of the drop-in ether_fcs (fcs_one_kernel): the frame travels inside the
 // kernel arguments, right-aligned in a 1536-byte window (zeros before it), one wave of 64 lanes
