@@ -614,9 +614,22 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
         S.x0 = (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
     }
 
+#ifdef FCS_BLOCKED   // measurement-only build: each workgroup walks its own contiguous frame range
+    const uint64_t Q = (uint64_t)kSlotsPerWg<kFixedWgThreads>;
+    const uint64_t per = ((p.n + Q - 1) / Q + gridDim.x - 1) / gridDim.x;   // items per workgroup
+    const uint64_t f0 = (uint64_t)blockIdx.x * per * Q + threadIdx.x / kGroup;
+    const uint64_t lim = (uint64_t)(blockIdx.x + 1) * per * Q < p.n ? (uint64_t)(blockIdx.x + 1) * per * Q : p.n;
+    int rem = f0 < lim ? (int)((lim - 1 - f0) / Q) + 1 : 0;
+#else
+#ifdef FCS_XCD   // measurement-only build: neighbouring frame slots on one XCD (round-robin dispatch)
+    const uint32_t wg = (gridDim.x & 7) ? blockIdx.x : (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+#else
+    const uint32_t wg = blockIdx.x;
+#endif
     const uint64_t Q = (uint64_t)gridDim.x * kSlotsPerWg<kFixedWgThreads>;
-    const uint64_t f0 = (uint64_t)blockIdx.x * kSlotsPerWg<kFixedWgThreads> + threadIdx.x / kGroup;
+    const uint64_t f0 = (uint64_t)wg * kSlotsPerWg<kFixedWgThreads> + threadIdx.x / kGroup;
     int rem = f0 < p.n ? (int)((p.n - 1 - f0) / Q) + 1 : 0;   // items left for this frame slot
+#endif
     uint64_t end = p.base + f0 * p.stride + p.flen;
     const uint64_t dend = Q * p.stride;
     uint64_t fi = f0;   // frame index of the item being processed
