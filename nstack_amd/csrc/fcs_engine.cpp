@@ -197,9 +197,9 @@ uint32_t mask_bound(uint32_t len) {
     return fcs::kChunkBytes * ((l0 + fcs::kChunkBytes - 1) / fcs::kChunkBytes) - l0;
 }
 
-int grid_for(const DevState *ds, uint64_t n, bool var) {
+int grid_for(const DevState *ds, uint64_t n, int threads) {
     // frame slots (quarter-waves) per workgroup of the kernel launch_fcs picks
-    const uint64_t slots = (var ? fcs::kWgThreads : fcs::kFixedWgThreads) / fcs::kGroup;
+    const uint64_t slots = (uint64_t)threads / fcs::kGroup;
     const uint64_t want = (n + slots - 1) / slots;
 #ifdef FCS_GRID_CUS   // measurement-only build: run the persistent grid on fewer CUs
     const uint64_t cus = std::min<uint64_t>((uint64_t)ds->cus, FCS_GRID_CUS);
@@ -232,7 +232,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
     p.dbg = g_dbg;
-    HIPTRY(fcs::launch_fcs(false, false, p, grid_for(ds, n, false), st), "launching fcs_kernel<fixed>");
+    HIPTRY(fcs::launch_fcs(false, false, p, grid_for(ds, n, fcs::fixed_threads(p)), st), "launching fcs_kernel<fixed>");
     return 0;
 }
 
@@ -254,7 +254,7 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     p.zmax = fcs::kChunkBytes;
     p.blob = ds->d_blob;
     const bool windowed = n > g_var_threshold.load(std::memory_order_relaxed);
-    HIPTRY(fcs::launch_fcs(true, windowed, p, grid_for(ds, n, true), st), "launching fcs_kernel<var>");
+    HIPTRY(fcs::launch_fcs(true, windowed, p, grid_for(ds, n, fcs::kWgThreads), st), "launching fcs_kernel<var>");
     return 0;
 }
 

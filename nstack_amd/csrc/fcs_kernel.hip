@@ -34,10 +34,8 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Frame slots (quarter-waves) per workgroup of NT threads; LDS (150 KiB) -> 1 WG per CU.
 template <int NT> constexpr int kSlotsPerWg = NT / kGroup;
-// fcs_kernel's thread count: small variable-length batches keep kWgThreads (every frame in flight
-// at once), fixed-length batches run kFixedWgThreads.
-template <bool VAR> constexpr int kBodyThreads = VAR ? kWgThreads : kFixedWgThreads;
-constexpr int kSingleMaskWords = 8;                // SINGLE variant: front-lane masks for words < 8
+
+constexpr int kSingleMaskWords = kSingleMaxLead / 4;   // SINGLE variant: front-lane masks for words < 8
 #ifndef FCS_CHAINS
 #define FCS_CHAINS 2                               // independent chains per lane (2 or 4)
 #endif
@@ -426,15 +424,15 @@ __device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds
 }
 
 // The quarter-wave-per-frame loop of one workgroup (`blk` of `nblk`), tables already in LDS.
-template <bool VAR, bool TINY, bool SINGLE>
+template <bool VAR, bool TINY, bool SINGLE, int NT>
 __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, uint32_t blk, uint32_t nblk) {
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<kBodyThreads<VAR>>};
+    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<NT>};
 
     typename Lane<VAR, TINY, SINGLE>::Pos A, B;
-    A.f = ((uint64_t)blk * kSlotsPerWg<kBodyThreads<VAR>>) + (threadIdx.x / kGroup);
+    A.f = ((uint64_t)blk * kSlotsPerWg<NT>) + (threadIdx.x / kGroup);
     A.k = 0;
     A.act = A.f < p.n;
     A.it = (SINGLE || A.act) ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
@@ -479,12 +477,12 @@ __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, u
 #endif
 }
 
-template <bool VAR, bool TINY, bool SINGLE>
-__global__ __launch_bounds__(kBodyThreads<VAR>, 1) void fcs_kernel(KParams p) {
+template <bool VAR, bool TINY, bool SINGLE, int NT>
+__global__ __launch_bounds__(NT, 1) void fcs_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    stage_tables<kBodyThreads<VAR>>(p, lds);
+    stage_tables<NT>(p, lds);
     init_bad(lds);
-    fcs_body<VAR, TINY, SINGLE>(p, lds, blockIdx.x, gridDim.x);
+    fcs_body<VAR, TINY, SINGLE, NT>(p, lds, blockIdx.x, gridDim.x);
     flush_bad(p, lds);
 }
 
@@ -1329,14 +1327,11 @@ __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t s
 // ---- host-side launchers (the engine TU never names the kernels) ----
 hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
-    const bool tiny = p.hi4 - p.lo4 < 2 * kChunkBytes;
-#ifdef FCS_NO_SINGLE   // measurement-only build
-    const bool single = false;
-#else
-    const bool single = !var && p.fseg == 1 && p.zmax <= 4 * kSingleMaskWords;
-#endif
+    const bool tiny = fixed_tiny(p);
+    const bool single = !var && fixed_single(p);
+    // fixed_threads(p) (fcs_launch.hpp) picks the workgroup size; the host sized the grid with it
 #define FCS_LAUNCH(V, T, S) \
-    hipLaunchKernelGGL((fcs_kernel<V, T, S>), dim3(grid), dim3(kBodyThreads<V>), 0, st, p)
+    hipLaunchKernelGGL((fcs_kernel<V, T, S, kWgThreads>), dim3(grid), dim3(kWgThreads), 0, st, p)
     if (var) {
         // windowed: throughput form (64-frame windows per wave, chunks dealt flat to the lanes);
         // otherwise one quarter-wave per frame, every frame in flight at once (small batches)
@@ -1365,6 +1360,8 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #else
         hipLaunchKernelGGL(fcs_single_kernel, dim3(grid), dim3(kFixedWgThreads), 0, st, p);
 #endif
+    } else if (fixed_threads(p) == kFixedWgThreads) {
+        hipLaunchKernelGGL((fcs_kernel<false, false, false, kFixedWgThreads>), dim3(grid), dim3(kFixedWgThreads), 0, st, p);
     } else {
         FCS_LAUNCH(false, false, false);
     }

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "fcs_tables.hpp"
+
 namespace fcs {
 
 struct KParams {
@@ -22,10 +24,12 @@ struct KParams {
     unsigned long long *bad;//   ... and *bad += number of frames that do not (else both null)
 };
 
-// Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). Fixed-length
-// kernels run 8 waves per CU: 2 per SIMD beat 4 per SIMD by 1-7 % on 1518-B and 9000-B frames
-// (tools/ab.py); 4, 6, 12 and 14 waves were slower or equal. The variable-length
-// kernels keep 16 waves (the flat kernel on IMIX: 4358 vs 3728 GB/s at 8 waves).
+// Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). The 1504..1536-B
+// single-segment kernel and frames of kWideSegs or more segments run 8 waves per CU: 2 per SIMD
+// beat 4 per SIMD by 1-7 % on 1518-B and 9000-B frames (tools/ab.py; 4, 6, 12 and
+// 14 waves were slower or equal). The generic kernel on 1-2 segments (64..1500 B, 1540 B) loses
+// 8-16 % at 8 waves and keeps 16 (3000 B: equal), as do the variable-length kernels (the flat
+// kernel on IMIX: 4358 vs 3728 GB/s at 8 waves).
 #ifndef FCS_WG_THREADS   // measurement-only overrides (tools/variants.sh)
 #define FCS_WG_THREADS 1024
 #endif
@@ -36,6 +40,8 @@ constexpr int kWgThreads = FCS_WG_THREADS;             // variable-length kernel
 constexpr int kFixedWgThreads = FCS_FIXED_WG_THREADS;  // fixed-length kernels
 static_assert(kWgThreads % 64 == 0 && kWgThreads <= 1024, "workgroup = 1..16 waves (LDS scratch holds 16)");
 static_assert(kFixedWgThreads % 64 == 0 && kFixedWgThreads <= 1024, "workgroup = 1..16 waves");
+constexpr uint32_t kWideSegs = 5;          // fixed frames of >= 5 x 1536 B: 8 waves per CU
+constexpr uint32_t kSingleMaxLead = 32;    // fcs_single_kernel: <= 32 leading bytes to mask
 
 // Single-frame kernel of the drop-in ether_fcs (fcs_one_kernel): the frame travels inside the
 // kernel arguments, right-aligned in a 1536-byte window (zeros before it), one wave of 64 lanes
@@ -86,6 +92,19 @@ struct TxSmallArgs {
     uint32_t kinit[kTxSmallMax];
 };
 
+
+// Fixed length: the launcher's kernel choice, shared with the host's grid sizing.
+inline bool fixed_tiny(const KParams &p) { return p.hi4 - p.lo4 < 2 * (uint64_t)kChunkBytes; }
+inline bool fixed_single(const KParams &p) {
+#ifdef FCS_NO_SINGLE   // measurement-only build
+    return false;
+#else
+    return p.fseg == 1 && p.zmax <= kSingleMaxLead;
+#endif
+}
+inline int fixed_threads(const KParams &p) {
+    return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;
+}
 
 hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st);
 hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st);
