@@ -60,11 +60,40 @@ __device__ __forceinline__ uint32_t lds_rd(const uint8_t *lds, uint32_t byte_add
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
 
+// Per-lane table bases for step4. Default: 32 replicas (replica = lane & 31), base0 = r*4 (T3 at
+// +0, T2 at +128), base1 = 0x10000 | r*4 (T1, T0). FCS_LDS16 (measurement-only): one 256-B row per
+// byte value e holding table slot b (the table of word byte b, T_{3-b}) x 16 replicas at
+// e*256 + b*64 + (lane & 15)*4; lanes 16-31 of each half-wave rotate the chain word by 16 bits, so
+// their lookup k uses slot k ^ 2 and the 32 lanes of one LDS pass hit 32 distinct banks.
+__device__ __forceinline__ void table_bases(int lane, uint32_t &base0, uint32_t &base1) {
+#ifdef FCS_LDS16
+    const uint32_t r = (uint32_t)(lane & 15) * 4u, G = (lane & 16) ? 2u : 0u;
+    base0 = r + G * 64u;
+    base1 = r + (2u - G) * 64u;
+#else
+    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
+    base0 = r4;
+    base1 = 0x10000u | r4;
+#endif
+}
+
 // One 4-byte step with the next word folded in: returns A_4(x) ^ wn, where
 // A_4(x) = T3[x.b0] ^ T2[x.b1] ^ T1[x.b2] ^ T0[x.b3] -> 4 v_perm + 4 ds_read + 2 v_bitop3.
 // base0 = r*4 (half 0: T3 at +0, T2 at +128), base1 = 0x10000 | r*4 (half 1: T1, T0).
 __device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32_t wn, uint32_t base0,
                                           uint32_t base1) {
+#ifdef FCS_LDS16   // measurement-only build: 64 KiB table set (see table_bases)
+    const uint32_t xr = __builtin_amdgcn_perm(x, x, (threadIdx.x & 16) ? 0x01000302u : 0x03020100u);
+    const uint32_t a0 = __builtin_amdgcn_perm(xr, base0, 0x0C0C0400u);
+    const uint32_t a1 = __builtin_amdgcn_perm(xr, base0, 0x0C0C0500u);
+    const uint32_t a2 = __builtin_amdgcn_perm(xr, base1, 0x0C0C0600u);
+    const uint32_t a3 = __builtin_amdgcn_perm(xr, base1, 0x0C0C0700u);
+    const uint32_t t3 = lds_rd(lds, a0);
+    const uint32_t t2 = lds_rd(lds, a1 + 64);
+    const uint32_t t1 = lds_rd(lds, a2);
+    const uint32_t t0 = lds_rd(lds, a3 + 64);
+    return xor3(xor3(t3, t2, t1), t0, wn);
+#else
     const uint32_t a0 = __builtin_amdgcn_perm(x, base0, 0x0C020400u);
     const uint32_t a1 = __builtin_amdgcn_perm(x, base0, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, base1, 0x0C020600u);
@@ -77,6 +106,7 @@ __device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32
     const uint32_t t1 = lds_rd(lds, a2);
     const uint32_t t0 = lds_rd(lds, a3 + 128);
     return xor3(xor3(t3, t2, t1), t0, wn);
+#endif
 #endif
 }
 
@@ -389,6 +419,13 @@ template <int NT>
 __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
     const int tid = threadIdx.x;
     // data: 8192 x 16 B; each b128 store = 4 replicas of one entry
+#ifdef FCS_LDS16
+    for (int i = tid; i < 4096; i += NT) {   // row e = i >> 4; 16-B store q = i & 15 -> slot q >> 2
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
+    }
+#else
     for (int i = tid; i < 8192; i += NT) {
         const int h = i >> 12;            // 64 KiB half
         const int b = (i >> 4) & 255;     // entry
@@ -399,6 +436,7 @@ __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
     }
+#endif
     const uint32_t *src = p.blob + kBlobLane;
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
     for (int i = tid; i < (int)(kBlobFlat - kBlobLane); i += NT) dst[i] = src[i];
@@ -409,6 +447,13 @@ __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
 // tables C_c in place of the per-lane tables.
 __device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds) {
     const int tid = threadIdx.x;
+#ifdef FCS_LDS16
+    for (int i = tid; i < 4096; i += kWgThreads) {
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
+    }
+#else
     for (int i = tid; i < 8192; i += kWgThreads) {
         const int h = i >> 12, b = (i >> 4) & 255, odd = (i >> 3) & 1;
         const int k = h == 0 ? (odd ? 2 : 3) : (odd ? 0 : 1);
@@ -416,6 +461,7 @@ __device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
     }
+#endif
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsJump);
     for (int i = tid; i < (int)(kBlobFlat - kBlobJump); i += kWgThreads) dst[i] = p.blob[kBlobJump + i];
     uint32_t *fl = reinterpret_cast<uint32_t *>(lds + kLdsFlat);
@@ -429,7 +475,9 @@ __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, u
     const int lane = threadIdx.x & 63;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    Lane<VAR, TINY, SINGLE> L{p, lds, j, r4, 0x10000u | r4, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<NT>};
+    uint32_t tb0, tb1;
+    table_bases(lane, tb0, tb1);
+    Lane<VAR, TINY, SINGLE> L{p, lds, j, tb0, tb1, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<NT>};
 
     typename Lane<VAR, TINY, SINGLE>::Pos A, B;
     A.f = ((uint64_t)blk * kSlotsPerWg<NT>) + (threadIdx.x / kGroup);
@@ -594,8 +642,7 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
     S.kp = &p;
     S.lds = lds;
     S.j = j;
-    S.base0 = r4;
-    S.base1 = 0x10000u | r4;
+    table_bases(lane, S.base0, S.base1);
     S.lanebase = kLdsLane | r4;
     S.zmax = p.zmax;
     const uint32_t loff = (uint32_t)kChunkBytes * (uint32_t)(j + 1);   // chunk start = end - loff
@@ -821,7 +868,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
     const int wave = threadIdx.x >> 6;
     const int j = lane & (kGroup - 1);
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    const uint32_t base0 = r4, base1 = 0x10000u | r4, lanebase = kLdsLane | r4;
+    const uint32_t lanebase = kLdsLane | r4;
+    uint32_t base0, base1;
+    table_bases(lane, base0, base1);
     uint8_t *lists = lds + kLdsWave + wave * kLdsWaveBytes;   // medium | full | multi | small, 64 each
     const uint64_t GW = (uint64_t)gridDim.x * (kWgThreads / 64);
 
@@ -925,8 +974,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
     const int j = lane & (kGroup - 1);
-    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    const uint32_t base0 = r4, base1 = 0x10000u | r4;
+    uint32_t base0, base1;
+    table_bases(lane, base0, base1);
     uint32_t *acc = reinterpret_cast<uint32_t *>(lds + kLdsWave + wave * kLdsWaveBytes);   // 64 frames
     uint8_t *mark = lds + kLdsFlatMark + wave * 64;
     uint8_t *list = lds + kLdsFlatList + wave * 64;
