@@ -216,6 +216,15 @@ uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
 // 16384 = 4 frames x 16 waves x 256 CUs: one item per quarter-wave on a full chip.
 std::atomic<uint64_t> g_var_threshold{16384};
 
+// Fixed-length batches of frames up to this length (and more than g_var_threshold frames) take the
+// flat variable-length kernel: a 64-B frame then costs one lane instead of a quarter-wave. Measured
+// against the quarter-wave kernel (tools/ab.py): 64 B 11x, 576 B 2.1x, 1300 B
+// +6.5 %; 1504..1536 B stay on the single kernel (the flat kernel is 9 % slower at 1518 B).
+#ifndef FCS_FIXED_FLAT_MAX   // measurement-only override (0 = never)
+#define FCS_FIXED_FLAT_MAX 1503
+#endif
+constexpr uint32_t kFixedFlatMaxLen = FCS_FIXED_FLAT_MAX;
+
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
                  uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
     fcs::KParams p{};
@@ -232,6 +241,13 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
     p.dbg = g_dbg;
+    if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed)) {
+        // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame
+        // instead of a 16-lane quarter-wave (len == null tells it the length is p.flen)
+        p.zmax = fcs::kChunkBytes;
+        HIPTRY(fcs::launch_fcs(true, true, p, grid_for(ds, n, fcs::kWgThreads), st), "launching fcs_flat_kernel<fixed>");
+        return 0;
+    }
     HIPTRY(fcs::launch_fcs(false, false, p, grid_for(ds, n, fcs::fixed_threads(p)), st), "launching fcs_kernel<fixed>");
     return 0;
 }

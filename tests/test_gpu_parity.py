@@ -414,3 +414,17 @@ def test_var_batches_fuzz(dev, batch, kernel):
             assert got[i] == zlib.crc32(arena[o:o + L].tobytes()), (kernel, L, o)
     finally:
         na.set_var_threshold(old)
+
+
+# Fixed-length batches above the small-batch threshold with frames of at most 1503 B take the flat
+# kernel (len array absent: the length is the batch's); lengths and strides the route covers.
+@pytest.mark.parametrize("L,stride", [(0, 4), (1, 1), (13, 17), (60, 60), (64, 64), (70, 72),
+                                      (96, 96), (97, 101), (576, 576), (1000, 1003), (1503, 1503)])
+def test_fixed_short_frames_flat_route(dev, oracle, L, stride):
+    n = 20000   # > the 16384-frame small-batch threshold
+    nbytes = (n - 1) * stride + L + 3
+    host = np.random.default_rng(L * 7919 + stride).integers(0, 256, nbytes, dtype=np.uint8)
+    base = to_dev(host, dev)
+    got = run_fixed(dev, base[3:], stride, L, n)   # odd base alignment
+    exp = oracle_fixed(oracle, host[3:].copy(), stride, L, n)
+    assert np.array_equal(got, exp)
