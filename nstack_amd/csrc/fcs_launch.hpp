@@ -25,7 +25,7 @@ struct KParams {
 };
 
 // Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). The 1504..1536-B
-// single-segment kernel and frames of kWideSegs or more segments run 8 waves per CU: 2 per SIMD
+// single-segment kernel and frames of kWideSegs (3) or more segments run 8 waves per CU: 2 per SIMD
 // beat 4 per SIMD by 1-7 % on 1518-B and 9000-B frames (tools/ab.py; 4, 6, 12 and
 // 14 waves were slower or equal). The generic kernel on 1-2 segments (64..1500 B, 1540 B) loses
 // 8-16 % at 8 waves and keeps 16 (3000 B: equal), as do the variable-length kernels (the flat
@@ -40,7 +40,10 @@ constexpr int kWgThreads = FCS_WG_THREADS;             // variable-length kernel
 constexpr int kFixedWgThreads = FCS_FIXED_WG_THREADS;  // fixed-length kernels
 static_assert(kWgThreads % 64 == 0 && kWgThreads <= 1024, "workgroup = 1..16 waves (LDS scratch holds 16)");
 static_assert(kFixedWgThreads % 64 == 0 && kFixedWgThreads <= 1024, "workgroup = 1..16 waves");
-constexpr uint32_t kWideSegs = 5;          // fixed frames of >= 5 x 1536 B: 8 waves per CU
+#ifndef FCS_WIDE_SEGS   // measurement-only override
+#define FCS_WIDE_SEGS 3
+#endif
+constexpr uint32_t kWideSegs = FCS_WIDE_SEGS;   // fixed frames of >= 3 segments (> 3072 B): 8 waves per CU
 constexpr uint32_t kSingleMaxLead = 32;    // fcs_single_kernel: <= 32 leading bytes to mask
 
 // Single-frame kernel of the drop-in ether_fcs (fcs_one_kernel): the frame travels inside the
