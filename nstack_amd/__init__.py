@@ -260,7 +260,7 @@ def timed_fixed_dev(base, stride: int, length: int, n: int, out, stream=None, re
 
 def tables_blob():
     import numpy as np
-    buf = np.zeros(8192, dtype=np.uint32)
+    buf = np.zeros(16384, dtype=np.uint32)
     n = _check(load().fcs_tables_blob(buf.ctypes.data, buf.size), "fcs_tables_blob")
     return buf[:n].copy()
 

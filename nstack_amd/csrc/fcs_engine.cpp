@@ -248,6 +248,8 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         HIPTRY(fcs::launch_fcs(true, true, p, grid_for(ds, n, fcs::kWgThreads), st), "launching fcs_flat_kernel<fixed>");
         return 0;
     }
+    if (fcs::fixed_dma(p))   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
+        p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
     HIPTRY(fcs::launch_fcs(false, false, p, grid_for(ds, n, fcs::fixed_threads(p)), st), "launching fcs_kernel<fixed>");
     return 0;
 }

@@ -141,6 +141,17 @@ __device__ __forceinline__ uint32_t uniform_shift(const uint8_t *lds, uint32_t s
     return xor9(r, extra);
 }
 
+// uniform_shift with the table region as a value (an unrolled loop's index).
+__device__ __forceinline__ uint32_t uniform_shift_at(const uint8_t *lds, uint32_t region, uint32_t s, uint32_t extra) {
+    uint32_t r[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        r[t] = lds_rd(lds, ((sh & 0x3Cu) | region) + t * 64);
+    }
+    return xor9(r, extra);
+}
+
 // XOR over each 16-lane row (one frame); every lane of the row ends with the row's XOR.
 __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
@@ -185,27 +196,32 @@ constexpr uint32_t kResidue = 0x2144DF1Cu;
 // the FCS over the whole frame equals the residue; non-matching frames are counted in the wave's
 // LDS slot (lane 0 only touches it) and added to *bad once per wave at kernel exit (flush_bad), so
 // an all-bad batch costs no atomics on the data path. Both outputs may be requested together.
+// BAD: LDS byte offset of the per-wave counters (kLdsBad; the LDS-DMA kernel keeps them elsewhere).
+template <uint32_t BAD = kLdsBad>
 __device__ __forceinline__ uint64_t *wave_bad(const uint8_t *lds) {   // the kernels' own __shared__ array
-    return reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(lds) + kLdsBad) + (threadIdx.x >> 6);
+    return reinterpret_cast<uint64_t *>(const_cast<uint8_t *>(lds) + BAD) + (threadIdx.x >> 6);
 }
 
+template <uint32_t BAD = kLdsBad>
 __device__ __forceinline__ void emit(const KParams &p, const uint8_t *lds, bool st, uint64_t i, uint32_t fcs) {
     if (p.out != nullptr && st) p.out[i] = fcs;
     if (p.ok != nullptr) {
         const bool good = fcs == kResidue;
         if (st) p.ok[i] = good ? 1 : 0;
         const uint64_t m = __ballot(st && !good);
-        if (m != 0 && (threadIdx.x & 63) == 0) *wave_bad(lds) += (uint64_t)__popcll(m);
+        if (m != 0 && (threadIdx.x & 63) == 0) *wave_bad<BAD>(lds) += (uint64_t)__popcll(m);
     }
 }
 
+template <uint32_t BAD = kLdsBad>
 __device__ __forceinline__ void init_bad(const uint8_t *lds) {
-    if ((threadIdx.x & 63) == 0) *wave_bad(lds) = 0;
+    if ((threadIdx.x & 63) == 0) *wave_bad<BAD>(lds) = 0;
 }
 
+template <uint32_t BAD = kLdsBad>
 __device__ __forceinline__ void flush_bad(const KParams &p, const uint8_t *lds) {
     if (p.ok != nullptr && (threadIdx.x & 63) == 0) {
-        const uint64_t b = *wave_bad(lds);
+        const uint64_t b = *wave_bad<BAD>(lds);
         if (b) atomicAdd(p.bad, (unsigned long long)b);
     }
 }
@@ -724,6 +740,171 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
     flush_bad(p, lds);
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Fixed length, one segment, frames staged through LDS by DMA (fcs_dma_kernel; host-selected for
+// kDmaMinLen..kDmaCover bytes, e.g. the 1518-B benchmark frames, when four consecutive frames fit
+// a 6 KiB slot: fixed_dma()).
+// A wave's item is four consecutive frames, as in fcs_single_kernel. The wave copies the item's
+// bytes into its own 6 KiB LDS slot with six global_load_lds_dwordx4 (each 1 KiB contiguous:
+// coalesced rows, no VGPR destination, non-temporal since every line is read exactly once), then
+// lane c of each frame reads its 96-byte window [E - e_c - 96, E - e_c) from the slot (25 dwords,
+// realigned with v_alignbyte as before; the window offsets e_c = dma_end_off(c) put one frame's 16
+// windows on 16 distinct banks) and runs the same two slice-by-4 chains, A_48 merge, lane shift
+// A_{e_c} and row XOR as the other fixed kernels. One slot per wave: the next item's DMA is issued
+// as soon as this item's words are in registers, so it lands while the CRC work runs.
+// LDS: the 64 KiB conflict-free table set (one 256-B row per byte value: 4 tables x 16 replicas,
+// step4_l16), the lane tables, A_48, INV and the per-wave slots.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kDmaLds16 = 0;                         // 65536: T3..T0 x 16 replicas
+constexpr uint32_t kDmaLane = 65536;                      // 16384: A_{e_c}, slot = lane & 31
+#ifndef FCS_DMA_CHAINS   // independent chains per lane window (2, 3, 4 or 6; measurement override)
+#define FCS_DMA_CHAINS 2
+#endif
+constexpr int kDmaChains = FCS_DMA_CHAINS;
+constexpr int kDmaChainWords = kChunkWords / kDmaChains;
+static_assert(kChunkWords % kDmaChains == 0 && kDmaChainWords % 2 == 0, "chains of an even word count");
+constexpr uint32_t kDmaMerge = kDmaLane + 16384;          // (kDmaChains - 1) x 512: A_{4 CL m}
+constexpr uint32_t kDmaInv = kDmaMerge + 512 * (kDmaChains - 1);   // 384
+constexpr uint32_t kDmaBad = kDmaInv + 384;               // 16 x 8
+constexpr uint32_t kDmaRing = kDmaBad + 128 + 64;         // 64-B pad: front windows may start before a slot
+constexpr uint32_t kDmaLdsBytes = kDmaRing + (kDmaWgThreads / 64) * kDmaItemBytes + 64;
+static_assert(kDmaRing % 16 == 0, "slots are 16-B aligned");
+static_assert(kDmaLdsBytes <= 163840, "LDS per CU");
+#ifndef FCS_DMA_AUX   // cache policy of the slot DMA (2 = nt; measurement-only override)
+#define FCS_DMA_AUX 2
+#endif
+
+// One slice-by-4 step against the 64 KiB table set: T_{3-s} lives in slot s of each 256-B row
+// (row = byte value, 16 replicas per slot, replica = lane & 15). ds_read_b32 banks are the dword
+// address mod 32, so slots s and s ^ 1 sit on opposite bank halves: lanes 16-31 of each 32-lane
+// group take the bytes in the order 1, 0, 3, 2 (rot) and look byte k ^ 1 up in slot k ^ 1, while
+// lanes 0-15 look byte k up in slot k; every lookup of a 32-lane group hits 32 distinct banks.
+// B[k] = replica * 4 + 64 * (k ^ (lane >> 4 & 1)): the per-lane slot rides in the v_perm base.
+__device__ __forceinline__ uint32_t step4_l16(const uint8_t *lds, uint32_t x, uint32_t wn, const uint32_t (&B)[4],
+                                              uint32_t rot) {
+    const uint32_t xr = __builtin_amdgcn_perm(x, x, rot);
+    const uint32_t t3 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[0], 0x0C0C0400u));
+    const uint32_t t2 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[1], 0x0C0C0500u));
+    const uint32_t t1 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[2], 0x0C0C0600u));
+    const uint32_t t0 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[3], 0x0C0C0700u));
+    return xor3(xor3(t3, t2, t1), t0, wn);
+}
+
+__device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int lane) {
+    typedef __attribute__((address_space(3))) void lds_void;
+#pragma unroll
+    for (int i = 0; i < (int)(kDmaItemBytes / 1024); i++)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 1024 * i + 16 * lane),
+                                         (lds_void *)(slot + 1024 * i), 16, 0, FCS_DMA_AUX);
+}
+
+__global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
+    const int tid = threadIdx.x;
+    // ---- tables: LDS16 slice tables, lane tables A_{e_c}, A_48, INV ----
+    for (int i = tid; i < 4096; i += kDmaWgThreads) {   // row e = i >> 4; 16-B store q = i & 15 -> slot q >> 2
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + kDmaLds16 + (uint32_t)i * 16) = vv;
+    }
+    for (int i = tid; i < 4096; i += kDmaWgThreads)
+        reinterpret_cast<uint32_t *>(lds + kDmaLane)[i] = p.blob[kBlobLaneDma + i];
+    for (int i = tid; i < 128 * (kDmaChains - 1); i += kDmaWgThreads)   // merge table m = A_{4 CL (m + 1)}
+        reinterpret_cast<uint32_t *>(lds + kDmaMerge)[i] =
+            p.blob[kBlobMerge + ((i >> 7) + 1) * (kDmaChainWords / 2) * 128 - 128 + (i & 127)];
+    for (int i = tid; i < kChunkBytes; i += kDmaWgThreads) reinterpret_cast<uint32_t *>(lds + kDmaInv)[i] = p.blob[kBlobInv + i];
+    init_bad<kDmaBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const int c = lane & (kGroup - 1);     // chunk index back from the frame end
+    const int g = lane >> 4;               // frame of the item
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
+    const uint32_t jl = (uint32_t)(lane >> 4) & 1u;
+    const uint32_t B[4] = {(uint32_t)(lane & 15) * 4u + 64u * (0u ^ jl), (uint32_t)(lane & 15) * 4u + 64u * (1u ^ jl),
+                           (uint32_t)(lane & 15) * 4u + 64u * (2u ^ jl), (uint32_t)(lane & 15) * 4u + 64u * (3u ^ jl)};
+    const uint32_t rot = jl ? 0x02030001u : 0x03020100u;
+    const uint32_t lanebase = kDmaLane | ((uint32_t)(lane & 31) * 4u);
+
+    // loop invariants: window offset within the item, front masks, INV start of the front lane
+    const uint32_t ec = dma_end_off(c);
+    const int64_t klane = (int64_t)g * (int64_t)p.stride + (int64_t)p.flen - (int64_t)ec - kChunkBytes;
+    const int zc = (c == kGroup - 1) ? (int)(kDmaCover - p.flen) : (dma_short_lane(c) ? 4 : 0);
+    uint32_t m[kSingleMaskWords];
+#pragma unroll
+    for (int i = 0; i < kSingleMaskWords; i++) {
+        int t = zc - 4 * i;
+        t = t < 0 ? 0 : (t > 4 ? 4 : t);
+        m[i] = (uint32_t)(0xFFFFFFFFull << (8 * t));
+    }
+    const uint32_t x0 = (c == kGroup - 1) ? lds_rd(lds, kDmaInv + 4u * (uint32_t)zc) : 0u;
+
+    const uint64_t lo16 = p.lo4 & ~15ull;
+    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start inside the arena
+    auto slot_src = [&](uint64_t S) {
+        const uint64_t a = S & ~15ull;
+        return a < lo16 ? lo16 : (a > smax ? smax : a);
+    };
+    const uint64_t Q = (uint64_t)gridDim.x * (kDmaWgThreads / 16);   // frames per sweep of the grid
+    uint64_t f = ((uint64_t)blockIdx.x * (kDmaWgThreads / 64) + (uint64_t)wave) * 4;
+    const uint64_t dS = Q * p.stride;
+    uint64_t S = p.base + f * p.stride;    // first frame of the item
+    if (f < p.n) dma_item(slot, slot_src(S), lane);
+
+    while (f < p.n) {   // wave-uniform
+        const uint64_t src = slot_src(S);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot DMA has landed
+        const int64_t x = (int64_t)(S - src) + klane;   // window start within the slot (>= -31)
+        const uint32_t r = (uint32_t)x & 3u;
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
+        uint32_t d[kChunkWords + 1];
+#pragma unroll
+        for (int q = 0; q <= kChunkWords; q++) d[q] = wp[q];
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+        const uint64_t fn = f + Q;
+        const uint64_t Sn = S + dS;
+        if (fn < p.n) dma_item(slot, slot_src(Sn), lane);
+
+#ifdef FCS_DMA_NOCRC   // measurement-only build: slot DMA and window reads, no CRC work (wrong FCS)
+        {
+            uint32_t acc = r;
+#pragma unroll
+            for (int q = 0; q <= kChunkWords; q++) acc ^= d[q];
+            if (acc == 0x12345678u) p.out[f] = acc;
+            f = fn;
+            S = Sn;
+            continue;
+        }
+#endif
+        uint32_t w[kChunkWords];
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#pragma unroll
+        for (int i = 0; i < kSingleMaskWords; i++)
+            if (4 * i < (int)p.zmax) w[i] &= m[i];
+        // kDmaChains independent chains of CL words; chain h ends 4 CL (kDmaChains - 1 - h) bytes
+        // before the window end, so the window value is XOR_h A_{4 CL (kDmaChains - 1 - h)}(chain h)
+        constexpr int CL = kDmaChainWords;
+        uint32_t xs[kDmaChains];
+#pragma unroll
+        for (int h = 0; h < kDmaChains; h++) xs[h] = w[h * CL] ^ (h == 0 ? x0 : 0u);
+#pragma unroll
+        for (int i = 0; i < CL; i++)
+#pragma unroll
+            for (int h = 0; h < kDmaChains; h++) xs[h] = step4_l16(lds, xs[h], i < CL - 1 ? w[h * CL + i + 1] : 0u, B, rot);
+        uint32_t mv = xs[kDmaChains - 1];
+#pragma unroll
+        for (int h = 0; h < kDmaChains - 1; h++) mv = uniform_shift_at(lds, kDmaMerge + 512u * (uint32_t)(kDmaChains - 2 - h), xs[h], mv);
+        uint32_t v = lane_shift(lds, mv, lanebase);
+        v = row_xor(v);
+        emit<kDmaBad>(p, lds, c == kGroup - 1 && f + g < p.n, f + g, ~v);
+        f = fn;
+        S = Sn;
+    }
+    flush_bad<kDmaBad>(p, lds);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Variable-length frames (IMIX-shaped batches): windowed class scheduling. Superseded by
@@ -1400,6 +1581,8 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
 #endif
         }
+    } else if (!tiny && fixed_dma(p)) {
+        hipLaunchKernelGGL(fcs_dma_kernel, dim3(grid), dim3(kDmaWgThreads), 0, st, p);
     } else if (tiny) {
         if (single) FCS_LAUNCH(false, true, true);
         else FCS_LAUNCH(false, true, false);

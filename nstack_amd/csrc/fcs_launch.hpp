@@ -105,7 +105,25 @@ inline bool fixed_single(const KParams &p) {
     return p.fseg == 1 && p.zmax <= kSingleMaxLead;
 #endif
 }
+// LDS-DMA kernel (fcs_dma_kernel): one-segment frames of kDmaMinLen..kDmaCover bytes whose four
+// consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
+// frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
+// and the arena must hold a whole slot (the last items' slots are clamped to its end).
+#ifndef FCS_DMA_WG_THREADS   // measurement-only override
+#define FCS_DMA_WG_THREADS 768
+#endif
+constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;
+static_assert(kDmaWgThreads % 64 == 0 && kDmaWgThreads <= 768, "LDS holds at most 12 wave slots");
+inline bool fixed_dma(const KParams &p) {
+#ifdef FCS_NO_DMA   // measurement-only build
+    return false;
+#else
+    return p.fseg == 1 && p.flen >= kDmaMinLen && p.flen <= kDmaCover && p.stride <= 2048 &&
+           3 * p.stride + p.flen <= kDmaItemBytes - 18 && p.hi4 - p.lo4 >= 2 * kDmaItemBytes;
+#endif
+}
 inline int fixed_threads(const KParams &p) {
+    if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;
     return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;
 }
 

@@ -23,6 +23,8 @@
 // These are constants of the algorithm, computed once per process; no frame bytes are ever
 // checksummed on the host (the product has no CPU CRC path).
 #pragma once
+#include <hip/hip_runtime.h>
+
 #include <cstdint>
 #include <cstring>
 #include <vector>
@@ -64,6 +66,18 @@ constexpr uint32_t kLdsFlatMark = kLdsFlat + kFlatBytes;        // 16 waves x 64
 constexpr uint32_t kLdsFlatList = kLdsFlatMark + 16 * 64;       // 16 waves x 64 B
 static_assert(kLdsFlatList + 16 * 64 <= kLdsJump, "flat scratch fits the lane-table region");
 
+// LDS-DMA fixed kernel (fcs_dma_kernel): frames arrive in LDS by global_load_lds, and lane c of a
+// frame's 16 reads its 96-byte window [E - e_c - 96, E - e_c) from there (E = frame end). Chunks
+// are 96 B except c = 3, 7, 11 (92 B: the window's first word belongs to lane c + 1 and is
+// masked), so e_c = 96 c - 4 (c / 4) and the 16 windows start on 16 distinct LDS banks
+// (e_c / 4 mod 32 = 8 (c mod 4) - c / 4): the data reads of one frame never conflict, where
+// 96-B steps put four lanes on each bank. 16 lanes cover e_15 + 96 = 1524 bytes.
+__host__ __device__ constexpr uint32_t dma_end_off(int c) { return 96u * (uint32_t)c - 4u * (uint32_t)(c >> 2); }
+__host__ __device__ constexpr bool dma_short_lane(int c) { return (c & 3) == 3 && c < 15; }
+constexpr uint32_t kDmaCover = dma_end_off(15) + kChunkBytes;   // 1524
+constexpr uint32_t kDmaMinLen = 1496;                            // front lane masks <= 28 B
+constexpr uint32_t kDmaItemBytes = 6144;                         // one wave's LDS slot: 6 x 1 KiB DMA
+
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
 constexpr uint32_t kBlobLane = 1024;                    // uint32 [8][16][32]
@@ -73,7 +87,9 @@ constexpr uint32_t kBlobH24 = kBlobH48 + 8 * 16;        // uint32 [8][16]
 constexpr uint32_t kBlobInv = kBlobH24 + 8 * 16;        // uint32 [96]
 constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
 constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][136] (C_c, LDS order)
-constexpr uint32_t kBlobWords = kBlobFlat + kFlatBytes / 4;
+constexpr uint32_t kBlobLaneDma = kBlobFlat + kFlatBytes / 4;   // uint32 [8][16][32]: A_{e_c}
+constexpr uint32_t kBlobMerge = kBlobLaneDma + 8 * 16 * 32;     // uint32 [11][8][16]: A_{8k}, k = 1..11
+constexpr uint32_t kBlobWords = kBlobMerge + 11 * 8 * 16;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -135,6 +151,16 @@ struct Tables {
             nibble_table((long)kChunkBytes * c, nt);
             for (int t = 0; t < 8; t++)
                 for (int e = 0; e < 16; e++) b[kBlobFlat + c * (kFlatStride / 4) + t * 16 + e] = nt[t][e];
+        }
+        for (int slot = 0; slot < 32; slot++) {
+            nibble_table((long)dma_end_off(slot % kGroup), nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobLaneDma + (t * 16 + e) * 32 + slot] = nt[t][e];
+        }
+        for (int k = 1; k <= 11; k++) {   // chain-merge shifts of the LDS-DMA kernel
+            nibble_table(8L * k, nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobMerge + (k - 1) * 128 + t * 16 + e] = nt[t][e];
         }
         return b;
     }

@@ -132,3 +132,114 @@ def model_frame(lds, mem: bytes, S: int, L: int):
     for j in range(GROUP):
         v ^= lane_shift(lds, state[j], j)
     return (~v & 0xFFFFFFFF) if L else 0
+
+
+# ---- LDS-DMA fixed kernel (fcs_dma_kernel): LDS16 tables, 6 KiB slots, windows at e_c ----
+BLOB_M768 = BLOB_INV + CHUNK
+BLOB_FLAT = BLOB_M768 + 8 * 16
+BLOB_LANE_DMA = BLOB_FLAT + 16 * 544 // 4
+DMA_SLOT = 6144
+DMA_COVER = 1524
+
+
+def dma_end_off(c):
+    return 96 * c - 4 * (c >> 2)
+
+
+def dma_short_lane(c):
+    return (c & 3) == 3 and c < 15
+
+
+BLOB_MERGE = BLOB_LANE_DMA + 8 * 16 * 32
+DMA_CHAINS = 2                    # fcs_kernel.hip FCS_DMA_CHAINS default
+DMA_MERGE = 81920
+DMA_INV = DMA_MERGE + 512 * (DMA_CHAINS - 1)
+
+
+def build_lds_dma(blob, chains=DMA_CHAINS):
+    """The DMA kernel's table image: LDS16 slice tables at 0, A_{e_c} lane tables at 65536, the
+    chain-merge tables A_{4 CL m} (m = 1 .. chains-1) at 81920, INV after them (byte offsets, as
+    fcs_dma_kernel stages them)."""
+    cl = 24 // chains
+    inv = DMA_MERGE + 512 * (chains - 1)
+    lds = np.zeros((inv + 384) // 4, dtype=np.uint32)
+    for i in range(4096):
+        v = blob[BLOB_SLICE + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)]
+        lds[i * 4:i * 4 + 4] = v
+    lds[65536 // 4:65536 // 4 + 4096] = blob[BLOB_LANE_DMA:BLOB_LANE_DMA + 4096]
+    for m in range(chains - 1):
+        k = (cl // 2) * (m + 1)          # A_{8k}
+        lds[(DMA_MERGE + 512 * m) // 4:(DMA_MERGE + 512 * m) // 4 + 128] = \
+            blob[BLOB_MERGE + (k - 1) * 128:BLOB_MERGE + k * 128]
+    lds[inv // 4:inv // 4 + 96] = blob[BLOB_INV:BLOB_INV + 96]
+    return lds
+
+
+def step4_l16(lds, x, lane):
+    jl = (lane >> 4) & 1
+    B = [(lane & 15) * 4 + 64 * (k ^ jl) for k in range(4)]
+    xr = v_perm(x, x, 0x02030001 if jl else 0x03020100)
+    r = 0
+    for k in range(4):
+        r ^= int(lds[v_perm(xr, B[k], 0x0C0C0400 + (k << 8)) // 4])
+    return r
+
+
+def lds16_banks(lane, x, k):
+    """Bank (dword address mod 32) of lane's lookup k of word x in the DMA kernel's table set."""
+    jl = (lane >> 4) & 1
+    xr = v_perm(x, x, 0x02030001 if jl else 0x03020100)
+    return (v_perm(xr, (lane & 15) * 4 + 64 * (k ^ jl), 0x0C0C0400 + (k << 8)) // 4) % 32
+
+
+def model_dma_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f: int, garbage: bytes,
+                   chains=DMA_CHAINS):
+    """The four FCS values fcs_dma_kernel computes for the wave item whose first frame is f (frames
+    >= n are None). mem is the whole arena, base its frame-0 offset; bytes a window reads outside
+    the slot image come from `garbage` (they must all be masked)."""
+    lo16 = (base & ~3) & ~15
+    hi16 = (((base + (n - 1) * stride + flen + 3) & ~3) + 15) & ~15
+    smax = hi16 - DMA_SLOT
+    S = base + f * stride
+    src = min(max(S & ~15, lo16), smax)
+    img = bytearray(garbage[:64]) + bytearray(DMA_SLOT) + bytearray(garbage[64:128])
+    chunk = mem[src:src + DMA_SLOT]
+    img[64:64 + len(chunk)] = chunk
+    zmax = max(4, DMA_COVER - flen)
+    cl = 24 // chains
+    inv = DMA_MERGE + 512 * (chains - 1)
+    out = []
+    for g in range(4):
+        regs = []
+        for c in range(16):
+            lane = 16 * g + c
+            ec = dma_end_off(c)
+            x = (S - src) + g * stride + flen - ec - CHUNK
+            r = x & 3
+            a = 64 + (x & ~3)
+            d = [int.from_bytes(img[a + 4 * q:a + 4 * q + 4], "little") for q in range(25)]
+            w = [alignbyte(d[i + 1], d[i], r) for i in range(24)]
+            zc = (DMA_COVER - flen) if c == 15 else (4 if dma_short_lane(c) else 0)
+            for i in range(8):
+                if 4 * i < zmax:
+                    t = max(0, min(4, zc - 4 * i))
+                    w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
+            x0 = int(lds[(inv + 4 * zc) // 4]) if c == 15 else 0
+            xs = [w[h * cl] ^ (x0 if h == 0 else 0) for h in range(chains)]
+            for i in range(cl):
+                for h in range(chains):
+                    xs[h] = step4_l16(lds, xs[h], lane) ^ (w[h * cl + i + 1] if i < cl - 1 else 0)
+            m = xs[chains - 1]
+            for h in range(chains - 1):
+                m = uniform_shift(lds, xs[h], DMA_MERGE + 512 * (chains - 2 - h)) ^ m
+            lanebase = 65536 | ((lane & 31) * 4)
+            s = 0
+            for t in range(8):
+                sh = (m >> (4 * t - 7)) if 4 * t >= 7 else ((m << (7 - 4 * t)) & 0xFFFFFFFF)
+                s ^= int(lds[(((sh & 0x780) | lanebase) + t * 2048) // 4])
+            regs.append(s)
+        v = 0
+        for s in regs:
+            v ^= s
+        out.append((~v & 0xFFFFFFFF) if f + g < n else None)
+    return out

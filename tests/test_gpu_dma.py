@@ -1,0 +1,94 @@
+"""GPU parity of the LDS-DMA fixed kernel (fcs_dma_kernel).
+
+Fixed-length batches of 1496..1524-B frames whose four consecutive frames fit a 6 KiB slot
+(3 stride + len <= 6126) and whose arena holds two slots take this kernel; smaller ones the
+register-load single kernel. Every case is checked bit-exact against the oracle (the CPU
+restatement of src/ether_fcs.c:4-19), at all four base alignments, with batch sizes on both sides
+of the selection threshold and grids from one partial item to many sweeps, so the slot clamping at
+the arena end and frames past n in a wave's last item are exercised. Verify mode (frames carrying
+their FCS trailer, RX residue check) goes through the same kernel's epilogue.
+"""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import nstack_amd as na
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    na.load()
+    return torch.device("cuda:0")
+
+
+def oracle_fixed(oracle, host: np.ndarray, stride, L, n):
+    out = np.empty(n, dtype=np.uint32)
+    oracle.oracle_fcs_fixed(host.ctypes.data, stride, L, n, out.ctypes.data, 1, 16)
+    return out
+
+
+LENS = [1496, 1497, 1503, 1504, 1513, 1514, 1517, 1518, 1519, 1520, 1523, 1524]
+
+
+@pytest.mark.parametrize("L", LENS)
+def test_dma_lengths_strides_alignments(dev, oracle, L):
+    strides = sorted({s for s in (L, L + 1, L + 2, L + 3, L + 10, 1536, 1544) if 3 * s + L <= 6126})
+    for stride in strides:
+        for n in (8, 9, 13, 257, 4099):
+            host = np.random.default_rng(L * 131 + stride * 7 + n).integers(0, 256, n * stride + 8, dtype=np.uint8)
+            d = torch.from_numpy(host).to(dev)
+            for lead in (0, 1, 2, 3):
+                # the last frame ends exactly at the end of the buffer the engine is told about
+                out = torch.empty(n, dtype=torch.int32, device=dev)
+                na.fixed_dev(d.data_ptr() + lead, stride, L, n, out)
+                torch.cuda.synchronize()
+                got = out.cpu().numpy().view(np.uint32)
+                exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+                assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
+
+
+def test_dma_many_sweeps(dev, oracle):
+    """More items than the persistent grid holds (every wave walks several items)."""
+    L, n = 1518, 70001
+    host = np.random.default_rng(5).integers(0, 256, n * L + 3, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    for lead in (0, 3):
+        out = torch.empty(n, dtype=torch.int32, device=dev)
+        na.fixed_dev(d.data_ptr() + lead, L, L, n, out)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, oracle_fixed(oracle, host[lead:], L, L, n)), lead
+
+
+@pytest.mark.parametrize("L", [1500, 1518, 1524])
+def test_dma_verify_mode(dev, L):
+    """RX residue check through the DMA kernel: frames of L bytes (L - 4 covered + LE FCS trailer),
+    a few corrupted; ok[] and the bad count against zlib."""
+    n = 20011
+    rng = np.random.default_rng(L)
+    host = rng.integers(0, 256, n * L, dtype=np.uint8)
+    for i in range(n):
+        f = host[i * L:i * L + L - 4].tobytes()
+        host[i * L + L - 4:i * L + L] = np.frombuffer(struct.pack("<I", zlib.crc32(f)), dtype=np.uint8)
+    bad_idx = sorted(set(int(x) for x in rng.integers(0, n, 37)) | {0, n - 1})
+    for i in bad_idx:
+        host[i * L + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    d = torch.from_numpy(host).to(dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    na.verify_fixed_dev(d, L, L, n, ok, bad)
+    torch.cuda.synchronize()
+    okh = ok.cpu().numpy()
+    exp = np.ones(n, dtype=np.uint8)
+    exp[bad_idx] = 0
+    assert np.array_equal(okh, exp)
+    assert int(bad.item()) == len(bad_idx)

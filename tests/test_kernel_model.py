@@ -115,3 +115,47 @@ def test_single_frame_kernel_decomposition():
             x = [y[j] ^ y[j ^ d] for j in range(64)]
         got = ~(x[0] ^ zshift(0xFFFFFFFF, L)) & 0xFFFFFFFF
         assert got == zlib.crc32(frame), L
+
+
+@pytest.fixture(scope="module")
+def lds_dma():
+    blob = na.tables_blob()
+    return {ch: km.build_lds_dma(blob, ch) for ch in (2, 3, 4, 6)}
+
+
+@pytest.mark.parametrize("chains", [2, 3, 4, 6])
+@pytest.mark.parametrize("flen,extra", [(1496, 0), (1514, 4), (1518, 0), (1518, 2), (1520, 0), (1524, 0), (1524, 12)])
+def test_dma_kernel_model(lds_dma, flen, extra, chains):
+    """fcs_dma_kernel's decomposition (LDS16 tables with the half-wave rotation, 6 KiB slots clamped
+    at the arena end, 92-B chunks at c = 3/7/11, front mask and INV of lane 15, the chains and
+    their one-step merge for every FCS_DMA_CHAINS value, A_{e_c} lane shift)
+    replayed on the CPU for every item of small batches at all four base alignments, against zlib."""
+    stride = flen + extra
+    rng = random.Random(flen * 31 + extra + chains)
+    garbage = bytes(rng.randrange(256) for _ in range(128))
+    for b0 in (0, 1, 2, 3):
+        n = 11
+        mem = bytes(rng.randrange(256) for _ in range(b0 + n * stride + 64))
+        for f in range(0, n, 4):
+            got = km.model_dma_item(lds_dma[chains], mem, b0, stride, flen, n, f, garbage, chains)
+            for g in range(4):
+                if f + g < n:
+                    S = b0 + (f + g) * stride
+                    assert got[g] == zlib.crc32(mem[S:S + flen]), (flen, extra, b0, f + g)
+
+
+def test_dma_windows_bank_distinct():
+    """The 16 windows of a frame start on 16 distinct dword banks (mod 32), for any frame end."""
+    for E in range(0, 64, 4):
+        banks = {((E - km.dma_end_off(c) - 96) // 4) % 32 for c in range(16)}
+        assert len(banks) == 16
+
+
+def test_dma_table_lookups_bank_distinct():
+    """Every table lookup of a 32-lane group hits 32 distinct banks (dword address mod 32, the
+    ds_read_b32 banking), whatever words the lanes hold."""
+    rng = random.Random(4)
+    for _ in range(200):
+        xs = [rng.getrandbits(32) for _ in range(32)]
+        for k in range(4):
+            assert len({km.lds16_banks(l, xs[l], k) for l in range(32)}) == 32
