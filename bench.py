@@ -14,10 +14,17 @@ Printed (rank 0, one JSON line): the contract fields plus
   roofline     — the FCS kernel's achieved algorithmic GB/s (frame bytes per launch / average
                  launch time from HIP events on the launch stream) against the 8 TB/s HBM peak;
                  `traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary
-                 (profiles/*pmc*.json), or null;
-  read_stream  — a pure read kernel over the same buffer (the measured HBM read ceiling);
-  cpu_baseline — the oracle's restatement of src/ether_fcs.c (nibble table, one host thread,
-                 -O2 and the reference's own -O0 flags) on 1 M x 1518 B, rank 0, N = 1.
+                 (profiles/*pmc_traffic*.json), or null; read_stream_gbs = a pure read kernel over
+                 the same buffer (the measured HBM read ceiling);
+  cpu_baseline — the reference's own src/ether_fcs.c (oracle/_ref, its Makefile flags) timed on
+                 1 M x 1518 B (SURVEY §8d) on one host thread, the oracle port beside it; rank 0, N = 1;
+  configs      — (N = 1) the other single-GPU BASELINE configs, each timed in this process after the
+                 headline and freed before the next: imix_128M (configs[2]), jumbo_16M_x_9000
+                 (configs[3]) and host_inclusive_1518 (frames in pinned host memory -> H2D -> kernel
+                 -> D2H, PCIe-bound; never `value`), each with ms, GB/s, roofline frac and a zlib
+                 spot check of sampled frames.
+For N > 1 the timing barrier and the max-over-ranks use gloo on the host: no RCCL collective
+anywhere (BASELINE north_star), and nothing but 8 bytes of timing crosses ranks.
 """
 from __future__ import annotations
 
@@ -67,17 +74,127 @@ def splitmix_bytes(seed: int, byte_off: int, n: int):
     return b[s:s + n]
 
 
-def _load_pmc_traffic(frames: int, L: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary, if one matches."""
+def _load_pmc_traffic(frames: int, L, kernel: str = None):
+    """HBM bytes per launch from the newest committed rocprofv3 PMC summary of this workload
+    (profiles/rNN_pmc_traffic*.json; later rounds sort later), if one matches."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
         try:
             d = json.load(open(p))
         except Exception:
             continue
+        if kernel is not None and kernel not in d.get("kernel", ""):
+            continue
         if d.get("frames") == frames and d.get("len") == L and d.get("hbm_bytes_per_launch"):
             best = (d["hbm_bytes_per_launch"], os.path.relpath(p, ROOT))
     return best
+
+
+def _time_launches(fn, reps, stream, torch):
+    """Average ms per launch from HIP events on the launch stream, after one untimed launch."""
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        fn()
+    e1.record(stream)
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+def _spot(crcs, frame_bytes, idx):
+    """Number of sampled frames whose GPU CRC differs from zlib.crc32 (= ether_fcs)."""
+    import zlib
+    return sum(int(zlib.crc32(frame_bytes(int(i))) != int(crcs[int(i)])) for i in idx)
+
+
+def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
+    """BASELINE configs[2] (IMIX), configs[3] (jumbo) and the host-inclusive rate, one after the other
+    in HBM (each freed before the next), timed like the headline. Returns a dict for the JSON line."""
+    import numpy as np
+    rng = np.random.default_rng(2026)
+    res = {}
+    # ---- configs[2]: 128 M IMIX frames, 7:4:1 of 64/576/1518 in exact counts, shuffled, packed ----
+    n = 128 << 20
+    counts = [78293676, 44739242, 11184810]
+    ln_np = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), counts)
+    np.random.default_rng(7).shuffle(ln_np)
+    ln = torch.from_numpy(ln_np.view(np.int32)).to(dev)
+    off = torch.zeros(n, dtype=torch.int64, device=dev)
+    off[1:] = torch.cumsum(ln[:-1].to(torch.int64), 0)
+    total = int(off[-1].item()) + int(ln_np[-1])
+    arena = torch.empty(total, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, total, SEED + 2, 0, stream)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    ms = _time_launches(lambda: na.batch_dev(arena, total, off, ln, out, n, stream), reps, stream, torch)
+    crcs = out.cpu().numpy().view(np.uint32)
+    offs = off.cpu().numpy()
+    idx = rng.integers(0, n, 256)
+    bad = _spot(crcs, lambda i: splitmix_bytes(SEED + 2, int(offs[i]), int(ln_np[i])).tobytes(), idx)
+    gbs = total / ms / 1e6
+    pmc = _load_pmc_traffic(n, "imix")
+    res["imix_128M"] = {"config": "BASELINE configs[2]", "frames": n, "bytes": total, "ms": round(ms, 4),
+                        "GB_s": round(gbs, 1), "GiB_s": round(total / ms / 1e-3 / GIB, 1),
+                        "Gframes_s": round(n / ms / 1e6, 3), "metadata_bytes": n * 12,
+                        "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc[0] if pmc else None,
+                                     "traffic_source": pmc[1] if pmc else None},
+                        "spot_checked": len(idx), "spot_bad": bad}
+    del arena, out, off, ln, crcs, offs, ln_np
+    torch.cuda.empty_cache()
+    # ---- configs[3]: 16 M x 9000-B jumbo frames ----
+    n, L = 16 << 20, 9000
+    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, n * L, SEED + 3, 0, stream)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    ms = _time_launches(lambda: na.fixed_dev(arena, L, L, n, out, stream), reps, stream, torch)
+    crcs = out.cpu().numpy().view(np.uint32)
+    idx = rng.integers(0, n, 128)
+    bad = _spot(crcs, lambda i: splitmix_bytes(SEED + 3, i * L, L).tobytes(), idx)
+    gbs = n * L / ms / 1e6
+    pmc = _load_pmc_traffic(n, L)
+    res["jumbo_16M_x_9000"] = {"config": "BASELINE configs[3]", "frames": n, "bytes": n * L, "ms": round(ms, 4),
+                               "GB_s": round(gbs, 1), "GiB_s": round(n * L / ms / 1e-3 / GIB, 1),
+                               "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS,
+                                            "unit": "GB/s", "frac": round(gbs / HBM_PEAK_GBS, 4),
+                                            "traffic": pmc[0] if pmc else None,
+                                            "traffic_source": pmc[1] if pmc else None},
+                               "spot_checked": len(idx), "spot_bad": bad}
+    del arena, out, crcs
+    torch.cuda.empty_cache()
+    # ---- host-inclusive: 1518-B frames in pinned host memory, through ether_fcs_fixed_host ----
+    L = 1518
+    n = int(host_gib * GIB) // L
+    nbytes = n * L
+    lib = na.load()
+    p = lib.fcs_host_alloc(nbytes)
+    if p:
+        pinned = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+        d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        na.fill_splitmix_dev(d, nbytes, SEED + 4, 0, stream)
+        torch.cuda.synchronize()
+        pinned[:] = d.cpu().numpy()
+        del d
+        torch.cuda.empty_cache()
+        hout = np.zeros(n, dtype=np.uint32)
+        na.fixed_host(p, L, L, min(n, 1 << 16), hout)     # pipeline buffers allocated untimed
+        t0 = time.perf_counter()
+        na.fixed_host(p, L, L, n, hout)
+        secs = time.perf_counter() - t0
+        idx = rng.integers(0, n, 128)
+        bad = _spot(hout, lambda i: pinned[i * L:(i + 1) * L].tobytes(), idx)
+        res["host_inclusive_1518"] = {"what": "pinned host frames -> chunked H2D -> kernel -> D2H of CRCs "
+                                              "(ether_fcs_fixed_host); PCIe Gen5 x16 bound, never `value`",
+                                      "frames": n, "bytes": nbytes, "ms": round(secs * 1e3, 3),
+                                      "GB_s": round(nbytes / secs / 1e9, 2), "GiB_s": round(nbytes / secs / GIB, 2),
+                                      "roofline": {"bound": "pcie", "achieved": round(nbytes / secs / 1e9, 2),
+                                                   "peak": 63.0, "unit": "GB/s",
+                                                   "frac": round(nbytes / secs / 1e9 / 63.0, 4)},
+                                      "spot_checked": len(idx), "spot_bad": bad}
+        del pinned, hout
+        lib.fcs_host_free(p)
+    return res
 
 
 def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
@@ -161,6 +278,7 @@ def main():
     ap.add_argument("--len", type=int, default=1518)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N = 1 only)")
     args = ap.parse_args()
 
     import numpy as np
@@ -172,9 +290,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
+        # gloo on the host: the barrier and the 8-byte max-over-ranks of the elapsed time are the
+        # only cross-rank traffic; frames never leave their GPU (no RCCL, BASELINE north_star)
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
+        dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -234,7 +354,7 @@ def main():
     wall = t1 - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps   # HIP events on the launch stream
 
-    times = torch.tensor([wall], dtype=torch.float64, device=dev)
+    times = torch.tensor([wall], dtype=torch.float64)
     if dist:
         dist.all_reduce(times, op=dist.ReduceOp.MAX)
     tmax = float(times.item())
@@ -253,13 +373,13 @@ def main():
         for i in idx:
             frame = splitmix_bytes(SEED, (lo + int(i)) * L, L)
             bad += int(zlib.crc32(frame.tobytes()) != int(crcs[i]))
-        flag = torch.tensor([bad], dtype=torch.int64, device=dev)
+        flag = torch.tensor([bad], dtype=torch.int64)
         if dist:
             dist.all_reduce(flag)
         verified = int(flag.item()) == 0
 
     achieved_gbs = nbytes / (kernel_ms * 1e-3) / 1e9
-    pmc = _load_pmc_traffic(n, L)
+    pmc = _load_pmc_traffic(n, L, "fcs_dma_kernel")
     roofline = {"bound": "hbm", "achieved": round(achieved_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved_gbs / HBM_PEAK_GBS, 4),
                 "traffic": pmc[0] if pmc else None,
@@ -272,6 +392,11 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
         cpu = cpu_baseline()
+    configs = None
+    if world == 1 and not args.no_configs and F == 64 << 20 and L == 1518:
+        del arena, out
+        torch.cuda.empty_cache()
+        configs = extra_configs(torch, na, dev, stream)
 
     if dist:
         dist.barrier()
@@ -297,6 +422,7 @@ def main():
             "verified": verified,
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "configs": configs,
             "engine": na.version(),
         }
         print(json.dumps(rec), flush=True)

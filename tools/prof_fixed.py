@@ -26,7 +26,11 @@ def main():
     if a.imix:
         import numpy as np
         a.var = True
-        ln_np = np.random.default_rng(7).choice(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.uint32), n)
+        if n == 128 << 20:   # BASELINE configs[2] exactly as bench.py builds it (7:4:1 counts, shuffled)
+            ln_np = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), [78293676, 44739242, 11184810])
+            np.random.default_rng(7).shuffle(ln_np)
+        else:
+            ln_np = np.random.default_rng(7).choice(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.uint32), n)
         ln = torch.from_numpy(ln_np.view(np.int32)).to(dev)
         off = torch.zeros(n, dtype=torch.int64, device=dev)
         off[1:] = torch.cumsum(ln[:-1].to(torch.int64), 0)

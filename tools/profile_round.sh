@@ -1,15 +1,20 @@
 #!/bin/bash
 # Round profile bundle (GPU box): rocprofv3 kernel-trace stats of the default bench command (its
-# JSON line and the kernel statistics come from the same process) and separate PMC passes for the
-# HBM traffic of the FCS kernel at the bench workload. Outputs under $1.
+# JSON line and the kernel statistics come from the same process), then separate PMC passes
+# (FETCH_SIZE, WRITE_SIZE; one counter group per run) for the HBM traffic of the headline kernel
+# (64 M x 1518 B) and of the IMIX flat kernel (BASELINE configs[2]). Outputs under $1.
 set -u
 OUT=${1:-gpurun_out/prof}; mkdir -p "$OUT"; export TMPDIR=/tmp
-timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench \
-    -- python3 bench.py > "$OUT/bench_under_rocprof.log" 2>&1
-rc=$?; echo "trace rc=$rc"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run --pmc FETCH_SIZE \
-    -- python3 tools/prof_fixed.py --reps 3 > "$OUT/pmc_fetch.log" 2>&1
-rc=$?; echo "pmc fetch rc=$rc"; [ $rc -ne 0 ] && exit $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run --pmc WRITE_SIZE \
-    -- python3 tools/prof_fixed.py --reps 3 > "$OUT/pmc_write.log" 2>&1
-rc=$?; echo "pmc write rc=$rc"; exit $rc
+step() {   # tag, timeout, command...
+  local tag=$1 lim=$2; shift 2
+  timeout -k 10 "$lim" "$@" > "$OUT/$tag.log" 2>&1
+  local rc=$?; echo "$tag rc=$rc"
+  [ $rc -ne 0 ] && exit $rc
+  return 0
+}
+step bench_under_rocprof 500 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/trace" -o bench -- python3 bench.py
+step pmc_fetch 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_fetch" -o run --pmc FETCH_SIZE -- python3 tools/prof_fixed.py --reps 3
+step pmc_write 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run --pmc WRITE_SIZE -- python3 tools/prof_fixed.py --reps 3
+step imix_fetch 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/imix_fetch" -o run --pmc FETCH_SIZE -- python3 tools/prof_fixed.py --reps 3 --imix --frames 134217728
+step imix_write 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/imix_write" -o run --pmc WRITE_SIZE -- python3 tools/prof_fixed.py --reps 3 --imix --frames 134217728
+exit 0

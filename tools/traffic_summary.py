@@ -1,17 +1,19 @@
 #!/usr/bin/env python3
-"""Write profiles/<round>_pmc_traffic.json from tools/profile_round.sh's PMC passes.
+"""Write profiles/<round>_pmc_traffic*.json from separate rocprofv3 FETCH_SIZE / WRITE_SIZE passes.
 
-    python tools/traffic_summary.py gpurun_out/prof profiles/r01_pmc_traffic.json
+    python tools/traffic_summary.py SRC DST [--kernel K] [--frames F] [--len L|imix] [--alg BYTES]
+                                    [--meta BYTES] [--sub-fetch pmc_fetch] [--sub-write pmc_write]
 
-HBM bytes per launch of the product's fixed-length kernel at the bench workload, corrected as
-MI355X_MICROARCH.md's HBM section prescribes: FETCH_SIZE (KB) x 2 on gfx950 for wide streaming
-reads, WRITE_SIZE (KB) as is, KB = 1024 B. bench.py reads the file for roofline.traffic.
+HBM bytes per launch of one kernel at one workload, corrected as MI355X_MICROARCH.md's HBM section
+prescribes: FETCH_SIZE (KB) x 2 on gfx950 for wide streaming reads (16 B per lane, global_load and
+LDS-DMA alike), WRITE_SIZE (KB) as is, KB = 1024 B. bench.py reads the newest matching file for
+roofline.traffic (kernel name, frames and len must match its workload).
 """
+import argparse
 import csv
 import glob
 import json
 import os
-import sys
 
 
 def per_dispatch(outdir, counter, kernel):
@@ -28,28 +30,38 @@ def per_dispatch(outdir, counter, kernel):
 
 
 def main():
-    src, dst = sys.argv[1], sys.argv[2]
-    kernel = "fcs_single_kernel"
-    frames, L = 64 << 20, 1518
-    fetch, n_f, ms_f = per_dispatch(os.path.join(src, "pmc_fetch"), "FETCH_SIZE", kernel)
-    write, n_w, ms_w = per_dispatch(os.path.join(src, "pmc_write"), "WRITE_SIZE", kernel)
-    alg = frames * L
+    ap = argparse.ArgumentParser()
+    ap.add_argument("src")
+    ap.add_argument("dst")
+    ap.add_argument("--kernel", default="fcs_dma_kernel")
+    ap.add_argument("--frames", type=int, default=64 << 20)
+    ap.add_argument("--len", default="1518")
+    ap.add_argument("--alg", type=int, default=None, help="algorithmic bytes per launch (default frames x len)")
+    ap.add_argument("--meta", type=int, default=0, help="metadata bytes per launch (offsets, lengths, CRCs)")
+    ap.add_argument("--sub-fetch", default="pmc_fetch")
+    ap.add_argument("--sub-write", default="pmc_write")
+    ap.add_argument("--command", default="tools/profile_round.sh")
+    a = ap.parse_args()
+    L = int(a.len) if a.len.isdigit() else a.len
+    alg = a.alg if a.alg is not None else a.frames * int(L)
+    fetch, n_f, ms_f = per_dispatch(os.path.join(a.src, a.sub_fetch), "FETCH_SIZE", a.kernel)
+    write, n_w, ms_w = per_dispatch(os.path.join(a.src, a.sub_write), "WRITE_SIZE", a.kernel)
     rd = fetch * 1024 * 2
     wr = write * 1024
     rec = {
-        "round": int(os.path.basename(dst)[1:3]),
-        "kernel": "fcs::fcs_single_kernel (fixed length, single segment; product kernel for 1518 B)",
-        "frames": frames, "len": L, "algorithmic_bytes_per_launch": alg,
-        "command": "tools/profile_round.sh: rocprofv3 --kernel-trace --output-format csv --pmc FETCH_SIZE -- "
-                   "python3 tools/prof_fixed.py --reps 3 (and a separate --pmc WRITE_SIZE pass)",
+        "round": int(os.path.basename(a.dst)[1:3]),
+        "kernel": "fcs::" + a.kernel,
+        "frames": a.frames, "len": L, "algorithmic_bytes_per_launch": alg, "metadata_bytes_per_launch": a.meta,
+        "command": a.command,
         "FETCH_SIZE_kb_per_launch": fetch, "WRITE_SIZE_kb_per_launch": write,
         "correction": "MI355X_MICROARCH.md HBM: on gfx950 FETCH_SIZE reports 1/2 of the bytes of a wide "
                       "coalesced read -> x2; WRITE_SIZE taken as is; KB = 1024 B",
         "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr, "hbm_bytes_per_launch": rd + wr,
         "read_over_algorithmic": rd / alg,
+        "read_over_algorithmic_plus_metadata": rd / (alg + a.meta),
         "dispatch_ms_under_pmc": ms_f, "launches_counted": n_f,
     }
-    json.dump(rec, open(dst, "w"), indent=1)
+    json.dump(rec, open(a.dst, "w"), indent=1)
     print(json.dumps(rec, indent=1))
 
 
