@@ -45,11 +45,12 @@ GIB = float(1 << 30)
 SEED = 0x4E535441434B        # "NSTACK"
 
 
-def shard_range(total_frames: int, world: int, rank: int):
-    """Contiguous frame range of `rank` (BASELINE configs[4]: 512 M frames over 8 GPUs)."""
-    lo = total_frames * rank // world
-    hi = total_frames * (rank + 1) // world
-    return lo, hi
+def shard_range(total_frames: int, world: int, rank: int, lengths=None):
+    """Contiguous frame range of `rank` (BASELINE configs[4]: 512 M frames over 8 GPUs), from the
+    engine's own shard planner (fcs_shard_plan; byte-balanced when `lengths` is given)."""
+    import nstack_amd as na
+    cut = na.shard_plan(total_frames, world, lengths)
+    return cut[rank], cut[rank + 1]
 
 
 def aggregate(bytes_per_rank, times):

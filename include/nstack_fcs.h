@@ -25,8 +25,10 @@
  * (-EINVAL bad arguments, -ENODEV no usable GPU / HIP code object missing, -ENOMEM,
  * -EIO a HIP runtime error; fcs_last_error() has the text). There is NO CPU fallback:
  * without a GPU the engine fails loudly. ether_fcs() has no error channel in the
- * reference (it cannot fail there), so on an engine failure it prints the reason to
- * stderr and aborts rather than return a wrong FCS.
+ * reference (it cannot fail there): a failed attempt (HIP error, lost completion, timeout)
+ * drops that lane's stream and result word and is retried once on a fresh lane; only if the
+ * retry fails too does it print the reason to stderr and abort rather than return a wrong FCS
+ * (fcs_engine_stats counts calls, retries and recoveries).
  *
  * Threading: every entry point is thread-safe and may be called concurrently (the reference
  * calls ether_fcs from the main, ingress, egress and TCP-timer threads: SURVEY.md §8b).
@@ -59,6 +61,15 @@ const char *fcs_engine_version(void);
  * (one quarter-wave per frame), larger ones the throughput-optimised windowed kernel. Results are
  * identical either way. Default 16384. Returns the previous value. */
 uint64_t fcs_engine_set_var_threshold(uint64_t frames);
+/* Drop-in health: ether_fcs calls, first attempts that failed and were retried, retries that
+ * succeeded, and lanes (stream + result word) dropped after a failure. Any pointer may be NULL. */
+void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t *dropin_recovered,
+                      uint64_t *lane_resets);
+/* Shard planner of the host batch paths (and of bench.py's ranks): cut[0..parts] such that part g
+ * is frames [cut[g], cut[g+1]). len == NULL: equal frame counts (cut[g] = n g / parts); otherwise
+ * byte-balanced contiguous ranges (cut[g] = first index whose length prefix reaches g/parts of the
+ * total). Pure host arithmetic, no GPU needed. Returns 0 or -EINVAL. */
+int fcs_shard_plan(const uint32_t *len, uint64_t n, uint32_t parts, uint64_t *cut);
 
 /* ---- device-resident batches (pointers in HBM of the current device) ---- */
 /* Variable-length frames: frame i = arena[off[i] .. off[i]+len[i]), all inside

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "tx_batch_host", "host_buffer", "host_free", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS"]
+           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -26,7 +26,7 @@ EXPORTS = [
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
-    "fcs_tables_blob",
+    "fcs_tables_blob", "fcs_engine_stats", "fcs_shard_plan",
     # include/nstack_txq.h — batched TX call site
     "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
@@ -87,6 +87,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_read_stream_dev": (i32, [vp, u64, vp, vp]),
         "fcs_timed_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, i32, c.POINTER(c.c_float)]),
         "fcs_tables_blob": (i32, [vp, u64]),
+        "fcs_engine_stats": (None, [c.POINTER(u64)] * 4),
+        "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_txq_create": (vp, [vp, u32, u32, vp, vp]),
         "fcs_txq_send": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
         "fcs_txq_flush": (i32, [vp]),
@@ -256,6 +258,25 @@ def timed_fixed_dev(base, stride: int, length: int, n: int, out, stream=None, re
     _check(load().fcs_timed_fixed_dev(_ptr(base), stride, length, n, _ptr(out), _stream(stream),
                                       reps, ctypes.byref(ms)), "fcs_timed_fixed_dev")
     return float(ms.value)
+
+
+def engine_stats() -> dict:
+    """Drop-in ether_fcs health counters (fcs_engine_stats)."""
+    import ctypes as c
+    v = [c.c_uint64(0) for _ in range(4)]
+    load().fcs_engine_stats(*[c.byref(x) for x in v])
+    return dict(zip(("dropin_calls", "dropin_retries", "dropin_recovered", "lane_resets"), (x.value for x in v)))
+
+
+def shard_plan(n: int, parts: int, lengths=None):
+    """The engine's shard planner (fcs_shard_plan): cut points [0 .. n] of `parts` contiguous frame
+    ranges, byte-balanced when `lengths` (uint32 per frame) is given. Host arithmetic only."""
+    import numpy as np
+    cut = np.zeros(parts + 1, dtype=np.uint64)
+    ln = None if lengths is None else np.ascontiguousarray(lengths, dtype=np.uint32)
+    _check(load().fcs_shard_plan(None if ln is None else ln.ctypes.data, n, parts, cut.ctypes.data),
+           "fcs_shard_plan")
+    return [int(x) for x in cut]
 
 
 def tables_blob():

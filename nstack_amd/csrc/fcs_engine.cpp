@@ -58,6 +58,39 @@ int hip_fail(hipError_t e, const char *what) {
         if (e_ != hipSuccess) return hip_fail(e_, what); \
     } while (0)
 
+// Makes `dev` current for the scope and restores the caller's device on exit (a host-batch call
+// must not leave a multi-GPU caller's thread on another device: its next *_dev call resolves the
+// device from the thread's current one).
+struct DeviceGuard {
+    int prev = -1;
+    hipError_t err = hipSuccess;
+    explicit DeviceGuard(int dev) {
+        if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+        err = hipSetDevice(dev);
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+    DeviceGuard(const DeviceGuard &) = delete;
+    DeviceGuard &operator=(const DeviceGuard &) = delete;
+};
+
+// Drop-in ether_fcs health counters (fcs_engine_stats).
+std::atomic<uint64_t> g_dropin_calls{0}, g_dropin_retries{0}, g_dropin_recovered{0}, g_lane_resets{0};
+
+#ifdef FCS_FAULT_HOOK
+// Test-only build (libnstack_fcs_faults.so): the calling thread's next N drop-in attempts fail as
+// if the GPU step had returned an error, so the recovery path can be exercised on a healthy GPU.
+thread_local int g_inject_faults = 0;
+bool injected_fault() {
+    if (g_inject_faults <= 0) return false;
+    g_inject_faults--;
+    return true;
+}
+#else
+inline bool injected_fault() { return false; }
+#endif
+
 // Double-buffered host pipeline resources of one device.
 struct Pipe {
     static constexpr int kDepth = 2;
@@ -397,7 +430,8 @@ constexpr uint64_t kChunkFramesMax = 1ull << 20;
 // Runs the chunked H2D -> kernel -> D2H pipeline of one device over frames [i0, i1).
 int run_host_job(DevState *ds, const HostJob &job) {
     std::lock_guard<std::mutex> lk(ds->pipe_mu);
-    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    DeviceGuard dg(ds->dev);
+    HIPTRY(dg.err, "hipSetDevice");
     int rc = ensure_pipe(ds, kChunkBytesHost + 2 * fcs::kSegBytes, kChunkFramesMax);
     if (rc) return rc;
     Pipe &pp = ds->pipe;
@@ -540,7 +574,8 @@ int ensure_small(DevState *ds) {
 int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t stride, const uint64_t *off,
                      const uint32_t *len, uint64_t n) {
     std::lock_guard<std::mutex> lk(ds->tx_mu);
-    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    DeviceGuard dg(ds->dev);
+    HIPTRY(dg.err, "hipSetDevice");
     if (!ds->tx_stream) {
         HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
         HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
@@ -609,18 +644,34 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
 
 // One frame of at most kOneBytes through fcs_one_kernel: the frame rides in the kernel arguments
 // and the FCS comes back in the calling thread's lane's mapped result word. Any host memory.
-int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
+uint32_t my_lane() {
     static std::atomic<uint32_t> next_thread{0};
     thread_local const uint32_t me = next_thread.fetch_add(1, std::memory_order_relaxed);
-    DevState::OneLane &L = ds->one_lane[me % DevState::kOneLanes];
+    return me % DevState::kOneLanes;
+}
+
+// Drop a lane whose last call failed: its stream and result word are recreated on next use, so a
+// stream left in an error state or a result word a stuck kernel may still write is never reused.
+void reset_lane(DevState *ds, DevState::OneLane &L) {
+    DeviceGuard dg(ds->dev);
+    if (L.st) (void)hipStreamDestroy(L.st);
+    if (L.flag) (void)hipHostFree(L.flag);
+    L.st = nullptr;
+    L.flag = L.dflag = nullptr;
+    L.seq = 0;
+    (void)hipGetLastError();
+    g_lane_resets.fetch_add(1, std::memory_order_relaxed);
+}
+
+int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc, uint32_t lane) {
+    DevState::OneLane &L = ds->one_lane[lane % DevState::kOneLanes];
     std::lock_guard<std::mutex> lk(L.mu);
-    int cur = 0;
-    HIPTRY(hipGetDevice(&cur), "hipGetDevice");
-    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
-    struct Restore {
-        int d;
-        ~Restore() { hipSetDevice(d); }
-    } restore{cur};
+    DeviceGuard dg(ds->dev);
+    HIPTRY(dg.err, "hipSetDevice");
+    if (injected_fault()) {
+        reset_lane(ds, L);
+        return fail(EIO, "single-frame kernel: injected fault (FCS_FAULT_HOOK build)");
+    }
     if (!L.st) {
         HIPTRY(hipStreamCreateWithFlags(&L.st, hipStreamNonBlocking), "hipStreamCreate");
         HIPTRY(hipHostMalloc(&L.flag, 64, hipHostMallocMapped), "hipHostMalloc(result word)");
@@ -636,7 +687,11 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
     uint8_t *win = reinterpret_cast<uint8_t *>(a.data);
     std::memset(win, 0, fcs::kOneBytes - bsize);
     if (bsize) std::memcpy(win + fcs::kOneBytes - bsize, data, bsize);
-    HIPTRY(fcs::launch_one(a, L.st), "launching the single-frame kernel");
+    if (const hipError_t le = fcs::launch_one(a, L.st); le != hipSuccess) {
+        const int r = hip_fail(le, "launching the single-frame kernel");
+        reset_lane(ds, L);
+        return r;
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 1;; i++) {
         const uint64_t v = __atomic_load_n(L.flag, __ATOMIC_ACQUIRE);
@@ -647,11 +702,19 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
         __builtin_ia32_pause();
         if ((i & 4095) == 0) {
             const hipError_t q = hipStreamQuery(L.st);
-            if (q == hipSuccess && (uint32_t)(__atomic_load_n(L.flag, __ATOMIC_ACQUIRE) >> 32) != a.seq)
+            if (q == hipSuccess && (uint32_t)(__atomic_load_n(L.flag, __ATOMIC_ACQUIRE) >> 32) != a.seq) {
+                reset_lane(ds, L);
                 return fail(EIO, "single-frame kernel finished without a result");
-            if (q != hipSuccess && q != hipErrorNotReady) return hip_fail(q, "single-frame kernel");
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10))
+            }
+            if (q != hipSuccess && q != hipErrorNotReady) {
+                const int r = hip_fail(q, "single-frame kernel");
+                reset_lane(ds, L);
+                return r;
+            }
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                reset_lane(ds, L);
                 return fail(ETIMEDOUT, "single-frame kernel: no result after 10 s");
+            }
         }
     }
 }
@@ -662,7 +725,8 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
 int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena_bytes, const uint64_t *off,
                              const uint32_t *len, uint8_t *ok, uint64_t n) {
     std::lock_guard<std::mutex> lk(ds->tx_mu);
-    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    DeviceGuard dg(ds->dev);
+    HIPTRY(dg.err, "hipSetDevice");
     if (!ds->tx_stream) {
         HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
         HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
@@ -759,13 +823,14 @@ int tx_one(uint8_t *frame, uint32_t len) {
     int rc = engine_devices(&devs);
     if (rc) return rc;
     uint32_t c = 0;
-    if ((rc = run_one(devs[0], frame, len, &c))) return rc;
+    if ((rc = run_one(devs[0], frame, len, &c, my_lane()))) return rc;
     std::memcpy(frame + len, &c, 4);
     return 0;
 }
 
 
-// Shard [0, n) over the engine devices (contiguous ranges, byte-balanced when lengths are known).
+// Shard [0, n) over the engine devices (contiguous ranges, byte-balanced when lengths are known:
+// fcs_shard_plan).
 int run_host_sharded(HostJob job, uint64_t n) {
     if (n == 0) return 0;
     std::vector<DevState *> devs;
@@ -773,19 +838,7 @@ int run_host_sharded(HostJob job, uint64_t n) {
     if (rc) return rc;
     const uint64_t G = std::min<uint64_t>(devs.size(), std::max<uint64_t>(1, n / 1024));
     std::vector<uint64_t> cut(G + 1, 0);
-    cut[G] = n;
-    if (job.len) {
-        uint64_t tot = 0;
-        for (uint64_t i = 0; i < n; i++) tot += job.len[i];
-        uint64_t acc = 0, g = 1;
-        for (uint64_t i = 0; i < n && g < G; i++) {
-            acc += job.len[i];
-            while (g < G && acc * G >= tot * g) cut[g++] = i + 1;
-        }
-        for (; g < G; g++) cut[g] = n;
-    } else {
-        for (uint64_t g = 1; g < G; g++) cut[g] = n * g / G;
-    }
+    if ((rc = fcs_shard_plan(job.len, n, (uint32_t)G, cut.data()))) return rc;
     if (G == 1) {
         job.i0 = 0;
         job.i1 = n;
@@ -812,6 +865,73 @@ int run_host_sharded(HostJob job, uint64_t n) {
     return 0;
 }
 
+// Frames over kOneBytes (no Ethernet frame is): copied into pinned, device-mapped staging and run
+// through the fixed-length kernels on the device's staging stream. On an error the staging stream
+// and words are dropped, so a retry starts from fresh ones.
+int run_staged(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
+    std::lock_guard<std::mutex> lk(ds->one_mu);
+    DeviceGuard dg(ds->dev);
+    HIPTRY(dg.err, "hipSetDevice");
+    auto reset = [ds] {
+        if (ds->one_stream) (void)hipStreamDestroy(ds->one_stream);
+        if (ds->one_hout) (void)hipHostFree(ds->one_hout);
+        if (ds->one_flag) (void)hipHostFree(ds->one_flag);
+        ds->one_stream = nullptr;
+        ds->one_hout = ds->one_dout = nullptr;
+        ds->one_flag = ds->one_dflag = nullptr;
+        (void)hipGetLastError();
+        g_lane_resets.fetch_add(1, std::memory_order_relaxed);
+    };
+    if (injected_fault()) {
+        reset();
+        return fail(EIO, "staged ether_fcs: injected fault (FCS_FAULT_HOOK build)");
+    }
+    int rc = 0;
+    hipError_t e = hipSuccess;
+    if (!ds->one_stream) {   // zero-copy: the kernel reads the frame and writes the FCS in pinned memory
+        if ((e = hipStreamCreateWithFlags(&ds->one_stream, hipStreamNonBlocking)) != hipSuccess ||
+            (e = hipHostMalloc(&ds->one_hout, 64, hipHostMallocMapped)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void **)&ds->one_dout, ds->one_hout, 0)) != hipSuccess ||
+            (e = hipHostMalloc(&ds->one_flag, 64, hipHostMallocMapped)) != hipSuccess ||
+            (e = hipHostGetDevicePointer((void **)&ds->one_dflag, ds->one_flag, 0)) != hipSuccess) {
+            rc = hip_fail(e, "staged ether_fcs: stream and result words");
+            reset();
+            return rc;
+        }
+        ds->one_flag[0] = ds->one_flag[1] = 0;
+        ds->one_seq = 0;
+    }
+    if (bsize > ds->one_cap) {
+        if (ds->one_h) (void)hipHostFree(ds->one_h);
+        ds->one_h = ds->one_hd = nullptr;
+        ds->one_cap = 0;
+        const uint64_t cap = std::max<uint64_t>(4096, bsize + 64);
+        HIPTRY(hipHostMalloc(&ds->one_h, cap, hipHostMallocMapped), "staged ether_fcs: hipHostMalloc");
+        HIPTRY(hipHostGetDevicePointer((void **)&ds->one_hd, ds->one_h, 0), "staged ether_fcs: map");
+        ds->one_cap = cap - 64;
+    }
+    std::memcpy(ds->one_h, data, bsize);
+    rc = launch_fixed(ds, ds->one_hd, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);
+    const uint64_t v = ++ds->one_seq;
+    if (!rc && (e = fcs::launch_signal(ds->one_dflag, v, ds->one_stream)) != hipSuccess)
+        rc = hip_fail(e, "staged ether_fcs: signal");
+    if (!rc) rc = wait_flag(ds->one_stream, ds->one_flag, v, "ether_fcs");
+    if (rc) {
+        reset();
+        return rc;
+    }
+    *crc = ds->one_hout[0];
+    return 0;
+}
+
+int dropin_attempt(const void *data, size_t bsize, uint32_t lane, uint32_t *crc) {
+    std::vector<DevState *> devs;
+    int rc = engine_devices(&devs);
+    if (rc) return rc;
+    if (bsize <= fcs::kOneBytes) return run_one(devs[0], data, bsize, crc, lane);
+    return run_staged(devs[0], data, bsize, crc);
+}
+
 }  // namespace
 
 // Pageable host bytes are copied into pinned staging before their DMA; one core copies
@@ -832,7 +952,8 @@ int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off
     if (rc) return rc;
     DevState *ds = devs[0];
     std::lock_guard<std::mutex> lk(ds->tx_mu);
-    HIPTRY(hipSetDevice(ds->dev), "hipSetDevice");
+    DeviceGuard dg(ds->dev);
+    HIPTRY(dg.err, "hipSetDevice");
     if ((rc = ensure_small(ds))) return rc;
     if (n <= fcs::kTxSmallMax) {   // the list fits the kernel arguments: one PCIe round trip less
         const std::vector<uint32_t> &kinit = kinit_table();
@@ -1149,66 +1270,64 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
     return rc ? rc : (int64_t)bad.load();
 }
 
-// Drop-in for src/ether_fcs.c:4. Synchronous, reentrant (per-device lock around the staging).
+// Drop-in for src/ether_fcs.c:4. Synchronous, reentrant. The reference cannot fail and has no
+// error channel (SURVEY.md §8b Errors), so an attempt that fails (HIP error, lost completion,
+// 10 s timeout) is retried once: the failed lane's stream and result word are dropped and the
+// frame goes through the next lane, freshly created. Only when the retry fails too (no GPU, a
+// sticky device error) does the call print the reason and abort — never return a wrong FCS.
+// There is no CPU CRC path to fall back to. Counters: fcs_engine_stats.
 uint32_t ether_fcs(const void *data, size_t bsize) {
     if (bsize == 0) return 0;   // src/ether_fcs.c: the loop does not run, crc stays 0
-    DevState *ds = nullptr;
-    int dev = 0;
-    int rc = 0;
-    {
-        std::vector<DevState *> devs;
-        rc = engine_devices(&devs);
-        if (!rc) ds = devs[0];
-    }
-    if (rc) {
-        std::fprintf(stderr, "nstack_fcs: ether_fcs: no usable GPU engine: %s\n", g_last_error.c_str());
+    g_dropin_calls.fetch_add(1, std::memory_order_relaxed);
+    if (bsize > 0xFFFFFFFFull) {   // the kernels take 32-bit frame lengths; never truncate
+        std::fprintf(stderr, "nstack_fcs: ether_fcs: %zu-byte buffer exceeds the 4 GiB frame limit\n", bsize);
         std::abort();
     }
-    if (bsize <= fcs::kOneBytes) {   // every Ethernet frame: one launch carrying the frame itself
-        uint32_t c = 0;
-        if ((rc = run_one(ds, data, bsize, &c))) {
-            std::fprintf(stderr, "nstack_fcs: ether_fcs: %s\n", g_last_error.c_str());
-            std::abort();
-        }
+    const uint32_t lane = my_lane();
+    uint32_t c = 0;
+    if (dropin_attempt(data, bsize, lane, &c) == 0) return c;
+    const std::string first = g_last_error;
+    g_dropin_retries.fetch_add(1, std::memory_order_relaxed);
+    if (dropin_attempt(data, bsize, lane + 1, &c) == 0) {
+        g_dropin_recovered.fetch_add(1, std::memory_order_relaxed);
+        g_last_error = "ether_fcs recovered after: " + first;
         return c;
     }
-    dev = ds->dev;
-    std::lock_guard<std::mutex> lk(ds->one_mu);
-    auto die = [](const char *what, hipError_t e) {
-        std::fprintf(stderr, "nstack_fcs: ether_fcs: %s: %s\n", what, hipGetErrorString(e));
-        std::abort();
-    };
-    int cur = 0;
-    hipError_t e = hipGetDevice(&cur);
-    if (e != hipSuccess) die("hipGetDevice", e);
-    if ((e = hipSetDevice(dev)) != hipSuccess) die("hipSetDevice", e);
-    if (!ds->one_stream) {   // zero-copy: the kernel reads the frame and writes the FCS in pinned memory
-        if ((e = hipStreamCreateWithFlags(&ds->one_stream, hipStreamNonBlocking)) != hipSuccess) die("stream", e);
-        if ((e = hipHostMalloc(&ds->one_hout, 64, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
-        if ((e = hipHostGetDevicePointer((void **)&ds->one_dout, ds->one_hout, 0)) != hipSuccess) die("map", e);
-        if ((e = hipHostMalloc(&ds->one_flag, 64, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
-        if ((e = hipHostGetDevicePointer((void **)&ds->one_dflag, ds->one_flag, 0)) != hipSuccess) die("map", e);
-        ds->one_flag[0] = ds->one_flag[1] = 0;
+    std::fprintf(stderr, "nstack_fcs: ether_fcs: %s (first attempt: %s); no usable GPU engine, aborting\n",
+                 g_last_error.c_str(), first.c_str());
+    std::abort();
+}
+
+void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t *dropin_recovered,
+                      uint64_t *lane_resets) {
+    if (dropin_calls) *dropin_calls = g_dropin_calls.load(std::memory_order_relaxed);
+    if (dropin_retries) *dropin_retries = g_dropin_retries.load(std::memory_order_relaxed);
+    if (dropin_recovered) *dropin_recovered = g_dropin_recovered.load(std::memory_order_relaxed);
+    if (lane_resets) *lane_resets = g_lane_resets.load(std::memory_order_relaxed);
+}
+
+#ifdef FCS_FAULT_HOOK
+void fcs_debug_fail_next(int attempts) { g_inject_faults = attempts; }
+#endif
+
+int fcs_shard_plan(const uint32_t *len, uint64_t n, uint32_t parts, uint64_t *cut) {
+    if (!cut || parts == 0) return fail(EINVAL, "fcs_shard_plan: bad arguments");
+    const uint64_t G = parts;
+    cut[0] = 0;
+    cut[G] = n;
+    if (len) {   // byte-balanced: cut g is the first index where the prefix reaches g/G of the bytes
+        uint64_t tot = 0;
+        for (uint64_t i = 0; i < n; i++) tot += len[i];
+        uint64_t acc = 0, g = 1;
+        for (uint64_t i = 0; i < n && g < G; i++) {
+            acc += len[i];
+            while (g < G && (unsigned __int128)acc * G >= (unsigned __int128)tot * g) cut[g++] = i + 1;
+        }
+        for (; g < G; g++) cut[g] = n;
+    } else {
+        for (uint64_t g = 1; g < G; g++) cut[g] = (uint64_t)((unsigned __int128)n * g / G);
     }
-    if (bsize > ds->one_cap) {
-        if (ds->one_h) hipHostFree(ds->one_h);
-        const uint64_t cap = std::max<uint64_t>(4096, bsize + 64);
-        if ((e = hipHostMalloc(&ds->one_h, cap, hipHostMallocMapped)) != hipSuccess) die("hipHostMalloc", e);
-        if ((e = hipHostGetDevicePointer((void **)&ds->one_hd, ds->one_h, 0)) != hipSuccess) die("map", e);
-        ds->one_cap = cap - 64;
-    }
-    std::memcpy(ds->one_h, data, bsize);
-    rc = launch_fixed(ds, ds->one_hd, bsize, (uint32_t)bsize, 1, ds->one_dout, ds->one_stream);
-    const uint64_t v = ++ds->one_seq;
-    if (!rc && (e = fcs::launch_signal(ds->one_dflag, v, ds->one_stream)) != hipSuccess) die("signal", e);
-    if (!rc) rc = wait_flag(ds->one_stream, ds->one_flag, v, "ether_fcs");
-    if (rc) {
-        std::fprintf(stderr, "nstack_fcs: ether_fcs: %s\n", g_last_error.c_str());
-        std::abort();
-    }
-    const uint32_t c = ds->one_hout[0];
-    hipSetDevice(cur);
-    return c;
+    return 0;
 }
 
 void *fcs_host_alloc(uint64_t bytes) {

@@ -1059,7 +1059,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
         // ---- window metadata: lane i <-> frame w0 + i ----
         const uint64_t f = w0 + lane;
         const bool act = f < p.n;
-        const uint32_t L = act ? p.len[f] : 0u;
+        const uint32_t L = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
         const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;   // off == null: slots of p.stride
         const bool small = act && L <= (uint32_t)kChunkBytes;
         const bool med = act && !small && L <= 8u * kChunkBytes;

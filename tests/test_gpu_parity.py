@@ -385,6 +385,31 @@ def test_concurrent_callers(dev, oracle):
     assert not errs, errs[:5]
 
 
+def test_host_calls_keep_the_callers_device(dev, oracle):
+    """Host-batch, TX and verify calls make their engine device current only for the call
+    (ADVICE r01): the calling thread's current device is unchanged afterwards."""
+    before = torch.cuda.current_device()
+    host = np.random.default_rng(3).integers(0, 256, 3000 * 1518, dtype=np.uint8)
+    out = np.zeros(3000, dtype=np.uint32)
+    na.fixed_host(host, 1518, 1518, 3000, out)
+    assert torch.cuda.current_device() == before
+    ln = np.full(3000, 1514, dtype=np.uint32)
+    tx = np.zeros(3000 * 1518, dtype=np.uint8)
+    na.tx_host(tx, 1518, ln, 3000)
+    assert torch.cuda.current_device() == before
+    buf = na.host_buffer(64 * 1518)
+    try:
+        lens = np.full(64, 1514, dtype=np.uint32)
+        na.tx_host(buf, 1518, lens, 64)
+        off = np.arange(64, dtype=np.uint64) * 1518
+        ok = np.zeros(64, dtype=np.uint8)
+        assert na.verify_host(buf, 64 * 1518, off, np.full(64, 1518, dtype=np.uint32), ok, 64) == 0
+    finally:
+        na.host_free(buf)
+    assert torch.cuda.current_device() == before
+    assert np.array_equal(out, oracle_fixed(oracle, host, 1518, 1518, 3000))
+
+
 def test_bad_arguments_are_rejected(dev):
     lib = na.load()
     assert lib.ether_fcs_fixed_dev(None, 1, 1, 1, None, None) == -22

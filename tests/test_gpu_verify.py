@@ -150,6 +150,26 @@ def test_verify_fixed_single_and_multi_segment(dev, oracle, L):
     assert int(bad.item()) == int((exp == 0).sum())
 
 
+@pytest.mark.parametrize("L", [64, 576, 1503])
+def test_verify_fixed_flat_route(dev, oracle, L):
+    """Fixed frames of <= 1503 B in batches of > 16384 take the flat chunk-stream kernel with no
+    length array (p.len == null) and the fused ok/bad epilogue: corrupted frames
+    included, ok[] and the bad count against the oracle."""
+    rng = np.random.default_rng(L + 1)
+    n = 20000
+    arena, off, ln = build_rx_batch(oracle, rng, [L] * n, corrupt_frac=0.05, gap_max=0)
+    base = int(off[0])
+    exp = expected_ok(oracle, arena, off, ln)
+    assert 0 < int((exp == 0).sum()) < n
+    ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    d = to_dev(arena, dev)
+    na.verify_fixed_dev(d.data_ptr() + base, L, L, n, ok, bad)
+    torch.cuda.synchronize()
+    assert np.array_equal(ok.cpu().numpy(), exp)
+    assert int(bad.item()) == int((exp == 0).sum())
+
+
 def test_verify_baseline_size_residue(dev):
     """4 M x 1518-B frames built on the device (FCS of bytes 0..1513 written LE at 1514): all pass;
     then k chosen frames get one bit flipped and exactly those fail (size-independent property)."""

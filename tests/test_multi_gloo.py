@@ -1,5 +1,8 @@
 """N > 1 path on CPU: two ranks over gloo (127.0.0.1) run bench.py's sharding and timing logic.
 
+The ranges come from the product's shard planner (fcs_shard_plan through bench.shard_range), for
+fixed-length frames and for a byte-balanced IMIX batch.
+
 Frames shard embarrassingly: each rank owns a contiguous slice of one global
 counter-based frame stream, computes its CRCs (here with the oracle — test infrastructure; on
 the GPU box the same ranges go to the HIP kernel), and the job reports all ranks' bytes over the
@@ -44,13 +47,35 @@ def _crcs(o, lo, hi):
     return out[:n]
 
 
-def _worker(rank, world, port, q):
+def _imix(n):
+    return np.random.default_rng(3).choice(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.uint32), n)
+
+
+def _crcs_var(o, ln, lo, hi):
+    """CRCs of frames [lo, hi) of a packed IMIX stream (frame i at the prefix sum of ln)."""
+    off = np.concatenate([[0], np.cumsum(ln, dtype=np.uint64)])
+    buf = np.empty(int(off[-1]) + 8, dtype=np.uint8)
+    o.oracle_splitmix_fill(buf.ctypes.data, int(off[-1]), SEED, 0)
+    out = np.zeros(max(hi - lo, 1), dtype=np.uint32)
+    o.oracle_fcs_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_size_t, ctypes.c_int]
+    if hi > lo:
+        o_ = np.ascontiguousarray(off[lo:hi], dtype=np.uint64)
+        l_ = np.ascontiguousarray(ln[lo:hi], dtype=np.uint32)
+        o.oracle_fcs_batch(buf.ctypes.data, o_.ctypes.data, l_.ctypes.data, out.ctypes.data, hi - lo, 1)
+    return out[:hi - lo]
+
+
+def _worker(rank, world, port, q, mode="fixed"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = _oracle()
-    lo, hi = bench.shard_range(TOTAL, world, rank)
+    if mode == "imix":
+        ln = _imix(TOTAL)
+        lo, hi = bench.shard_range(TOTAL, world, rank, ln)
+    else:
+        lo, hi = bench.shard_range(TOTAL, world, rank)
     dist.barrier()
-    crc = _crcs(o, lo, hi)
+    crc = _crcs_var(o, ln, lo, hi) if mode == "imix" else _crcs(o, lo, hi)
     elapsed = torch.tensor([0.5 + rank], dtype=torch.float64)   # synthetic per-rank times
     dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
     sizes = [None] * world
@@ -90,6 +115,26 @@ def test_two_rank_sharding_matches_single_pass(world):
     assert tmax == 0.5 + (world - 1)
     value, t = bench.aggregate([(s[1] - s[0]) * L for s in sizes], [0.5, 1.5])
     assert t == 1.5 and value == TOTAL * L / 1.5
+
+
+def test_two_rank_imix_byte_balanced_shards_match_single_pass():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "imix")) for r in range(world)]
+    for p in procs:
+        p.start()
+    sizes, _ = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ln = _imix(TOTAL)
+    assert sizes[0][0] == 0 and sizes[-1][1] == TOTAL and sizes[0][1] == sizes[1][0]
+    b0, b1 = int(ln[:sizes[0][1]].sum()), int(ln[sizes[0][1]:].sum())
+    assert abs(b0 - b1) <= 2 * 1518                      # byte-balanced cut from fcs_shard_plan
+    gathered = np.concatenate([np.array(s[2], dtype=np.uint32) for s in sizes])
+    assert np.array_equal(gathered, _crcs_var(_oracle(), ln, 0, TOTAL))
 
 
 def test_shard_ranges_cover_eight_gpus():
