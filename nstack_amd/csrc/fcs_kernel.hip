@@ -141,17 +141,6 @@ __device__ __forceinline__ uint32_t uniform_shift(const uint8_t *lds, uint32_t s
     return xor9(r, extra);
 }
 
-// uniform_shift with the table region as a value (an unrolled loop's index).
-__device__ __forceinline__ uint32_t uniform_shift_at(const uint8_t *lds, uint32_t region, uint32_t s, uint32_t extra) {
-    uint32_t r[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
-        r[t] = lds_rd(lds, ((sh & 0x3Cu) | region) + t * 64);
-    }
-    return xor9(r, extra);
-}
-
 // XOR over each 16-lane row (one frame); every lane of the row ends with the row's XOR.
 __device__ __forceinline__ uint32_t row_xor(uint32_t v) {
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
@@ -746,74 +735,146 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
 // kDmaMinLen..kDmaCover bytes, e.g. the 1518-B benchmark frames, when four consecutive frames fit
 // a 6 KiB slot: fixed_dma()).
 // A wave's item is four consecutive frames, as in fcs_single_kernel. The wave copies the item's
-// bytes into its own 6 KiB LDS slot with six global_load_lds_dwordx4 (each 1 KiB contiguous:
+// bytes into one of its LDS slots with six global_load_lds_dwordx4 (each 1 KiB contiguous:
 // coalesced rows, no VGPR destination, non-temporal since every line is read exactly once), then
 // lane c of each frame reads its 96-byte window [E - e_c - 96, E - e_c) from the slot (25 dwords,
-// realigned with v_alignbyte as before; the window offsets e_c = dma_end_off(c) put one frame's 16
-// windows on 16 distinct banks) and runs the same two slice-by-4 chains, A_48 merge, lane shift
-// A_{e_c} and row XOR as the other fixed kernels. One slot per wave: the next item's DMA is issued
-// as soon as this item's words are in registers, so it lands while the CRC work runs.
-// LDS: the 64 KiB conflict-free table set (one 256-B row per byte value: 4 tables x 16 replicas,
-// step4_l16), the lane tables, A_48, INV and the per-wave slots.
+// realigned with v_alignbyte; the window offsets e_c = dma_end_off(c) put one frame's 16 windows on
+// 16 distinct banks) and runs two slice-by-4 chains, the A_48 merge, the lane shift A_{e_c} and the
+// row XOR. kDmaSlots slots per wave: the DMA of item k + kDmaSlots is issued as soon as item k's
+// words are in registers, so it has kDmaSlots item periods to land (at one slot per wave it was
+// still late for ~27 % of each item: tools/stamps_dma.py).
+//
+// LDS (160 KiB): a 64 KiB table image of 256 rows of 256 B (row = byte value e) and the slots.
+//   row bytes [0, 128): slice tables, slot s = T_{3-s}[e] x 8 replicas (lookups: step4_l8);
+//   row bytes [128, 256) ("hole" e): hole 16 t + n = nibble n of the lane tables' table t for the
+//     32 lane slots; holes 128.. the chain-merge tables, then INV, then the verify counters.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kDmaLds16 = 0;                         // 65536: T3..T0 x 16 replicas
-constexpr uint32_t kDmaLane = 65536;                      // 16384: A_{e_c}, slot = lane & 31
 #ifndef FCS_DMA_CHAINS   // independent chains per lane window (2, 3, 4 or 6; measurement override)
 #define FCS_DMA_CHAINS 2
 #endif
 constexpr int kDmaChains = FCS_DMA_CHAINS;
 constexpr int kDmaChainWords = kChunkWords / kDmaChains;
 static_assert(kChunkWords % kDmaChains == 0 && kDmaChainWords % 2 == 0, "chains of an even word count");
-constexpr uint32_t kDmaMerge = kDmaLane + 16384;          // (kDmaChains - 1) x 512: A_{4 CL m}
-constexpr uint32_t kDmaInv = kDmaMerge + 512 * (kDmaChains - 1);   // 384
-constexpr uint32_t kDmaBad = kDmaInv + 384;               // 16 x 8
-constexpr uint32_t kDmaRing = kDmaBad + 128 + 64;         // 64-B pad: front windows may start before a slot
-constexpr uint32_t kDmaLdsBytes = kDmaRing + (kDmaWgThreads / 64) * kDmaItemBytes + 64;
-static_assert(kDmaRing % 16 == 0, "slots are 16-B aligned");
+constexpr uint32_t kDmaHole = 128;                                  // byte offset of a row's hole
+__host__ __device__ constexpr uint32_t dma_hole(uint32_t q) { return q * 256u + kDmaHole; }
+constexpr uint32_t kDmaMergeHole = 128;                             // 4 holes per merge table
+constexpr uint32_t kDmaInvHole = kDmaMergeHole + 4 * 5;             // 3 holes: INV[0..95]
+constexpr uint32_t kDmaBad = dma_hole(kDmaInvHole + 3);            // 16 x 8 B
+constexpr uint32_t kDmaRing = 65536;                                // slots start after the tables
+constexpr int kDmaWaves = kDmaWgThreads / 64;
+constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)(kDmaWaves * kDmaSlots) * kDmaItemBytes;
 static_assert(kDmaLdsBytes <= 163840, "LDS per CU");
+static_assert(kDmaChains - 1 <= 5, "merge holes");
 #ifndef FCS_DMA_AUX   // cache policy of the slot DMA (2 = nt; measurement-only override)
 #define FCS_DMA_AUX 2
 #endif
 
-// One slice-by-4 step against the 64 KiB table set: T_{3-s} lives in slot s of each 256-B row
-// (row = byte value, 16 replicas per slot, replica = lane & 15). ds_read_b32 banks are the dword
-// address mod 32, so slots s and s ^ 1 sit on opposite bank halves: lanes 16-31 of each 32-lane
-// group take the bytes in the order 1, 0, 3, 2 (rot) and look byte k ^ 1 up in slot k ^ 1, while
-// lanes 0-15 look byte k up in slot k; every lookup of a 32-lane group hits 32 distinct banks.
-// B[k] = replica * 4 + 64 * (k ^ (lane >> 4 & 1)): the per-lane slot rides in the v_perm base.
-__device__ __forceinline__ uint32_t step4_l16(const uint8_t *lds, uint32_t x, uint32_t wn, const uint32_t (&B)[4],
-                                              uint32_t rot) {
-    const uint32_t xr = __builtin_amdgcn_perm(x, x, rot);
-    const uint32_t t3 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[0], 0x0C0C0400u));
-    const uint32_t t2 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[1], 0x0C0C0500u));
-    const uint32_t t1 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[2], 0x0C0C0600u));
-    const uint32_t t0 = lds_rd(lds, kDmaLds16 + __builtin_amdgcn_perm(xr, B[3], 0x0C0C0700u));
+// One slice-by-4 step against the 32 KiB slice tables: T_{3-s}[e] at e * 256 + s * 32 + replica * 4
+// (replica = lane & 7). ds_read_b32 banks are the dword address mod 32, so the 4 slots x 8
+// replicas of a row are the 32 banks. Lane group h = (lane >> 3) & 3 looks byte k ^ h up in slot
+// k ^ h at its k-th lookup, so the four 8-lane groups of a 32-lane access use four different
+// slots and every lookup hits 32 distinct banks. Byte and slot are per-lane constants of the
+// v_perm that forms the address: selector SEL[k] picks byte k ^ h of x, base B[k] = replica * 4 +
+// 32 * (k ^ h).
+__device__ __forceinline__ uint32_t step4_l8(const uint8_t *lds, uint32_t x, uint32_t wn, const uint32_t (&B)[4],
+                                             const uint32_t (&SEL)[4]) {
+#ifdef FCS_DMA_ABL_NOLDS   // measurement-only: lookups replaced by VALU on the addresses (wrong FCS)
+    const uint32_t a0 = __builtin_amdgcn_perm(x, B[0], SEL[0]), a1 = __builtin_amdgcn_perm(x, B[1], SEL[1]);
+    const uint32_t a2 = __builtin_amdgcn_perm(x, B[2], SEL[2]), a3 = __builtin_amdgcn_perm(x, B[3], SEL[3]);
+    return xor3(xor3(a0, a1 << 3, a2 >> 1), a3 << 7, wn);
+#else
+    const uint32_t t3 = lds_rd(lds, __builtin_amdgcn_perm(x, B[0], SEL[0]));
+    const uint32_t t2 = lds_rd(lds, __builtin_amdgcn_perm(x, B[1], SEL[1]));
+    const uint32_t t1 = lds_rd(lds, __builtin_amdgcn_perm(x, B[2], SEL[2]));
+    const uint32_t t0 = lds_rd(lds, __builtin_amdgcn_perm(x, B[3], SEL[3]));
     return xor3(xor3(t3, t2, t1), t0, wn);
+#endif
 }
 
+// A_{e_c}(s) from the lane tables in the holes: nibble n of table t at hole 16 t + n, slot lane & 31.
+__device__ __forceinline__ uint32_t lane_shift_dma(const uint8_t *lds, uint32_t s, uint32_t lanebase) {
+    uint32_t r[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 8) ? (s >> (4 * t - 8)) : (s << (8 - 4 * t));
+        r[t] = lds_rd(lds, ((sh & 0xF00u) | lanebase) + (uint32_t)t * 4096u);
+    }
+    return xor9(r, 0u);
+}
+
+// Merge table m (A_{4 CL (m + 1)}): nibble table t at hole kDmaMergeHole + 4 m + t / 2, +64 (t odd).
+__device__ __forceinline__ uint32_t merge_shift_dma(const uint8_t *lds, int m, uint32_t s, uint32_t extra) {
+    uint32_t r[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        const uint32_t base = dma_hole(kDmaMergeHole + 4u * (uint32_t)m + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1);
+        r[t] = lds_rd(lds, (sh & 0x3Cu) | base);
+    }
+    return xor9(r, extra);
+}
+
+// The slot DMA: six 1 KiB rows from two address registers. The instruction's offset (13-bit,
+// 0 .. 3 KiB here) applies to the global AND the LDS address, so each group of rows passes the
+// same LDS base (one M0 value).
 __device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int lane) {
     typedef __attribute__((address_space(3))) void lds_void;
-#pragma unroll
-    for (int i = 0; i < (int)(kDmaItemBytes / 1024); i++)
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(src + 1024 * i + 16 * lane),
-                                         (lds_void *)(slot + 1024 * i), 16, 0, FCS_DMA_AUX);
+    static_assert(kDmaItemBytes == 6 * 1024, "six rows");
+    const uint64_t a = src + 16 * (uint64_t)lane, b = a + 4096;
+    lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_AUX);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_AUX);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
 }
 
+// Wait until item k's slot DMA has landed. Vector-memory operations retire in issue order; younger
+// than item k's six rows are the result stores of items k-2 and k-1 (at least one instruction per
+// item: lane 15 of the item's first frame always stores) and, when it exists, item k+1's DMA (two
+// slots per wave). One slot per wave: everything outstanding is older than the next DMA.
+__device__ __forceinline__ void wait_slot(bool next_inflight, uint32_t k) {
+    if (kDmaSlots == 1) {
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+        return;
+    }
+    const uint32_t st = k >= 2 ? 2u : k;      // result stores issued since item k's DMA
+    if (next_inflight) {
+        if (st == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | 8);
+        else if (st == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | 7);
+        else __builtin_amdgcn_s_waitcnt(0x0F70 | 6);
+    } else {
+        if (st == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | 2);
+        else if (st == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | 1);
+        else __builtin_amdgcn_s_waitcnt(0x0F70);
+    }
+}
+
+// MW: words a front mask can touch (host-selected: 2 when the front lane masks at most 8 bytes,
+// i.e. len >= 1516, else kSingleMaskWords).
+template <int MW>
 __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
     const int tid = threadIdx.x;
-    // ---- tables: LDS16 slice tables, lane tables A_{e_c}, A_48, INV ----
-    for (int i = tid; i < 4096; i += kDmaWgThreads) {   // row e = i >> 4; 16-B store q = i & 15 -> slot q >> 2
-        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)];
+    // ---- table image: slice tables (16-B stores of one value: 4 replicas), lane tables, merge
+    //      tables, INV ----
+    for (int i = tid; i < 2048; i += kDmaWgThreads) {   // row e = i >> 3; store j = i & 7 -> slot j >> 1
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(lds + kDmaLds16 + (uint32_t)i * 16) = vv;
+        *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
     }
-    for (int i = tid; i < 4096; i += kDmaWgThreads)
-        reinterpret_cast<uint32_t *>(lds + kDmaLane)[i] = p.blob[kBlobLaneDma + i];
-    for (int i = tid; i < 128 * (kDmaChains - 1); i += kDmaWgThreads)   // merge table m = A_{4 CL (m + 1)}
-        reinterpret_cast<uint32_t *>(lds + kDmaMerge)[i] =
-            p.blob[kBlobMerge + ((i >> 7) + 1) * (kDmaChainWords / 2) * 128 - 128 + (i & 127)];
-    for (int i = tid; i < kChunkBytes; i += kDmaWgThreads) reinterpret_cast<uint32_t *>(lds + kDmaInv)[i] = p.blob[kBlobInv + i];
+    for (int i = tid; i < 4096; i += kDmaWgThreads)   // [t][n][slot]: hole 16 t + n
+        *reinterpret_cast<uint32_t *>(lds + dma_hole((uint32_t)i >> 5) + (uint32_t)(i & 31) * 4u) = p.blob[kBlobLaneDma + i];
+    for (int i = tid; i < 128 * (kDmaChains - 1); i += kDmaWgThreads) {   // merge table m = A_{4 CL (m + 1)}
+        const int m = i >> 7, t = (i >> 4) & 7, e = i & 15;
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaMergeHole + 4u * (uint32_t)m + (uint32_t)(t >> 1)) +
+                                      64u * (uint32_t)(t & 1) + 4u * (uint32_t)e) =
+            p.blob[kBlobMerge + ((m + 1) * (kDmaChainWords / 2) - 1) * 128 + (i & 127)];
+    }
+    for (int i = tid; i < kChunkBytes; i += kDmaWgThreads)
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
+            p.blob[kBlobInv + i];
     init_bad<kDmaBad>(lds);
     __syncthreads();
 
@@ -821,25 +882,27 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     const int c = lane & (kGroup - 1);     // chunk index back from the frame end
     const int g = lane >> 4;               // frame of the item
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
-    const uint32_t jl = (uint32_t)(lane >> 4) & 1u;
-    const uint32_t B[4] = {(uint32_t)(lane & 15) * 4u + 64u * (0u ^ jl), (uint32_t)(lane & 15) * 4u + 64u * (1u ^ jl),
-                           (uint32_t)(lane & 15) * 4u + 64u * (2u ^ jl), (uint32_t)(lane & 15) * 4u + 64u * (3u ^ jl)};
-    const uint32_t rot = jl ? 0x02030001u : 0x03020100u;
-    const uint32_t lanebase = kDmaLane | ((uint32_t)(lane & 31) * 4u);
+    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)(wave * kDmaSlots) * kDmaItemBytes;
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
 
     // loop invariants: window offset within the item, front masks, INV start of the front lane
     const uint32_t ec = dma_end_off(c);
     const int64_t klane = (int64_t)g * (int64_t)p.stride + (int64_t)p.flen - (int64_t)ec - kChunkBytes;
     const int zc = (c == kGroup - 1) ? (int)(kDmaCover - p.flen) : (dma_short_lane(c) ? 4 : 0);
-    uint32_t m[kSingleMaskWords];
+    static_assert(MW >= 1 && MW <= kSingleMaskWords, "mask words");
+    uint32_t m[MW];
 #pragma unroll
-    for (int i = 0; i < kSingleMaskWords; i++) {
+    for (int i = 0; i < MW; i++) {
         int t = zc - 4 * i;
         t = t < 0 ? 0 : (t > 4 ? 4 : t);
         m[i] = (uint32_t)(0xFFFFFFFFull << (8 * t));
     }
-    const uint32_t x0 = (c == kGroup - 1) ? lds_rd(lds, kDmaInv + 4u * (uint32_t)zc) : 0u;
+    const uint32_t x0 = (c == kGroup - 1) ? lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zc / 32u) + (uint32_t)(zc % 32) * 4u)
+                                          : 0u;
 
     const uint64_t lo16 = p.lo4 & ~15ull;
     const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start inside the arena
@@ -848,61 +911,112 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         return a < lo16 ? lo16 : (a > smax ? smax : a);
     };
     const uint64_t Q = (uint64_t)gridDim.x * (kDmaWgThreads / 16);   // frames per sweep of the grid
-    uint64_t f = ((uint64_t)blockIdx.x * (kDmaWgThreads / 64) + (uint64_t)wave) * 4;
+    uint64_t f = ((uint64_t)blockIdx.x * (kDmaWaves) + (uint64_t)wave) * 4;
     const uint64_t dS = Q * p.stride;
     uint64_t S = p.base + f * p.stride;    // first frame of the item
-    if (f < p.n) dma_item(slot, slot_src(S), lane);
+#pragma unroll
+    for (int j = 0; j < kDmaSlots; j++)
+        if (f + (uint64_t)j * Q < p.n) dma_item(slot0 + j * kDmaItemBytes, slot_src(S + (uint64_t)j * dS), lane);
 
-    while (f < p.n) {   // wave-uniform
+#ifdef FCS_STAMPS   // measurement-only: per-wave cycles waiting for the slot vs. the whole item
+    uint64_t st_wait = 0, st_all = 0, st_items = 0;
+    const uint64_t st_rt0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
+#endif
+    for (uint32_t k = 0; f < p.n; k++) {   // wave-uniform
+        const uint8_t *slot = slot0 + (kDmaSlots == 1 ? 0u : (k & 1u) * kDmaItemBytes);
         const uint64_t src = slot_src(S);
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot DMA has landed
-        const int64_t x = (int64_t)(S - src) + klane;   // window start within the slot (>= -31)
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        wait_slot(f + Q < p.n, k);
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts1 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+        st_wait += ts1 - ts0;
+#endif
+        const int64_t x = (int64_t)(S - src) + klane;   // window start within the slot (>= -28)
         const uint32_t r = (uint32_t)x & 3u;
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
         uint32_t d[kChunkWords + 1];
 #pragma unroll
-        for (int q = 0; q <= kChunkWords; q++) d[q] = wp[q];
+        for (int q = 0; q < kChunkWords; q++) d[q] = wp[q];
+        {   // the 25th dword matters only when r != 0; then it lies inside the slot. Clamped so the
+            // last slot in LDS is never read past its end.
+            const uint64_t a24 = (uint64_t)(wp + kChunkWords), lim = (uint64_t)(slot + kDmaItemBytes - 4);
+            d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
+        }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
         const uint64_t fn = f + Q;
         const uint64_t Sn = S + dS;
-        if (fn < p.n) dma_item(slot, slot_src(Sn), lane);
+        if (f + (uint64_t)kDmaSlots * Q < p.n) dma_item(slot, slot_src(S + (uint64_t)kDmaSlots * dS), lane);
 
 #ifdef FCS_DMA_NOCRC   // measurement-only build: slot DMA and window reads, no CRC work (wrong FCS)
         {
             uint32_t acc = r;
 #pragma unroll
             for (int q = 0; q <= kChunkWords; q++) acc ^= d[q];
-            if (acc == 0x12345678u) p.out[f] = acc;
+            p.out[f] = acc;   // one store per item, as the product (keeps wait_slot's count)
             f = fn;
             S = Sn;
+#ifdef FCS_STAMPS
+            st_all += __builtin_amdgcn_s_memtime() - ts0;
+            st_items++;
+#endif
             continue;
         }
 #endif
         uint32_t w[kChunkWords];
 #pragma unroll
+#ifdef FCS_DMA_ABL_NOALIGN   // measurement-only: no realignment (wrong FCS unless r == 0)
+        for (int i = 0; i < kChunkWords; i++) w[i] = d[i] ^ (i == 0 ? r : 0u);
+#else
         for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#endif
 #pragma unroll
-        for (int i = 0; i < kSingleMaskWords; i++)
-            if (4 * i < (int)p.zmax) w[i] &= m[i];
+        for (int i = 0; i < MW; i++) w[i] &= m[i];
         // kDmaChains independent chains of CL words; chain h ends 4 CL (kDmaChains - 1 - h) bytes
         // before the window end, so the window value is XOR_h A_{4 CL (kDmaChains - 1 - h)}(chain h)
         constexpr int CL = kDmaChainWords;
         uint32_t xs[kDmaChains];
 #pragma unroll
-        for (int h = 0; h < kDmaChains; h++) xs[h] = w[h * CL] ^ (h == 0 ? x0 : 0u);
+        for (int hh = 0; hh < kDmaChains; hh++) xs[hh] = w[hh * CL] ^ (hh == 0 ? x0 : 0u);
 #pragma unroll
         for (int i = 0; i < CL; i++)
 #pragma unroll
-            for (int h = 0; h < kDmaChains; h++) xs[h] = step4_l16(lds, xs[h], i < CL - 1 ? w[h * CL + i + 1] : 0u, B, rot);
+            for (int hh = 0; hh < kDmaChains; hh++)
+                xs[hh] = step4_l8(lds, xs[hh], i < CL - 1 ? w[hh * CL + i + 1] : 0u, B, SEL);
         uint32_t mv = xs[kDmaChains - 1];
 #pragma unroll
-        for (int h = 0; h < kDmaChains - 1; h++) mv = uniform_shift_at(lds, kDmaMerge + 512u * (uint32_t)(kDmaChains - 2 - h), xs[h], mv);
-        uint32_t v = lane_shift(lds, mv, lanebase);
+        for (int hh = 0; hh < kDmaChains - 1; hh++) mv = merge_shift_dma(lds, kDmaChains - 2 - hh, xs[hh], mv);
+        uint32_t v = lane_shift_dma(lds, mv, lanebase);
         v = row_xor(v);
         emit<kDmaBad>(p, lds, c == kGroup - 1 && f + g < p.n, f + g, ~v);
         f = fn;
         S = Sn;
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        st_all += __builtin_amdgcn_s_memtime() - ts0;
+        st_items++;
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
+#ifdef FCS_STAMPS
+    if (p.dbg != nullptr && lane == 0) {
+        const uint32_t wv = blockIdx.x * kDmaWaves + (uint32_t)wave;
+        p.dbg[wv * 8 + 0] = st_wait;
+        p.dbg[wv * 8 + 1] = st_all;
+        p.dbg[wv * 8 + 2] = st_items;
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        p.dbg[wv * 8 + 3] = rt1 - st_rt0;
+        p.dbg[wv * 8 + 4] = __builtin_amdgcn_s_memtime() - st_c0;
+        p.dbg[wv * 8 + 5] = st_rt0;
+        p.dbg[wv * 8 + 6] = rt1;
+        p.dbg[wv * 8 + 7] = __builtin_amdgcn_s_getreg(/*HW_REG_XCC_ID*/ (20 << 0) | (0 << 6) | (3 << 11));
+    }
+#endif
     flush_bad<kDmaBad>(p, lds);
 }
 
@@ -1582,7 +1696,8 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #endif
         }
     } else if (!tiny && fixed_dma(p)) {
-        hipLaunchKernelGGL(fcs_dma_kernel, dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+        if (p.zmax <= 8) hipLaunchKernelGGL(fcs_dma_kernel<2>, dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+        else hipLaunchKernelGGL(fcs_dma_kernel<kSingleMaskWords>, dim3(grid), dim3(kDmaWgThreads), 0, st, p);
     } else if (tiny) {
         if (single) FCS_LAUNCH(false, true, true);
         else FCS_LAUNCH(false, true, false);

@@ -109,11 +109,16 @@ inline bool fixed_single(const KParams &p) {
 // consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
 // frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
 // and the arena must hold a whole slot (the last items' slots are clamped to its end).
-#ifndef FCS_DMA_WG_THREADS   // measurement-only override
-#define FCS_DMA_WG_THREADS 768
+#ifndef FCS_DMA_WG_THREADS   // measurement-only overrides
+#define FCS_DMA_WG_THREADS 1024
+#endif
+#ifndef FCS_DMA_SLOTS
+#define FCS_DMA_SLOTS 1
 #endif
 constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;
-static_assert(kDmaWgThreads % 64 == 0 && kDmaWgThreads <= 768, "LDS holds at most 12 wave slots");
+constexpr int kDmaSlots = FCS_DMA_SLOTS;           // 6 KiB LDS slots per wave (items in flight)
+static_assert(kDmaWgThreads % 64 == 0 && (kDmaSlots == 1 || kDmaSlots == 2) &&
+              (kDmaWgThreads / 64) * kDmaSlots <= 16, "LDS holds 16 slots next to the 64 KiB tables");
 inline bool fixed_dma(const KParams &p) {
 #ifdef FCS_NO_DMA   // measurement-only build
     return false;

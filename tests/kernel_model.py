@@ -152,44 +152,58 @@ def dma_short_lane(c):
 
 BLOB_MERGE = BLOB_LANE_DMA + 8 * 16 * 32
 DMA_CHAINS = 2                    # fcs_kernel.hip FCS_DMA_CHAINS default
-DMA_MERGE = 81920
-DMA_INV = DMA_MERGE + 512 * (DMA_CHAINS - 1)
+MERGE_HOLE, INV_HOLE = 128, 128 + 4 * 5
+
+
+def hole(q):
+    """Byte offset of hole q: the upper 128 B of row q of the DMA kernel's table image."""
+    return q * 256 + 128
 
 
 def build_lds_dma(blob, chains=DMA_CHAINS):
-    """The DMA kernel's table image: LDS16 slice tables at 0, A_{e_c} lane tables at 65536, the
-    chain-merge tables A_{4 CL m} (m = 1 .. chains-1) at 81920, INV after them (byte offsets, as
-    fcs_dma_kernel stages them)."""
+    """fcs_dma_kernel's 64 KiB table image (byte offsets as the kernel stages them): row e = 256 B;
+    bytes [0,128) slot s = T_{3-s}[e] x 8 replicas; hole 16t+n = lane-table t nibble n for the 32
+    lane slots; holes MERGE_HOLE.. the chain-merge tables A_{4 CL m}; INV after them."""
     cl = 24 // chains
-    inv = DMA_MERGE + 512 * (chains - 1)
-    lds = np.zeros((inv + 384) // 4, dtype=np.uint32)
+    lds = np.zeros(65536 // 4, dtype=np.uint32)
+    for e in range(256):
+        for sl in range(4):
+            lds[(e * 256 + sl * 32) // 4:(e * 256 + sl * 32) // 4 + 8] = blob[BLOB_SLICE + 256 * (3 - sl) + e]
     for i in range(4096):
-        v = blob[BLOB_SLICE + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)]
-        lds[i * 4:i * 4 + 4] = v
-    lds[65536 // 4:65536 // 4 + 4096] = blob[BLOB_LANE_DMA:BLOB_LANE_DMA + 4096]
+        lds[(hole(i >> 5) + (i & 31) * 4) // 4] = blob[BLOB_LANE_DMA + i]
     for m in range(chains - 1):
         k = (cl // 2) * (m + 1)          # A_{8k}
-        lds[(DMA_MERGE + 512 * m) // 4:(DMA_MERGE + 512 * m) // 4 + 128] = \
-            blob[BLOB_MERGE + (k - 1) * 128:BLOB_MERGE + k * 128]
-    lds[inv // 4:inv // 4 + 96] = blob[BLOB_INV:BLOB_INV + 96]
+        for t in range(8):
+            for e in range(16):
+                lds[(hole(MERGE_HOLE + 4 * m + (t >> 1)) + 64 * (t & 1) + 4 * e) // 4] = \
+                    blob[BLOB_MERGE + (k - 1) * 128 + t * 16 + e]
+    for z in range(96):
+        lds[(hole(INV_HOLE + z // 32) + (z % 32) * 4) // 4] = blob[BLOB_INV + z]
     return lds
 
 
-def step4_l16(lds, x, lane):
-    jl = (lane >> 4) & 1
-    B = [(lane & 15) * 4 + 64 * (k ^ jl) for k in range(4)]
-    xr = v_perm(x, x, 0x02030001 if jl else 0x03020100)
+def step4_l8(lds, x, lane):
+    """fcs_dma_kernel's step4_l8: lane group h = (lane >> 3) & 3 looks byte k ^ h up in slot k ^ h."""
+    h = (lane >> 3) & 3
     r = 0
     for k in range(4):
-        r ^= int(lds[v_perm(xr, B[k], 0x0C0C0400 + (k << 8)) // 4])
+        B = (lane & 7) * 4 + 32 * (k ^ h)
+        r ^= int(lds[v_perm(x, B, 0x0C0C0400 + ((k ^ h) << 8)) // 4])
     return r
 
 
-def lds16_banks(lane, x, k):
-    """Bank (dword address mod 32) of lane's lookup k of word x in the DMA kernel's table set."""
-    jl = (lane >> 4) & 1
-    xr = v_perm(x, x, 0x02030001 if jl else 0x03020100)
-    return (v_perm(xr, (lane & 15) * 4 + 64 * (k ^ jl), 0x0C0C0400 + (k << 8)) // 4) % 32
+def l8_banks(lane, x, k):
+    """Bank (dword address mod 32) of lane's lookup k of word x in the DMA kernel's slice tables."""
+    h = (lane >> 3) & 3
+    return (v_perm(x, (lane & 7) * 4 + 32 * (k ^ h), 0x0C0C0400 + ((k ^ h) << 8)) // 4) % 32
+
+
+def merge_shift(lds, m, s):
+    r = 0
+    for t in range(8):
+        sh = (s >> (4 * t - 2)) if 4 * t >= 2 else ((s << 2) & 0xFFFFFFFF)
+        r ^= int(lds[((sh & 0x3C) | (hole(MERGE_HOLE + 4 * m + (t >> 1)) + 64 * (t & 1))) // 4])
+    return r
 
 
 def model_dma_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f: int, garbage: bytes,
@@ -207,7 +221,6 @@ def model_dma_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f
     img[64:64 + len(chunk)] = chunk
     zmax = max(4, DMA_COVER - flen)
     cl = 24 // chains
-    inv = DMA_MERGE + 512 * (chains - 1)
     out = []
     for g in range(4):
         regs = []
@@ -224,19 +237,19 @@ def model_dma_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f
                 if 4 * i < zmax:
                     t = max(0, min(4, zc - 4 * i))
                     w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
-            x0 = int(lds[(inv + 4 * zc) // 4]) if c == 15 else 0
+            x0 = int(lds[(hole(INV_HOLE + zc // 32) + (zc % 32) * 4) // 4]) if c == 15 else 0
             xs = [w[h * cl] ^ (x0 if h == 0 else 0) for h in range(chains)]
             for i in range(cl):
                 for h in range(chains):
-                    xs[h] = step4_l16(lds, xs[h], lane) ^ (w[h * cl + i + 1] if i < cl - 1 else 0)
+                    xs[h] = step4_l8(lds, xs[h], lane) ^ (w[h * cl + i + 1] if i < cl - 1 else 0)
             m = xs[chains - 1]
             for h in range(chains - 1):
-                m = uniform_shift(lds, xs[h], DMA_MERGE + 512 * (chains - 2 - h)) ^ m
-            lanebase = 65536 | ((lane & 31) * 4)
+                m = merge_shift(lds, chains - 2 - h, xs[h]) ^ m
+            lanebase = 128 + (lane & 31) * 4
             s = 0
             for t in range(8):
-                sh = (m >> (4 * t - 7)) if 4 * t >= 7 else ((m << (7 - 4 * t)) & 0xFFFFFFFF)
-                s ^= int(lds[(((sh & 0x780) | lanebase) + t * 2048) // 4])
+                sh = (m >> (4 * t - 8)) if 4 * t >= 8 else ((m << (8 - 4 * t)) & 0xFFFFFFFF)
+                s ^= int(lds[(((sh & 0xF00) | lanebase) + t * 4096) // 4])
             regs.append(s)
         v = 0
         for s in regs:

@@ -126,7 +126,7 @@ def lds_dma():
 @pytest.mark.parametrize("chains", [2, 3, 4, 6])
 @pytest.mark.parametrize("flen,extra", [(1496, 0), (1514, 4), (1518, 0), (1518, 2), (1520, 0), (1524, 0), (1524, 12)])
 def test_dma_kernel_model(lds_dma, flen, extra, chains):
-    """fcs_dma_kernel's decomposition (LDS16 tables with the half-wave rotation, 6 KiB slots clamped
+    """fcs_dma_kernel's decomposition (32 KiB slice tables looked up in per-group byte order, 6 KiB slots clamped
     at the arena end, 92-B chunks at c = 3/7/11, front mask and INV of lane 15, the chains and
     their one-step merge for every FCS_DMA_CHAINS value, A_{e_c} lane shift)
     replayed on the CPU for every item of small batches at all four base alignments, against zlib."""
@@ -158,4 +158,4 @@ def test_dma_table_lookups_bank_distinct():
     for _ in range(200):
         xs = [rng.getrandbits(32) for _ in range(32)]
         for k in range(4):
-            assert len({km.lds16_banks(l, xs[l], k) for l in range(32)}) == 32
+            assert len({km.l8_banks(l, xs[l], k) for l in range(32)}) == 32
