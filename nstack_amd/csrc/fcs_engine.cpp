@@ -113,6 +113,11 @@ struct DevState {
     uint32_t *d_blob = nullptr;
     uint32_t *d_one_blob = nullptr;   // tables of the single-frame kernel (drop-in ether_fcs)
     uint32_t *d_kinit = nullptr;      // kinit_table() in device memory (mapped-list kernel)
+    // Dynamic-tail counters of the LDS-DMA kernel: a ring of kCtrSlots, one 64-B line each; a
+    // large fixed launch takes the next slot and zeroes it on its own stream before the kernel.
+    static constexpr uint32_t kCtrSlots = 256;
+    unsigned long long *d_ctr = nullptr;
+    std::atomic<uint32_t> ctr_seq{0};
     std::mutex pipe_mu;      // one host pipeline at a time per device
     Pipe pipe;
     std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
@@ -200,6 +205,8 @@ int dev_state(int dev, DevState **out) {
         const std::vector<uint32_t> &ki = kinit_table();
         if (ae == hipSuccess) ae = hipMalloc(&st->d_kinit, ki.size() * 4);
         if (ae == hipSuccess) ae = hipMemcpy(st->d_kinit, ki.data(), ki.size() * 4, hipMemcpyHostToDevice);
+        if (ae == hipSuccess) ae = hipMalloc(&st->d_ctr, DevState::kCtrSlots * 64);
+        if (ae == hipSuccess) ae = hipMemset(st->d_ctr, 0, DevState::kCtrSlots * 64);
         hipSetDevice(cur);
         if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
         g_dev[dev] = std::move(st);
@@ -281,9 +288,17 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         HIPTRY(fcs::launch_fcs(true, true, p, grid_for(ds, n, fcs::kWgThreads), st), "launching fcs_flat_kernel<fixed>");
         return 0;
     }
-    if (fcs::fixed_dma(p))   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
+    const int grid = grid_for(ds, n, fcs::fixed_threads(p));
+    if (fcs::fixed_dma(p)) {   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
         p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
-    HIPTRY(fcs::launch_fcs(false, false, p, grid_for(ds, n, fcs::fixed_threads(p)), st), "launching fcs_kernel<fixed>");
+        const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
+        if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic tail
+            const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
+            p.ctr = ds->d_ctr + 8 * slot;
+            HIPTRY(hipMemsetAsync(p.ctr, 0, 8, st), "zeroing the work counter");
+        }
+    }
+    HIPTRY(fcs::launch_fcs(false, false, p, grid, st), "launching fcs_kernel<fixed>");
     return 0;
 }
 
@@ -1119,6 +1134,7 @@ void fcs_engine_fini(void) {
         if (ds->d_blob) hipFree(ds->d_blob);
         if (ds->d_one_blob) hipFree(ds->d_one_blob);
         if (ds->d_kinit) hipFree(ds->d_kinit);
+        if (ds->d_ctr) hipFree(ds->d_ctr);
     }
     g_dev.clear();
     g_engine_devs.clear();

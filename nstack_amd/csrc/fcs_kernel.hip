@@ -740,9 +740,13 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
 // lane c of each frame reads its 96-byte window [E - e_c - 96, E - e_c) from the slot (25 dwords,
 // realigned with v_alignbyte; the window offsets e_c = dma_end_off(c) put one frame's 16 windows on
 // 16 distinct banks) and runs two slice-by-4 chains, the A_48 merge, the lane shift A_{e_c} and the
-// row XOR. kDmaSlots slots per wave: the DMA of item k + kDmaSlots is issued as soon as item k's
-// words are in registers, so it has kDmaSlots item periods to land (at one slot per wave it was
-// still late for ~27 % of each item: tools/stamps_dma.py).
+// row XOR. One slot per wave, 16 waves per CU: the DMA of a wave's next item is issued as soon as
+// the current item's words are in registers, so it lands while the CRC work runs.
+// Items: a static interleaved share (item wid + k W for wave wid of W) and, for large batches
+// (p.ctr != null), a dynamic tail: the remaining items are handed out in chunks by a device
+// counter, chunk sizes shrinking with the work left (guided), the next chunk requested one chunk
+// ahead. Without it the waves' finishing times spread over 18 % of the kernel (slower XCDs and
+// CUs), and the kernel ends with the slowest (tools/stamps_dma.py).
 //
 // LDS (160 KiB): a 64 KiB table image of 256 rows of 256 B (row = byte value e) and the slots.
 //   row bytes [0, 128): slice tables, slot s = T_{3-s}[e] x 8 replicas (lookups: step4_l8);
@@ -762,11 +766,14 @@ constexpr uint32_t kDmaInvHole = kDmaMergeHole + 4 * 5;             // 3 holes: 
 constexpr uint32_t kDmaBad = dma_hole(kDmaInvHole + 3);            // 16 x 8 B
 constexpr uint32_t kDmaRing = 65536;                                // slots start after the tables
 constexpr int kDmaWaves = kDmaWgThreads / 64;
-constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)(kDmaWaves * kDmaSlots) * kDmaItemBytes;
+constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)kDmaWaves * kDmaItemBytes;
 static_assert(kDmaLdsBytes <= 163840, "LDS per CU");
 static_assert(kDmaChains - 1 <= 5, "merge holes");
 #ifndef FCS_DMA_AUX   // cache policy of the slot DMA (2 = nt; measurement-only override)
 #define FCS_DMA_AUX 2
+#endif
+#ifndef FCS_DMA_DYN_PCT   // share of the items handed out dynamically when p.ctr is set
+#define FCS_DMA_DYN_PCT 25
 #endif
 
 // One slice-by-4 step against the 32 KiB slice tables: T_{3-s}[e] at e * 256 + s * 32 + replica * 4
@@ -830,27 +837,6 @@ __device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int 
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
 }
 
-// Wait until item k's slot DMA has landed. Vector-memory operations retire in issue order; younger
-// than item k's six rows are the result stores of items k-2 and k-1 (at least one instruction per
-// item: lane 15 of the item's first frame always stores) and, when it exists, item k+1's DMA (two
-// slots per wave). One slot per wave: everything outstanding is older than the next DMA.
-__device__ __forceinline__ void wait_slot(bool next_inflight, uint32_t k) {
-    if (kDmaSlots == 1) {
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-        return;
-    }
-    const uint32_t st = k >= 2 ? 2u : k;      // result stores issued since item k's DMA
-    if (next_inflight) {
-        if (st == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | 8);
-        else if (st == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | 7);
-        else __builtin_amdgcn_s_waitcnt(0x0F70 | 6);
-    } else {
-        if (st == 2) __builtin_amdgcn_s_waitcnt(0x0F70 | 2);
-        else if (st == 1) __builtin_amdgcn_s_waitcnt(0x0F70 | 1);
-        else __builtin_amdgcn_s_waitcnt(0x0F70);
-    }
-}
-
 // MW: words a front mask can touch (host-selected: 2 when the front lane masks at most 8 bytes,
 // i.e. len >= 1516, else kSingleMaskWords).
 template <int MW>
@@ -882,7 +868,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     const int c = lane & (kGroup - 1);     // chunk index back from the frame end
     const int g = lane >> 4;               // frame of the item
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)(wave * kDmaSlots) * kDmaItemBytes;
+    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
     const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
     const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
     const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
@@ -910,27 +896,63 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         const uint64_t a = S & ~15ull;
         return a < lo16 ? lo16 : (a > smax ? smax : a);
     };
-    const uint64_t Q = (uint64_t)gridDim.x * (kDmaWgThreads / 16);   // frames per sweep of the grid
-    uint64_t f = ((uint64_t)blockIdx.x * (kDmaWaves) + (uint64_t)wave) * 4;
-    const uint64_t dS = Q * p.stride;
-    uint64_t S = p.base + f * p.stride;    // first frame of the item
-#pragma unroll
-    for (int j = 0; j < kDmaSlots; j++)
-        if (f + (uint64_t)j * Q < p.n) dma_item(slot0 + j * kDmaItemBytes, slot_src(S + (uint64_t)j * dS), lane);
+    // ---- items (4 frames each): static share, then the dynamic tail ----
+    constexpr uint64_t kEnd = ~0ull;
+    const uint64_t I = (p.n + 3) >> 2;
+    const uint64_t W = (uint64_t)gridDim.x * kDmaWaves;
+    const uint64_t wid = (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave;
+    const uint64_t Is = p.ctr ? (I * (100 - FCS_DMA_DYN_PCT) / 100) / W * W : I;   // static items in all
+    const uint64_t Ks = wid < Is ? (Is - wid + W - 1) / W : 0;                       // ... of this wave
+    uint64_t k = 0;          // static items taken
+    uint64_t ce = 0;         // end of the current dynamic chunk
+    uint64_t pend = 0, psize = 0, seen = 0;   // the requested next chunk (start, size), progress seen
+    auto grab = [&]() {      // request the next chunk: guided size from the progress last seen
+        const uint64_t left = I - Is > seen ? I - Is - seen : 0;
+        uint64_t sz = left / (2 * W);
+        sz = sz < 4 ? 4 : (sz > 64 ? 64 : sz);
+        uint64_t v = 0;
+        if (lane == 0) v = atomicAdd(p.ctr, (unsigned long long)sz);
+        pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+        psize = sz;
+    };
+    auto take = [&]() -> uint64_t {   // move to the requested chunk, request the one after it
+        const uint64_t cb = Is + pend;
+        seen = pend + psize;
+        if (cb >= I) return kEnd;
+        ce = cb + psize < I ? cb + psize : I;
+        grab();
+        return cb;
+    };
+    auto advance = [&](uint64_t cur) -> uint64_t {   // the item after `cur` (wave-uniform)
+        if (k + 1 < Ks) return wid + (++k) * W;
+        if (!p.ctr) return kEnd;
+        if (k + 1 == Ks) {   // static share done: first dynamic chunk
+            k++;
+            return take();
+        }
+        return cur + 1 < ce ? cur + 1 : take();
+    };
+    if (p.ctr) grab();   // the first dynamic chunk, requested while the static share runs
+    uint64_t it = Ks ? wid : (p.ctr ? (k = 1, take()) : kEnd);
+    auto item_start = [&](uint64_t i) { return p.base + 4 * i * p.stride; };   // first frame of item i
+    if (it != kEnd) dma_item(slot0, slot_src(item_start(it)), lane);
 
 #ifdef FCS_STAMPS   // measurement-only: per-wave cycles waiting for the slot vs. the whole item
     uint64_t st_wait = 0, st_all = 0, st_items = 0;
     const uint64_t st_rt0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
 #endif
-    for (uint32_t k = 0; f < p.n; k++) {   // wave-uniform
-        const uint8_t *slot = slot0 + (kDmaSlots == 1 ? 0u : (k & 1u) * kDmaItemBytes);
+    while (it != kEnd) {   // wave-uniform
+        const uint8_t *slot = slot0;
+        const uint64_t f = 4 * it;
+        const uint64_t S = item_start(it);
         const uint64_t src = slot_src(S);
 #ifdef FCS_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts0 = __builtin_amdgcn_s_memtime();
         __builtin_amdgcn_sched_barrier(0);
 #endif
-        wait_slot(f + Q < p.n, k);
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot DMA has landed
 #ifdef FCS_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         const uint64_t ts1 = __builtin_amdgcn_s_memtime();
@@ -949,18 +971,16 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
             d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
-        const uint64_t fn = f + Q;
-        const uint64_t Sn = S + dS;
-        if (f + (uint64_t)kDmaSlots * Q < p.n) dma_item(slot, slot_src(S + (uint64_t)kDmaSlots * dS), lane);
+        const uint64_t nxt = advance(it);
+        if (nxt != kEnd) dma_item(slot, slot_src(item_start(nxt)), lane);
 
 #ifdef FCS_DMA_NOCRC   // measurement-only build: slot DMA and window reads, no CRC work (wrong FCS)
         {
             uint32_t acc = r;
 #pragma unroll
             for (int q = 0; q <= kChunkWords; q++) acc ^= d[q];
-            p.out[f] = acc;   // one store per item, as the product (keeps wait_slot's count)
-            f = fn;
-            S = Sn;
+            p.out[f] = acc;   // one store per item, as the product
+            it = nxt;
 #ifdef FCS_STAMPS
             st_all += __builtin_amdgcn_s_memtime() - ts0;
             st_items++;
@@ -994,8 +1014,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         uint32_t v = lane_shift_dma(lds, mv, lanebase);
         v = row_xor(v);
         emit<kDmaBad>(p, lds, c == kGroup - 1 && f + g < p.n, f + g, ~v);
-        f = fn;
-        S = Sn;
+        it = nxt;
 #ifdef FCS_STAMPS
         __builtin_amdgcn_sched_barrier(0);
         st_all += __builtin_amdgcn_s_memtime() - ts0;

@@ -22,6 +22,7 @@ struct KParams {
     uint64_t *dbg;          // diagnostic stamp sink (FCS_STAMPS builds only; null otherwise)
     uint8_t *ok;            // verify mode: ok[i] = 1 iff frame i (FCS trailer included) checks
     unsigned long long *bad;//   ... and *bad += number of frames that do not (else both null)
+    unsigned long long *ctr;// LDS-DMA kernel: zeroed device counter for the dynamic tail (null: static)
 };
 
 // Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). The 1504..1536-B
@@ -109,16 +110,14 @@ inline bool fixed_single(const KParams &p) {
 // consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
 // frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
 // and the arena must hold a whole slot (the last items' slots are clamped to its end).
-#ifndef FCS_DMA_WG_THREADS   // measurement-only overrides
+#ifndef FCS_DMA_WG_THREADS   // measurement-only override
 #define FCS_DMA_WG_THREADS 1024
 #endif
-#ifndef FCS_DMA_SLOTS
-#define FCS_DMA_SLOTS 1
-#endif
-constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;
-constexpr int kDmaSlots = FCS_DMA_SLOTS;           // 6 KiB LDS slots per wave (items in flight)
-static_assert(kDmaWgThreads % 64 == 0 && (kDmaSlots == 1 || kDmaSlots == 2) &&
-              (kDmaWgThreads / 64) * kDmaSlots <= 16, "LDS holds 16 slots next to the 64 KiB tables");
+constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;  // one 6 KiB LDS slot per wave
+static_assert(kDmaWgThreads % 64 == 0 && kDmaWgThreads <= 1024, "LDS holds 16 slots next to the 64 KiB tables");
+// Batches of at least this many items (4 frames) per wave of the grid hand their tail out
+// dynamically (KParams::ctr): below it the static share alone balances well enough.
+constexpr uint64_t kDmaDynMinItemsPerWave = 16;
 inline bool fixed_dma(const KParams &p) {
 #ifdef FCS_NO_DMA   // measurement-only build
     return false;

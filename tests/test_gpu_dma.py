@@ -92,3 +92,37 @@ def test_dma_verify_mode(dev, L):
     exp[bad_idx] = 0
     assert np.array_equal(okh, exp)
     assert int(bad.item()) == len(bad_idx)
+
+
+@pytest.mark.parametrize("L,stride,lead", [(1518, 1518, 0), (1518, 1518, 3), (1514, 1518, 1), (1524, 1524, 2)])
+def test_dma_dynamic_tail(dev, oracle, L, stride, lead):
+    """Batches of >= 16 items (64 frames) per wave of the grid hand the last quarter of their items out
+    through the device work counter (guided chunks): every frame of a 1 M-frame batch against the
+    oracle, and a second launch on the same stream reusing the counter ring."""
+    n = (1 << 20) + 7
+    host = np.random.default_rng(L + stride + lead).integers(0, 256, n * stride + 8, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+    for _ in range(2):
+        out = torch.zeros(n, dtype=torch.int32, device=dev)
+        na.fixed_dev(d.data_ptr() + lead, stride, L, n, out)
+        torch.cuda.synchronize()
+        got = out.cpu().numpy().view(np.uint32)
+        assert np.array_equal(got, exp), int(np.argmax(got != exp))
+
+
+def test_dma_dynamic_tail_concurrent_streams(dev, oracle):
+    """Two large launches in flight on two streams take different counter slots."""
+    L, n = 1518, (1 << 19) + 3
+    host = np.random.default_rng(11).integers(0, 256, n * L, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    exp = oracle_fixed(oracle, host, L, L, n)
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    o1 = torch.zeros(n, dtype=torch.int32, device=dev)
+    o2 = torch.zeros(n, dtype=torch.int32, device=dev)
+    torch.cuda.synchronize()
+    na.fixed_dev(d, L, L, n, o1, s1)
+    na.fixed_dev(d, L, L, n, o2, s2)
+    torch.cuda.synchronize()
+    assert np.array_equal(o1.cpu().numpy().view(np.uint32), exp)
+    assert np.array_equal(o2.cpu().numpy().view(np.uint32), exp)
