@@ -15,7 +15,8 @@ Printed (rank 0, one JSON line): the contract fields plus
                  launch time from HIP events on the launch stream) against the 8 TB/s HBM peak;
                  `traffic` = HBM bytes per launch from the committed rocprofv3 PMC summary
                  (profiles/*pmc_traffic*.json), or null; read_stream_gbs = a pure read kernel over
-                 the same buffer (the measured HBM read ceiling);
+                 the same buffer (plain 16-B loads), dma_stream_gbs = the kernel's own LDS-DMA loads
+                 and schedule without the CRC work (the measured read ceilings);
   cpu_baseline — the reference's own src/ether_fcs.c (oracle/_ref, its Makefile flags) timed on
                  1 M x 1518 B (SURVEY §8d) on one host thread, the oracle port beside it; rank 0, N = 1;
   configs      — (N = 1) the other single-GPU BASELINE configs, each timed in this process after the
@@ -331,6 +332,14 @@ def main():
     torch.cuda.synchronize()
     read_ms = rs.elapsed_time(re_) / 5
     read_gbs = nbytes / (read_ms * 1e-3) / 1e9
+    # the LDS-DMA read ceiling: the headline kernel's own loads and schedule without the CRC work
+    na.dma_stream_dev(arena, nbytes, sink, stream)
+    rs.record(stream)
+    for _ in range(5):
+        na.dma_stream_dev(arena, nbytes, sink, stream)
+    re_.record(stream)
+    torch.cuda.synchronize()
+    dma_gbs = nbytes / (rs.elapsed_time(re_) / 5 * 1e-3) / 1e9
 
 
     for _ in range(args.warmup):
@@ -388,7 +397,9 @@ def main():
                 "algorithmic_bytes_per_launch": nbytes,
                 "kernel_ms_per_launch": round(kernel_ms, 4),
                 "read_stream_gbs": round(read_gbs, 1),
-                "frac_of_read_stream": round(achieved_gbs / read_gbs, 4)}
+                "frac_of_read_stream": round(achieved_gbs / read_gbs, 4),
+                "dma_stream_gbs": round(dma_gbs, 1),
+                "frac_of_dma_stream": round(achieved_gbs / dma_gbs, 4)}
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:

@@ -126,6 +126,9 @@ int fcs_fill_splitmix64_dev(void *p, uint64_t bytes, uint64_t seed, uint64_t byt
                             void *stream);
 /* Pure HBM read-stream kernel over [p, p+bytes): the measured read ceiling. */
 int fcs_read_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
+/* The LDS-DMA read ceiling: the headline kernel's slot DMA (global_load_lds, nt), schedule and
+ * window reads over [p, p+bytes) viewed as 1518-B frames, without the CRC work. */
+int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
 /* Average device time (ms) per launch of the last `reps` timed FCS launches measured with
  * HIP events on the launch stream: fcs_timed_fixed_dev() launches ether_fcs_fixed_dev
  * `reps` times back to back, bracketed by events recorded on `stream`. */

@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "tx_batch_host", "host_buffer", "host_free", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan"]
+           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan", "dma_stream_dev"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -26,7 +26,7 @@ EXPORTS = [
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
-    "fcs_tables_blob", "fcs_engine_stats", "fcs_shard_plan",
+    "fcs_tables_blob", "fcs_engine_stats", "fcs_shard_plan", "fcs_dma_stream_dev",
     # include/nstack_txq.h — batched TX call site
     "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
@@ -89,6 +89,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_tables_blob": (i32, [vp, u64]),
         "fcs_engine_stats": (None, [c.POINTER(u64)] * 4),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
+        "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
         "fcs_txq_create": (vp, [vp, u32, u32, vp, vp]),
         "fcs_txq_send": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
         "fcs_txq_flush": (i32, [vp]),
@@ -246,6 +247,10 @@ def verify_host(arena, arena_bytes: int, off, length, ok, n: int) -> int:
 def fill_splitmix_dev(ptr, nbytes: int, seed: int, byte_offset: int = 0, stream=None) -> None:
     _check(load().fcs_fill_splitmix64_dev(_ptr(ptr), nbytes, seed, byte_offset, _stream(stream)),
            "fcs_fill_splitmix64_dev")
+
+
+def dma_stream_dev(ptr, nbytes: int, sink, stream=None) -> None:
+    _check(load().fcs_dma_stream_dev(_ptr(ptr), nbytes, _ptr(sink), _stream(stream)), "fcs_dma_stream_dev")
 
 
 def read_stream_dev(ptr, nbytes: int, sink, stream=None) -> None:

@@ -1070,8 +1070,9 @@ extern "C" {
 const char *fcs_last_error(void) { return g_last_error.c_str(); }
 
 const char *fcs_engine_version(void) {
-    return "nstack-fcs 0.3 gfx950: quarter-wave/frame, 96B lane chunks as 2 chains, slice-by-4 "
-           "LDS x32 replicas, v_perm addressing, DPP reduce; var: flat chunk stream per 64-frame window";
+    return "nstack-fcs 0.4 gfx950: quarter-wave/frame, 96B lane windows as 2 slice-by-4 chains, v_perm "
+           "addressing, DPP reduce; 1496-1524B: LDS-DMA (nt global_load_lds) 6KiB slot/wave, 16 waves/CU, "
+           "32KiB 8-replica tables, guided dynamic items; var: flat chunk stream per 64-frame window";
 }
 
 int fcs_engine_init(int ndev) {
@@ -1381,6 +1382,33 @@ int fcs_fill_splitmix64_dev(void *p, uint64_t bytes, uint64_t seed, uint64_t byt
 int fcs_read_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream) {
     if (!p || !sink) return fail(EINVAL, "null pointer");
     HIPTRY(fcs::launch_read_stream(p, bytes, sink, (hipStream_t)stream), "launching read stream");
+    return 0;
+}
+
+int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream) {
+    if (!p || !sink) return fail(EINVAL, "null pointer");
+    constexpr uint32_t L = 1518;   // the headline kernel's geometry over the same bytes
+    if (bytes < 4 * fcs::kDmaItemBytes) return fail(EINVAL, "fcs_dma_stream_dev: at least 24 KiB");
+    DevState *ds = nullptr;
+    int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    fcs::KParams k{};
+    k.base = (uint64_t)p;
+    k.stride = L;
+    k.flen = L;
+    k.fseg = 1;
+    k.n = bytes / L;
+    k.lo4 = floor4((uint64_t)p);
+    k.hi4 = ceil4((uint64_t)p + k.n * L);
+    k.zmax = fcs::kDmaCover - L;
+    k.blob = ds->d_blob;
+    k.out = sink;
+    const hipStream_t st = (hipStream_t)stream;
+    const int grid = grid_for(ds, k.n, fcs::kDmaWgThreads);
+    const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
+    k.ctr = ds->d_ctr + 8 * slot;
+    HIPTRY(hipMemsetAsync(k.ctr, 0, 8, st), "zeroing the work counter");
+    HIPTRY(fcs::launch_dma_stream(k, grid, st), "launching the LDS-DMA read stream");
     return 0;
 }
 

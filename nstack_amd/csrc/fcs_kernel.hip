@@ -773,7 +773,10 @@ static_assert(kDmaChains - 1 <= 5, "merge holes");
 #define FCS_DMA_AUX 2
 #endif
 #ifndef FCS_DMA_DYN_PCT   // share of the items handed out dynamically when p.ctr is set
-#define FCS_DMA_DYN_PCT 25
+#define FCS_DMA_DYN_PCT 100
+#endif
+#ifndef FCS_DMA_CHUNK_MAX   // largest dynamic chunk (items); measurement-only override
+#define FCS_DMA_CHUNK_MAX 64
 #endif
 
 // One slice-by-4 step against the 32 KiB slice tables: T_{3-s}[e] at e * 256 + s * 32 + replica * 4
@@ -839,7 +842,9 @@ __device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int 
 
 // MW: words a front mask can touch (host-selected: 2 when the front lane masks at most 8 bytes,
 // i.e. len >= 1516, else kSingleMaskWords).
-template <int MW>
+// STREAM: the measurement form behind fcs_dma_stream_dev: the same slot DMA, schedule and window
+// reads, no CRC work (bench.py's LDS-DMA read ceiling beside the plain read stream).
+template <int MW, bool STREAM>
 __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
     const int tid = threadIdx.x;
@@ -909,7 +914,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     auto grab = [&]() {      // request the next chunk: guided size from the progress last seen
         const uint64_t left = I - Is > seen ? I - Is - seen : 0;
         uint64_t sz = left / (2 * W);
-        sz = sz < 4 ? 4 : (sz > 64 ? 64 : sz);
+        sz = sz < 4 ? 4 : (sz > FCS_DMA_CHUNK_MAX ? FCS_DMA_CHUNK_MAX : sz);
         uint64_t v = 0;
         if (lane == 0) v = atomicAdd(p.ctr, (unsigned long long)sz);
         pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
@@ -974,12 +979,11 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         const uint64_t nxt = advance(it);
         if (nxt != kEnd) dma_item(slot, slot_src(item_start(nxt)), lane);
 
-#ifdef FCS_DMA_NOCRC   // measurement-only build: slot DMA and window reads, no CRC work (wrong FCS)
-        {
+        if (STREAM) {   // read ceiling: the words are only XORed together
             uint32_t acc = r;
 #pragma unroll
             for (int q = 0; q <= kChunkWords; q++) acc ^= d[q];
-            p.out[f] = acc;   // one store per item, as the product
+            if (acc == 0x9E3779B9u) p.out[0] = acc;   // keeps the reads live; practically never stores
             it = nxt;
 #ifdef FCS_STAMPS
             st_all += __builtin_amdgcn_s_memtime() - ts0;
@@ -987,7 +991,6 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
 #endif
             continue;
         }
-#endif
         uint32_t w[kChunkWords];
 #pragma unroll
 #ifdef FCS_DMA_ABL_NOALIGN   // measurement-only: no realignment (wrong FCS unless r == 0)
@@ -1715,8 +1718,8 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #endif
         }
     } else if (!tiny && fixed_dma(p)) {
-        if (p.zmax <= 8) hipLaunchKernelGGL(fcs_dma_kernel<2>, dim3(grid), dim3(kDmaWgThreads), 0, st, p);
-        else hipLaunchKernelGGL(fcs_dma_kernel<kSingleMaskWords>, dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+        if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dma_kernel<2, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+        else hipLaunchKernelGGL((fcs_dma_kernel<kSingleMaskWords, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
     } else if (tiny) {
         if (single) FCS_LAUNCH(false, true, true);
         else FCS_LAUNCH(false, true, false);
@@ -1754,6 +1757,12 @@ hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hip
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
     hipLaunchKernelGGL(read_stream_kernel, dim3(8192), dim3(256), 0, st, (const u32x4 *)p, bytes / 16, sink);
+    return hipGetLastError();
+}
+
+hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st) {
+    (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    hipLaunchKernelGGL((fcs_dma_kernel<2, true>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
     return hipGetLastError();
 }
 
