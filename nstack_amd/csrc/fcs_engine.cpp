@@ -265,6 +265,22 @@ std::atomic<uint64_t> g_var_threshold{16384};
 #endif
 constexpr uint32_t kFixedFlatMaxLen = FCS_FIXED_FLAT_MAX;
 
+// A zeroed work counter for one launch (Dispenser in fcs_kernel.hip): the next slot of the
+// device's ring, cleared on the launch's own stream just before the kernel.
+int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p) {
+    const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
+    p.ctr = ds->d_ctr + 8 * slot;
+    HIPTRY(hipMemsetAsync(p.ctr, 0, 8, st), "zeroing the work counter");
+    return 0;
+}
+
+// The flat kernel hands its 64-frame windows out dynamically once there are at least this many
+// windows per wave of the grid.
+#ifndef FCS_FLAT_DYN_MIN   // measurement-only override (a huge value keeps the flat kernel static)
+#define FCS_FLAT_DYN_MIN 4
+#endif
+constexpr uint64_t kFlatDynMinWindowsPerWave = FCS_FLAT_DYN_MIN;
+
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
                  uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
     fcs::KParams p{};
@@ -285,17 +301,21 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame
         // instead of a 16-lane quarter-wave (len == null tells it the length is p.flen)
         p.zmax = fcs::kChunkBytes;
-        HIPTRY(fcs::launch_fcs(true, true, p, grid_for(ds, n, fcs::kWgThreads), st), "launching fcs_flat_kernel<fixed>");
+        const int fgrid = grid_for(ds, n, fcs::kWgThreads);
+        if ((n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)fgrid * (fcs::kWgThreads / 64)) {
+            const int rc = take_counter(ds, st, p);
+            if (rc) return rc;
+        }
+        HIPTRY(fcs::launch_fcs(true, true, p, fgrid, st), "launching fcs_flat_kernel<fixed>");
         return 0;
     }
     const int grid = grid_for(ds, n, fcs::fixed_threads(p));
     if (fcs::fixed_dma(p)) {   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
         p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
         const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
-        if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic tail
-            const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
-            p.ctr = ds->d_ctr + 8 * slot;
-            HIPTRY(hipMemsetAsync(p.ctr, 0, 8, st), "zeroing the work counter");
+        if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic schedule
+            const int rc = take_counter(ds, st, p);
+            if (rc) return rc;
         }
     }
     HIPTRY(fcs::launch_fcs(false, false, p, grid, st), "launching fcs_kernel<fixed>");
@@ -320,7 +340,12 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     p.zmax = fcs::kChunkBytes;
     p.blob = ds->d_blob;
     const bool windowed = n > g_var_threshold.load(std::memory_order_relaxed);
-    HIPTRY(fcs::launch_fcs(true, windowed, p, grid_for(ds, n, fcs::kWgThreads), st), "launching fcs_kernel<var>");
+    const int grid = grid_for(ds, n, fcs::kWgThreads);
+    if (windowed && (n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)grid * (fcs::kWgThreads / 64)) {
+        const int rc = take_counter(ds, st, p);
+        if (rc) return rc;
+    }
+    HIPTRY(fcs::launch_fcs(true, windowed, p, grid, st), "launching fcs_kernel<var>");
     return 0;
 }
 
@@ -1405,9 +1430,7 @@ int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stre
     k.out = sink;
     const hipStream_t st = (hipStream_t)stream;
     const int grid = grid_for(ds, k.n, fcs::kDmaWgThreads);
-    const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
-    k.ctr = ds->d_ctr + 8 * slot;
-    HIPTRY(hipMemsetAsync(k.ctr, 0, 8, st), "zeroing the work counter");
+    if ((rc = take_counter(ds, st, k))) return rc;
     HIPTRY(fcs::launch_dma_stream(k, grid, st), "launching the LDS-DMA read stream");
     return 0;
 }

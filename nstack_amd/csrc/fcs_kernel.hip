@@ -730,6 +730,62 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
 }
 
 
+// Hands out the units [0, U) of a launch to the waves of a persistent grid (wave-uniform state).
+// Without a counter: wave wid of W takes wid, wid + W, ... (interleaved). With one (a zeroed device
+// word, KParams::ctr): the first (100 - dyn_pct) % of the units that way, the rest in chunks of
+// consecutive units from *ctr, sized by the work left (guided: left / 2W, clamped to cmin..cmax),
+// each chunk requested when the previous one starts so the atomic's latency stays hidden.
+struct Dispenser {
+    static constexpr uint64_t kEnd = ~0ull;
+    unsigned long long *ctr;
+    uint64_t U, W, wid, Is, Ks;
+    uint64_t k = 0, ce = 0, pend = 0, psize = 0, seen = 0;
+    uint32_t cmin, cmax;
+    int lane;
+    bool dyn = false;
+
+    __device__ Dispenser(unsigned long long *ctr_, uint64_t U_, uint64_t W_, uint64_t wid_, int lane_,
+                         uint32_t dyn_pct, uint32_t cmin_, uint32_t cmax_)
+        : ctr(ctr_), U(U_), W(W_), wid(wid_), cmin(cmin_), cmax(cmax_), lane(lane_) {
+        Is = ctr ? (U * (100 - dyn_pct) / 100) / W * W : U;   // statically assigned units in all
+        Ks = wid < Is ? (Is - wid + W - 1) / W : 0;             // ... of this wave
+    }
+    __device__ void grab() {
+        const uint64_t left = U - Is > seen ? U - Is - seen : 0;
+        uint64_t sz = left / (2 * W);
+        sz = sz < cmin ? cmin : (sz > cmax ? cmax : sz);
+        uint64_t v = 0;
+        if (lane == 0) v = atomicAdd(ctr, (unsigned long long)sz);
+        pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+        psize = sz;
+    }
+    __device__ uint64_t take() {   // move to the requested chunk, request the one after it
+        const uint64_t cb = Is + pend;
+        seen = pend + psize;
+        if (cb >= U) return kEnd;
+        ce = cb + psize < U ? cb + psize : U;
+        grab();
+        return cb;
+    }
+    __device__ uint64_t first() {
+        if (ctr) grab();   // the first dynamic chunk, requested while the static share runs
+        if (Ks) return wid;
+        if (!ctr) return kEnd;
+        dyn = true;
+        return take();
+    }
+    __device__ uint64_t next(uint64_t cur) {
+        if (!dyn) {
+            if (k + 1 < Ks) return wid + (++k) * W;
+            if (!ctr) return kEnd;
+            dyn = true;
+            return take();
+        }
+        return cur + 1 < ce ? cur + 1 : take();
+    }
+};
+
 // ---------------------------------------------------------------------------------------------
 // Fixed length, one segment, frames staged through LDS by DMA (fcs_dma_kernel; host-selected for
 // kDmaMinLen..kDmaCover bytes, e.g. the 1518-B benchmark frames, when four consecutive frames fit
@@ -901,45 +957,11 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         const uint64_t a = S & ~15ull;
         return a < lo16 ? lo16 : (a > smax ? smax : a);
     };
-    // ---- items (4 frames each): static share, then the dynamic tail ----
-    constexpr uint64_t kEnd = ~0ull;
-    const uint64_t I = (p.n + 3) >> 2;
-    const uint64_t W = (uint64_t)gridDim.x * kDmaWaves;
-    const uint64_t wid = (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave;
-    const uint64_t Is = p.ctr ? (I * (100 - FCS_DMA_DYN_PCT) / 100) / W * W : I;   // static items in all
-    const uint64_t Ks = wid < Is ? (Is - wid + W - 1) / W : 0;                       // ... of this wave
-    uint64_t k = 0;          // static items taken
-    uint64_t ce = 0;         // end of the current dynamic chunk
-    uint64_t pend = 0, psize = 0, seen = 0;   // the requested next chunk (start, size), progress seen
-    auto grab = [&]() {      // request the next chunk: guided size from the progress last seen
-        const uint64_t left = I - Is > seen ? I - Is - seen : 0;
-        uint64_t sz = left / (2 * W);
-        sz = sz < 4 ? 4 : (sz > FCS_DMA_CHUNK_MAX ? FCS_DMA_CHUNK_MAX : sz);
-        uint64_t v = 0;
-        if (lane == 0) v = atomicAdd(p.ctr, (unsigned long long)sz);
-        pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-        psize = sz;
-    };
-    auto take = [&]() -> uint64_t {   // move to the requested chunk, request the one after it
-        const uint64_t cb = Is + pend;
-        seen = pend + psize;
-        if (cb >= I) return kEnd;
-        ce = cb + psize < I ? cb + psize : I;
-        grab();
-        return cb;
-    };
-    auto advance = [&](uint64_t cur) -> uint64_t {   // the item after `cur` (wave-uniform)
-        if (k + 1 < Ks) return wid + (++k) * W;
-        if (!p.ctr) return kEnd;
-        if (k + 1 == Ks) {   // static share done: first dynamic chunk
-            k++;
-            return take();
-        }
-        return cur + 1 < ce ? cur + 1 : take();
-    };
-    if (p.ctr) grab();   // the first dynamic chunk, requested while the static share runs
-    uint64_t it = Ks ? wid : (p.ctr ? (k = 1, take()) : kEnd);
+    // ---- items (4 frames each), from the dispenser ----
+    constexpr uint64_t kEnd = Dispenser::kEnd;
+    Dispenser D(p.ctr, (p.n + 3) >> 2, (uint64_t)gridDim.x * kDmaWaves,
+                (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
+    uint64_t it = D.first();
     auto item_start = [&](uint64_t i) { return p.base + 4 * i * p.stride; };   // first frame of item i
     if (it != kEnd) dma_item(slot0, slot_src(item_start(it)), lane);
 
@@ -976,7 +998,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
             d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
-        const uint64_t nxt = advance(it);
+        const uint64_t nxt = D.next(it);
         if (nxt != kEnd) dma_item(slot, slot_src(item_start(nxt)), lane);
 
         if (STREAM) {   // read ceiling: the words are only XORed together
@@ -1298,9 +1320,11 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     uint8_t *list = lds + kLdsFlatList + wave * 64;
     acc[lane] = 0u;
     mark[lane] = 0;
-    const uint64_t GW = (uint64_t)gridDim.x * (kWgThreads / 64);
-
-    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kWgThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
+    // windows of 64 frames from the dispenser (dynamic chunks of up to 16 windows when p.ctr is set)
+    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
+                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, 16);
+    for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
+        const uint64_t w0 = win * 64;
         // ---- window metadata: lane i <-> frame w0 + i ----
         const uint64_t f = w0 + lane;
         const bool act = f < p.n;

@@ -453,3 +453,25 @@ def test_fixed_short_frames_flat_route(dev, oracle, L, stride):
     got = run_fixed(dev, base[3:], stride, L, n)   # odd base alignment
     exp = oracle_fixed(oracle, host[3:].copy(), stride, L, n)
     assert np.array_equal(got, exp)
+
+
+@pytest.mark.parametrize("mode", ["imix", "fixed576"])
+def test_flat_kernel_dynamic_windows(dev, oracle, mode):
+    """Batches of >= 4 windows (64 frames) per wave take their windows from the work counter:
+    1.1 M frames through the flat kernel, every one against the oracle."""
+    n = 1100003
+    rng = np.random.default_rng(5)
+    if mode == "imix":
+        ln = rng.choice(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.uint32), n)
+        off = np.zeros(n, dtype=np.uint64)
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        total = int(off[-1]) + int(ln[-1])
+        arena = rng.integers(0, 256, total + 5, dtype=np.uint8)
+        got = run_var(dev, arena, off, ln)
+        assert np.array_equal(got, oracle_var(oracle, arena, off, ln))
+    else:
+        L = 576
+        host = rng.integers(0, 256, n * L + 3, dtype=np.uint8)
+        d = to_dev(host, dev)
+        got = run_fixed(dev, d.data_ptr() + 1, L, L, n)
+        assert np.array_equal(got, oracle_fixed(oracle, host[1:], L, L, n))
