@@ -281,6 +281,13 @@ int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p) {
 #endif
 constexpr uint64_t kFlatDynMinWindowsPerWave = FCS_FLAT_DYN_MIN;
 
+// The generic fixed-length kernel hands its 4-frame units out dynamically from this many units per
+// wave of the grid.
+#ifndef FCS_FIXED_DYN_MIN   // measurement-only override (a huge value keeps the kernel static)
+#define FCS_FIXED_DYN_MIN 4
+#endif
+constexpr uint64_t kFixedDynMinUnitsPerWave = FCS_FIXED_DYN_MIN;
+
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
                  uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
     fcs::KParams p{};
@@ -314,6 +321,13 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
         const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
         if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic schedule
+            const int rc = take_counter(ds, st, p);
+            if (rc) return rc;
+        }
+    } else if (!fcs::fixed_tiny(p) && !fcs::fixed_single(p)) {
+        // generic kernel: units of 4 frames (one per quarter-wave), dynamic for large batches
+        const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);
+        if (units >= kFixedDynMinUnitsPerWave * waves) {
             const int rc = take_counter(ds, st, p);
             if (rc) return rc;
         }

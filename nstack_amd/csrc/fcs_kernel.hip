@@ -307,6 +307,71 @@ __device__ __forceinline__ void shift_up(uint32_t (&d)[N], int dlead) {
     }
 }
 
+// Hands out the units [0, U) of a launch to the waves of a persistent grid (wave-uniform state).
+// Without a counter: wave wid of W takes wid, wid + W, ... (interleaved). With one (a zeroed device
+// word, KParams::ctr): the first (100 - dyn_pct) % of the units that way, the rest in chunks of
+// consecutive units from *ctr, sized by the work left (guided: left / 2W, clamped to cmin..cmax),
+// each chunk requested when the previous one starts so the atomic's latency stays hidden.
+#ifndef FCS_FIXED_CHUNK_MAX   // measurement-only overrides: largest dynamic chunk, in units
+#define FCS_FIXED_CHUNK_MAX 64   // generic fixed kernel: units of 4 frames
+#endif
+#ifndef FCS_FIXED_DYN_PCT
+#define FCS_FIXED_DYN_PCT 100    // generic fixed kernel: share of the units handed out dynamically
+#endif
+#ifndef FCS_FLAT_CHUNK_MAX
+#define FCS_FLAT_CHUNK_MAX 16    // flat kernel: 64-frame windows
+#endif
+struct Dispenser {
+    static constexpr uint64_t kEnd = ~0ull;
+    unsigned long long *ctr;
+    uint64_t U, W, wid, Is, Ks;
+    uint64_t k = 0, ce = 0, pend = 0, psize = 0, seen = 0;
+    uint32_t cmin, cmax;
+    int lane;
+    bool dyn = false;
+
+    __device__ Dispenser(unsigned long long *ctr_, uint64_t U_, uint64_t W_, uint64_t wid_, int lane_,
+                         uint32_t dyn_pct, uint32_t cmin_, uint32_t cmax_)
+        : ctr(ctr_), U(U_), W(W_), wid(wid_), cmin(cmin_), cmax(cmax_), lane(lane_) {
+        Is = ctr ? (U * (100 - dyn_pct) / 100) / W * W : U;   // statically assigned units in all
+        Ks = wid < Is ? (Is - wid + W - 1) / W : 0;             // ... of this wave
+    }
+    __device__ void grab() {
+        const uint64_t left = U - Is > seen ? U - Is - seen : 0;
+        uint64_t sz = left / (2 * W);
+        sz = sz < cmin ? cmin : (sz > cmax ? cmax : sz);
+        uint64_t v = 0;
+        if (lane == 0) v = atomicAdd(ctr, (unsigned long long)sz);
+        pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
+               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
+        psize = sz;
+    }
+    __device__ uint64_t take() {   // move to the requested chunk, request the one after it
+        const uint64_t cb = Is + pend;
+        seen = pend + psize;
+        if (cb >= U) return kEnd;
+        ce = cb + psize < U ? cb + psize : U;
+        grab();
+        return cb;
+    }
+    __device__ uint64_t first() {
+        if (ctr) grab();   // the first dynamic chunk, requested while the static share runs
+        if (Ks) return wid;
+        if (!ctr) return kEnd;
+        dyn = true;
+        return take();
+    }
+    __device__ uint64_t next(uint64_t cur) {
+        if (!dyn) {
+            if (k + 1 < Ks) return wid + (++k) * W;
+            if (!ctr) return kEnd;
+            dyn = true;
+            return take();
+        }
+        return cur + 1 < ce ? cur + 1 : take();
+    }
+};
+
 template <bool VAR, bool TINY, bool SINGLE>
 struct Lane {
     const KParams &p;
@@ -314,9 +379,12 @@ struct Lane {
     int j;            // lane within the frame's 16
     uint32_t base0, base1, lanebase;
     uint64_t Q;       // frame slots in the grid
+    Dispenser *D;     // fixed frames of any segment count: wave units of 4 frames (else null)
+    uint32_t q;       // quarter of the wave (frame 4u + q of unit u)
 
     struct Pos {
         uint64_t f;
+        uint64_t u;   // D's unit (D only)
         uint32_t k;
         bool act;
         Item it;
@@ -324,7 +392,15 @@ struct Lane {
 
     __device__ __forceinline__ Pos next(const Pos &c) const {
         Pos n = c;
-        if (SINGLE) {
+        if (!VAR && !SINGLE && D != nullptr) {
+            // every frame has p.fseg segments: the quarters wrap together, the unit step is uniform
+            n.k = c.k + 1;
+            if (n.k >= p.fseg) {
+                n.k = 0;
+                n.u = c.u == Dispenser::kEnd ? c.u : D->next(c.u);
+                n.f = n.u == Dispenser::kEnd ? p.n : 4 * n.u + q;
+            }
+        } else if (SINGLE) {
             n.f = c.f + Q;
             n.k = 0;
         } else {
@@ -482,10 +558,22 @@ __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, u
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
     uint32_t tb0, tb1;
     table_bases(lane, tb0, tb1);
-    Lane<VAR, TINY, SINGLE> L{p, lds, j, tb0, tb1, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<NT>};
+    // Fixed frames: a wave's unit is 4 consecutive frames (one per quarter), units from the
+    // dispenser (interleaved over the grid's waves, the tail dynamic when the host gave a counter).
+    constexpr bool kUnits = !VAR && !SINGLE && !TINY;
+    Dispenser D(kUnits ? p.ctr : nullptr, (p.n + 3) >> 2, (uint64_t)nblk * (NT / 64),
+                (uint64_t)blk * (NT / 64) + (threadIdx.x >> 6), lane, FCS_FIXED_DYN_PCT, 1, FCS_FIXED_CHUNK_MAX);
+    Lane<VAR, TINY, SINGLE> L{p, lds, j, tb0, tb1, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<NT>,
+                              kUnits ? &D : nullptr, (uint32_t)(threadIdx.x >> 4) & 3u};
 
     typename Lane<VAR, TINY, SINGLE>::Pos A, B;
-    A.f = ((uint64_t)blk * kSlotsPerWg<NT>) + (threadIdx.x / kGroup);
+    if (kUnits) {
+        A.u = D.first();
+        A.f = A.u == Dispenser::kEnd ? p.n : 4 * A.u + L.q;
+    } else {
+        A.u = 0;
+        A.f = ((uint64_t)blk * kSlotsPerWg<NT>) + (threadIdx.x / kGroup);
+    }
     A.k = 0;
     A.act = A.f < p.n;
     A.it = (SINGLE || A.act) ? frame_item<VAR>(p, A.f) : Item{0, 0, 1};
@@ -729,62 +817,6 @@ __global__ __launch_bounds__(kFixedWgThreads, 1) void fcs_single_kernel(KParams 
     flush_bad(p, lds);
 }
 
-
-// Hands out the units [0, U) of a launch to the waves of a persistent grid (wave-uniform state).
-// Without a counter: wave wid of W takes wid, wid + W, ... (interleaved). With one (a zeroed device
-// word, KParams::ctr): the first (100 - dyn_pct) % of the units that way, the rest in chunks of
-// consecutive units from *ctr, sized by the work left (guided: left / 2W, clamped to cmin..cmax),
-// each chunk requested when the previous one starts so the atomic's latency stays hidden.
-struct Dispenser {
-    static constexpr uint64_t kEnd = ~0ull;
-    unsigned long long *ctr;
-    uint64_t U, W, wid, Is, Ks;
-    uint64_t k = 0, ce = 0, pend = 0, psize = 0, seen = 0;
-    uint32_t cmin, cmax;
-    int lane;
-    bool dyn = false;
-
-    __device__ Dispenser(unsigned long long *ctr_, uint64_t U_, uint64_t W_, uint64_t wid_, int lane_,
-                         uint32_t dyn_pct, uint32_t cmin_, uint32_t cmax_)
-        : ctr(ctr_), U(U_), W(W_), wid(wid_), cmin(cmin_), cmax(cmax_), lane(lane_) {
-        Is = ctr ? (U * (100 - dyn_pct) / 100) / W * W : U;   // statically assigned units in all
-        Ks = wid < Is ? (Is - wid + W - 1) / W : 0;             // ... of this wave
-    }
-    __device__ void grab() {
-        const uint64_t left = U - Is > seen ? U - Is - seen : 0;
-        uint64_t sz = left / (2 * W);
-        sz = sz < cmin ? cmin : (sz > cmax ? cmax : sz);
-        uint64_t v = 0;
-        if (lane == 0) v = atomicAdd(ctr, (unsigned long long)sz);
-        pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
-               (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)v);
-        psize = sz;
-    }
-    __device__ uint64_t take() {   // move to the requested chunk, request the one after it
-        const uint64_t cb = Is + pend;
-        seen = pend + psize;
-        if (cb >= U) return kEnd;
-        ce = cb + psize < U ? cb + psize : U;
-        grab();
-        return cb;
-    }
-    __device__ uint64_t first() {
-        if (ctr) grab();   // the first dynamic chunk, requested while the static share runs
-        if (Ks) return wid;
-        if (!ctr) return kEnd;
-        dyn = true;
-        return take();
-    }
-    __device__ uint64_t next(uint64_t cur) {
-        if (!dyn) {
-            if (k + 1 < Ks) return wid + (++k) * W;
-            if (!ctr) return kEnd;
-            dyn = true;
-            return take();
-        }
-        return cur + 1 < ce ? cur + 1 : take();
-    }
-};
 
 // ---------------------------------------------------------------------------------------------
 // Fixed length, one segment, frames staged through LDS by DMA (fcs_dma_kernel; host-selected for
@@ -1107,8 +1139,10 @@ __device__ __forceinline__ void issue_any(const KParams &p, int64_t cstart, bool
 
 // Register value of one chunk (realigned, bytes before the frame start masked, x0 injected),
 // before the lane shift: A_48(chain(words 0..11)) ^ chain(words 12..23).
+// zb: this lane's claim on the masking (zr if its value is used, 0 if the caller discards it): the
+// wave masks 16-byte groups of words only up to its largest claim (IMIX items: 32 bytes, not 96).
 template <bool TINY>
-__device__ __forceinline__ uint32_t chunk_value(const uint8_t *lds, const Chunk &c, int zr, uint32_t x0,
+__device__ __forceinline__ uint32_t chunk_value(const uint8_t *lds, const Chunk &c, int zr, int zb, uint32_t x0,
                                                 uint32_t base0, uint32_t base1) {
     uint32_t d[kChunkWords + 1];
 #pragma unroll
@@ -1123,6 +1157,7 @@ __device__ __forceinline__ uint32_t chunk_value(const uint8_t *lds, const Chunk 
     uint32_t w[kChunkWords];
 #pragma unroll
     for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], c.r);
+#ifdef FCS_MASK_ALL   // measurement-only build: every word masked whenever any lane has a front
     if (__any(zr > 0)) {
 #pragma unroll
         for (int i = 0; i < kChunkWords; i++) {
@@ -1131,6 +1166,19 @@ __device__ __forceinline__ uint32_t chunk_value(const uint8_t *lds, const Chunk 
             w[i] &= (uint32_t)(0xFFFFFFFFull << (8 * t));
         }
     }
+#else
+    const int zr8 = 8 * zr;
+#pragma unroll
+    for (int g = 0; g < kChunkWords / 4; g++) {
+        if (!__any(zb > 16 * g)) break;
+#pragma unroll
+        for (int i = 4 * g; i < 4 * g + 4; i++) {
+            int t = zr8 - 32 * i;
+            t = t < 0 ? 0 : (t > 32 ? 32 : t);
+            w[i] &= (uint32_t)(0xFFFFFFFFull << t);
+        }
+    }
+#endif
     uint32_t xa = x0 ^ w[0], xb = w[12];
 #pragma unroll
     for (int i = 0; i < 12; i++) {
@@ -1184,7 +1232,7 @@ __device__ __forceinline__ void unit_finish(const KParams &p, const uint8_t *lds
                                             int lane, int j, uint32_t base0, uint32_t base1, uint32_t lanebase) {
     const bool valid = it.meta & (1u << 8), isfull = it.meta & (1u << 9), issmall = it.meta & (1u << 10);
     const int zr = (int)(it.meta & 0xFFu) - 1;
-    const uint32_t own = chunk_value<TINY>(lds, it.ch, zr, valid ? inv_start(lds, zr) : 0u, base0, base1);
+    const uint32_t own = chunk_value<TINY>(lds, it.ch, zr, zr, valid ? inv_start(lds, zr) : 0u, base0, base1);
     uint32_t v = lane_shift(lds, own, lanebase);   // A_{96 j}
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
     v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
@@ -1268,7 +1316,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
                 const int zr = (on && k == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
                 Chunk c;
                 issue_any<TINY>(p, cstart, on && zr < kChunkBytes, c);
-                const uint32_t r = chunk_value<TINY>(lds, c, zr, (on && k == 0) ? inv_start(lds, zr) : 0u,
+                const uint32_t r = chunk_value<TINY>(lds, c, zr, on ? zr : 0, (on && k == 0) ? inv_start(lds, zr) : 0u,
                                                      base0, base1);
                 s = on ? (k == 0 ? r : uniform_shift<kLdsJump>(lds, s, r)) : s;
             }
@@ -1322,7 +1370,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     mark[lane] = 0;
     // windows of 64 frames from the dispenser (dynamic chunks of up to 16 windows when p.ctr is set)
     Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
-                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, 16);
+                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
     for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
         const uint64_t w0 = win * 64;
         // ---- window metadata: lane i <-> frame w0 + i ----
@@ -1376,7 +1424,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 #pragma unroll
             for (int q = 0; q < 6; q++) v ^= it.ch.x[q].x ^ it.ch.x[q].y ^ it.ch.x[q].z ^ it.ch.x[q].w;
 #else
-            const uint32_t own = chunk_value<TINY>(lds, it.ch, it.zr, it.valid ? inv_start(lds, it.zr) : 0u, base0, base1);
+            // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
+            const uint32_t own = chunk_value<TINY>(lds, it.ch, it.zr, it.zr < kChunkBytes ? it.zr : 0,
+                                                   it.valid ? inv_start(lds, it.zr) : 0u, base0, base1);
             const uint32_t v = chunk_shift(lds, own, it.c & 15u);
 #endif
             if (it.valid && v) atomicXor(&acc[it.src], v);
@@ -1426,7 +1476,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
                     const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
                     Chunk cc;
                     issue_any<TINY>(p, cstart, on && zr < kChunkBytes, cc);
-                    const uint32_t r = chunk_value<TINY>(lds, cc, zr, (on && q == 0) ? inv_start(lds, zr) : 0u,
+                    const uint32_t r = chunk_value<TINY>(lds, cc, zr, on ? zr : 0, (on && q == 0) ? inv_start(lds, zr) : 0u,
                                                          base0, base1);
                     s = on ? (q == 0 ? r : uniform_shift<kLdsJump>(lds, s, r)) : s;
                 }

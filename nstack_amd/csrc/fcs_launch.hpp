@@ -22,7 +22,7 @@ struct KParams {
     uint64_t *dbg;          // diagnostic stamp sink (FCS_STAMPS builds only; null otherwise)
     uint8_t *ok;            // verify mode: ok[i] = 1 iff frame i (FCS trailer included) checks
     unsigned long long *bad;//   ... and *bad += number of frames that do not (else both null)
-    unsigned long long *ctr;// LDS-DMA kernel: zeroed device counter for the dynamic tail (null: static)
+    unsigned long long *ctr;// zeroed device work counter for a dynamic schedule (null: static interleave)
 };
 
 // Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). The 1504..1536-B

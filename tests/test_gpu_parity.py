@@ -475,3 +475,17 @@ def test_flat_kernel_dynamic_windows(dev, oracle, mode):
         d = to_dev(host, dev)
         got = run_fixed(dev, d.data_ptr() + 1, L, L, n)
         assert np.array_equal(got, oracle_fixed(oracle, host[1:], L, L, n))
+
+
+@pytest.mark.parametrize("L,stride,n,lead", [(2000, 2000, 70001, 1), (1540, 1544, 90003, 0),
+                                            (9000, 9000, 40001, 3), (9018, 9024, 33333, 2)])
+def test_generic_kernel_dynamic_units(dev, oracle, L, stride, n, lead):
+    """Fixed-length batches of >= 4 units (4 frames, one per quarter-wave) per wave of the grid take
+    their units from the work counter (guided chunks): every frame against the oracle, twice on
+    the same stream (the counter ring's next slot)."""
+    host = np.random.default_rng(L + n).integers(0, 256, n * stride + 8, dtype=np.uint8)
+    d = to_dev(host, dev)
+    exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+    for _ in range(2):
+        got = run_fixed(dev, d.data_ptr() + lead, stride, L, n)
+        assert np.array_equal(got, exp), int(np.argmax(got != exp))
