@@ -915,17 +915,28 @@ __device__ __forceinline__ uint32_t merge_shift_dma(const uint8_t *lds, int m, u
 // The slot DMA: six 1 KiB rows from two address registers. The instruction's offset (13-bit,
 // 0 .. 3 KiB here) applies to the global AND the LDS address, so each group of rows passes the
 // same LDS base (one M0 value).
-__device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int lane) {
+// The first and last row of an item share their 128-B lines with the neighbouring items: those
+// two rows keep the default cache policy (the line stays in L2 for the neighbour), the middle
+// rows are non-temporal; the last row is trimmed to the lanes the item's bytes reach. Both +1.1 %
+// on 64 M x 1518 B (tools/ab.py).
+#ifndef FCS_DMA_EDGE_AUX   // measurement-only override
+#define FCS_DMA_EDGE_AUX 0
+#endif
+__device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int lane, uint32_t need) {
     typedef __attribute__((address_space(3))) void lds_void;
     static_assert(kDmaItemBytes == 6 * 1024, "six rows");
     const uint64_t a = src + 16 * (uint64_t)lane, b = a + 4096;
     lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_AUX);
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_EDGE_AUX);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_AUX);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
     __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
+#ifndef FCS_DMA_NO_TRIM   // measurement-only: FCS_DMA_NO_TRIM loads the whole last row
+    if (5120u + 16u * (uint32_t)lane < need)
+#endif
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_EDGE_AUX);
+    (void)need;
 }
 
 // MW: words a front mask can touch (host-selected: 2 when the front lane masks at most 8 bytes,
@@ -995,7 +1006,12 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
                 (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
     uint64_t it = D.first();
     auto item_start = [&](uint64_t i) { return p.base + 4 * i * p.stride; };   // first frame of item i
-    if (it != kEnd) dma_item(slot0, slot_src(item_start(it)), lane);
+    // slot bytes an item's windows read: up to its last frame's end plus the realignment dword
+    auto item_need = [&](uint64_t S, uint64_t src) {
+        const uint64_t e = S + 3 * p.stride + p.flen + 4 - src;
+        return (uint32_t)(e < (uint64_t)kDmaItemBytes ? e : (uint64_t)kDmaItemBytes);
+    };
+    if (it != kEnd) dma_item(slot0, slot_src(item_start(it)), lane, item_need(item_start(it), slot_src(item_start(it))));
 
 #ifdef FCS_STAMPS   // measurement-only: per-wave cycles waiting for the slot vs. the whole item
     uint64_t st_wait = 0, st_all = 0, st_items = 0;
@@ -1031,7 +1047,10 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
         const uint64_t nxt = D.next(it);
-        if (nxt != kEnd) dma_item(slot, slot_src(item_start(nxt)), lane);
+        if (nxt != kEnd) {
+            const uint64_t Sn = item_start(nxt), sn = slot_src(Sn);
+            dma_item(slot, sn, lane, item_need(Sn, sn));
+        }
 
         if (STREAM) {   // read ceiling: the words are only XORed together
             uint32_t acc = r;
