@@ -922,33 +922,35 @@ __device__ __forceinline__ uint32_t merge_shift_dma(const uint8_t *lds, int m, u
 #ifndef FCS_DMA_EDGE_AUX   // measurement-only override
 #define FCS_DMA_EDGE_AUX 0
 #endif
+// TRIM_ALL (segmented kernel, whose items can be shorter than 5 KiB): every row only as far as
+// the item's bytes reach.
+template <bool TRIM_ALL = false>
 __device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int lane, uint32_t need) {
     typedef __attribute__((address_space(3))) void lds_void;
     static_assert(kDmaItemBytes == 6 * 1024, "six rows");
     const uint64_t a = src + 16 * (uint64_t)lane, b = a + 4096;
     lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_EDGE_AUX);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_AUX);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
+    const uint32_t o = 16u * (uint32_t)lane;
+    if (!TRIM_ALL || o < need)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_EDGE_AUX);
+    if (!TRIM_ALL || 1024u + o < need)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_AUX);
+    if (!TRIM_ALL || 2048u + o < need)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
+    if (!TRIM_ALL || 3072u + o < need)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
+    if (!TRIM_ALL || 4096u + o < need)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
 #ifndef FCS_DMA_NO_TRIM   // measurement-only: FCS_DMA_NO_TRIM loads the whole last row
-    if (5120u + 16u * (uint32_t)lane < need)
+    if (5120u + o < need)
 #endif
         __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_EDGE_AUX);
     (void)need;
 }
 
-// MW: words a front mask can touch (host-selected: 2 when the front lane masks at most 8 bytes,
-// i.e. len >= 1516, else kSingleMaskWords).
-// STREAM: the measurement form behind fcs_dma_stream_dev: the same slot DMA, schedule and window
-// reads, no CRC work (bench.py's LDS-DMA read ceiling beside the plain read stream).
-template <int MW, bool STREAM>
-__global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
-    const int tid = threadIdx.x;
-    // ---- table image: slice tables (16-B stores of one value: 4 replicas), lane tables, merge
-    //      tables, INV ----
+// Table image of the LDS-DMA kernels: slice tables (16-B stores of one value: 4 replicas), lane
+// tables, merge tables, INV.
+__device__ __forceinline__ void stage_dma_tables(const KParams &p, uint8_t *lds, int tid) {
     for (int i = tid; i < 2048; i += kDmaWgThreads) {   // row e = i >> 3; store j = i & 7 -> slot j >> 1
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
@@ -965,6 +967,17 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     for (int i = tid; i < kChunkBytes; i += kDmaWgThreads)
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
             p.blob[kBlobInv + i];
+}
+
+// MW: words a front mask can touch (host-selected: 2 when the front lane masks at most 8 bytes,
+// i.e. len >= 1516, else kSingleMaskWords).
+// STREAM: the measurement form behind fcs_dma_stream_dev: the same slot DMA, schedule and window
+// reads, no CRC work (bench.py's LDS-DMA read ceiling beside the plain read stream).
+template <int MW, bool STREAM>
+__global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
+    const int tid = threadIdx.x;
+    stage_dma_tables(p, lds, tid);
     init_bad<kDmaBad>(lds);
     __syncthreads();
 
@@ -1112,6 +1125,248 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         p.dbg[wv * 8 + 7] = __builtin_amdgcn_s_getreg(/*HW_REG_XCC_ID*/ (20 << 0) | (0 << 6) | (3 << 11));
     }
 #endif
+    flush_bad<kDmaBad>(p, lds);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fixed length over 1524 B (jumbo frames, e.g. 9000 B), staged through LDS by DMA
+// (fcs_dmaseg_kernel; host-selected by fixed_dmaseg(): packed frames, stride - len <= 8, and a
+// split into m = ceil(len / 1524) segments of Ls = floor(len / m) >= 1496 bytes, the front one
+// Lf = Ls + len mod m <= 1524 bytes).
+// Every segment is then shaped like a frame of fcs_dma_kernel: its 16 lane windows end e_c bytes
+// before the segment end, and only lane 15 masks the 1524 - Ls (front: 1524 - Lf) cover bytes
+// before the segment start (loop-invariant masks); the front segment's lane 15 injects INV. The
+// frame's register is XOR_s A_{Ls s}(v_s), s = 0 for the frame's last segment.
+// The segments of a unit of F frames (F m a multiple of 4, F = 1, 2 or 4) form a stream; a wave's
+// item is 4 consecutive stream segments, one per quarter-wave, in one 6 KiB slot DMA (consecutive
+// segments of packed frames are contiguous). Quarter q advances its segment value over the
+// segments of its frame that follow in the item (A_{Ls t}, t <= 3); the frame open at the item
+// start carries its register C from the previous item, advanced by A_{Ls k} over its k segments
+// here (wave-uniform code on the four quarter values). Units come from the dispenser, so a
+// frame's segments are all processed by one wave, in order.
+// A first version cut frames into 1524-B segments from the frame end (one short front segment,
+// lanes above its first byte zeroed, a partial lane masked per item): the per-item mask code
+// broke the chain block's scheduling and ran 2-12 % slower than the register-load kernel.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kDmaSegJumpHole = kDmaInvHole + 4;   // 4 holes per table: A_{Ls k}, k = 1..4
+static_assert(kDmaSegJumpHole + 16 <= 256, "holes");
+
+// A_{Ls k}(s) for k = 1..4; k = 0 returns s. Nibble table t of A_{Ls k} at hole
+// kDmaSegJumpHole + 4 (k - 1) + t / 2, +64 B for odd t.
+__device__ __forceinline__ uint32_t seg_jump(const uint8_t *lds, uint32_t k, uint32_t s) {
+    uint32_t r[8];
+    const uint32_t kk = k ? k - 1u : 0u;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        const uint32_t base = dma_hole(kDmaSegJumpHole + 4u * kk + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1);
+        r[t] = lds_rd(lds, (sh & 0x3Cu) | base);
+    }
+    const uint32_t v = xor9(r, 0u);
+    return k ? v : s;
+}
+
+// MW: words lane 15's masks can touch (host-selected: 2 when 1524 - Lf <= 8, else kSingleMaskWords).
+template <int MW>
+__global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
+    const int tid = threadIdx.x;
+    // ---- frame geometry (wave-uniform) ----
+    const uint32_t L = p.flen;
+    const uint32_t m = (L + kDmaCover - 1) / kDmaCover;                    // segments per frame, >= 2
+    const uint32_t F = (m & 3u) == 0 ? 1u : ((m & 1u) == 0 ? 2u : 4u);     // frames per unit
+    const uint32_t Ls = L / m, Lf = L - Ls * (m - 1);                        // segment, front segment
+
+    stage_dma_tables(p, lds, tid);
+    for (int i = tid; i < 4 * 128; i += kDmaWgThreads) {   // segment jumps A_{Ls k}, k = 1..4
+        const int k = i >> 7, t = (i >> 4) & 7, e = i & 15;
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaSegJumpHole + 4u * (uint32_t)k + (uint32_t)(t >> 1)) +
+                                      64u * (uint32_t)(t & 1) + 4u * (uint32_t)e) =
+            p.blob[kBlobSegJump + (Ls - kDmaMinLen) * 512u + (uint32_t)i];
+    }
+    init_bad<kDmaBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const int c = lane & (kGroup - 1);        // window index back from the segment end
+    const uint32_t q = (uint32_t)lane >> 4;   // quarter: stream segment 4 j + q of the item
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
+    const uint32_t ec = dma_end_off(c);
+
+    // loop invariants: lane 15 masks the cover bytes before its segment (front and other
+    // segments), lanes 3/7/11 their overlap word; INV start of the front segment's lane 15
+    const int zn = (c == kGroup - 1) ? (int)(kDmaCover - Ls) : (dma_short_lane(c) ? 4 : 0);
+    const int zf = (c == kGroup - 1) ? (int)(kDmaCover - Lf) : (dma_short_lane(c) ? 4 : 0);
+    static_assert(MW >= 1 && MW <= kSingleMaskWords, "mask words");
+    uint32_t mn[MW], mf[MW];
+#pragma unroll
+    for (int i = 0; i < MW; i++) {
+        int t = zn - 4 * i, u = zf - 4 * i;
+        t = t < 0 ? 0 : (t > 4 ? 4 : t);
+        u = u < 0 ? 0 : (u > 4 ? 4 : u);
+        mn[i] = (uint32_t)(0xFFFFFFFFull << (8 * t));
+        mf[i] = (uint32_t)(0xFFFFFFFFull << (8 * u));
+    }
+    const uint32_t x0f = (c == kGroup - 1)
+                             ? lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zf / 32u) + (uint32_t)(zf % 32) * 4u)
+                             : 0u;
+
+    const uint64_t lo16 = p.lo4 & ~15ull;
+    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start inside the arena
+    auto slot_src = [&](uint64_t S) {
+        const uint64_t a = S & ~15ull;
+        return a < lo16 ? lo16 : (a > smax ? smax : a);
+    };
+    constexpr uint64_t kEnd = Dispenser::kEnd;
+    const uint64_t units = (p.n + F - 1) / F;
+    const uint32_t per_unit = F * m / 4;                                    // items of a full unit
+    const uint32_t cmax = per_unit >= 64 ? 1u : 64u / per_unit;
+    Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kDmaWaves, (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave,
+                lane, 100, 1, cmax);
+
+    // Item state, wave-uniform: unit u (frames u F ..), item j of J, and the stream position of
+    // quarter 0: frame fi0 of the unit, segment r0 counted from the frame's front (s = m - 1 - r).
+    struct It {
+        uint64_t u, fb0, src;   // fb0: start of quarter 0's frame; src: slot start
+        uint32_t j, J, Fu, fi0, r0, need;
+    };
+    auto seg_end = [&](uint32_t r) { return (uint64_t)Lf + (uint64_t)Ls * r; };   // from the frame start
+    auto place = [&](It &t) {
+        t.fb0 = p.base + (t.u * F + t.fi0) * p.stride;
+        t.src = slot_src(t.fb0 + (t.r0 ? seg_end(t.r0 - 1) : 0));
+        const uint32_t last = 4 * t.j + 3 < t.Fu * m ? 3u : t.Fu * m - 1u - 4 * t.j;   // last active quarter
+        uint32_t fi = 0, r = t.r0 + last;
+        while (r >= m) {
+            r -= m;
+            fi++;
+        }
+        const uint64_t nb = t.fb0 + fi * p.stride + seg_end(r) + 4 - t.src;
+        t.need = (uint32_t)(nb < (uint64_t)kDmaItemBytes ? nb : (uint64_t)kDmaItemBytes);
+    };
+    auto start_unit = [&](It &t, uint64_t u) {
+        t.u = u;
+        t.j = 0;
+        t.fi0 = 0;
+        t.r0 = 0;
+        const uint64_t left = p.n - u * F;
+        t.Fu = left < F ? (uint32_t)left : F;
+        t.J = (t.Fu * m + 3u) / 4u;
+        place(t);
+    };
+
+    It cur{};
+    bool live = false;
+    {
+        const uint64_t u0 = D.first();
+        if (u0 != kEnd) {
+            start_unit(cur, u0);
+            live = true;
+            dma_item<true>(slot, cur.src, lane, cur.need);
+        }
+    }
+    uint32_t C = 0;   // register of the frame open at the item start (wave-uniform)
+    while (live) {
+        // this lane's segment: quarter q = stream position (fi0, r0) + q
+        uint32_t dfi = 0, r = cur.r0 + q;
+        while (r >= m) {
+            r -= m;
+            dfi++;
+        }
+        const bool act = cur.fi0 + dfi < cur.Fu;
+        const uint32_t s = m - 1u - r;
+        const bool front = r == 0;
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot DMA has landed
+        const int64_t x = act ? (int64_t)(cur.fb0 + dfi * p.stride + seg_end(r) - cur.src) - (int64_t)ec - kChunkBytes : 0;
+        const uint32_t ra = (uint32_t)x & 3u;
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
+        uint32_t d[kChunkWords + 1];
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) d[i] = wp[i];
+        {
+            const uint64_t a24 = (uint64_t)(wp + kChunkWords), lim = (uint64_t)(slot + kDmaItemBytes - 4);
+            d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+
+        // ---- the next item (same unit, or the dispenser's next unit): its DMA lands meanwhile ----
+        It nxt = cur;
+        bool nlive = true;
+        if (cur.j + 1 < cur.J) {
+            nxt.j++;
+            nxt.r0 += 4;
+            while (nxt.r0 >= m) {
+                nxt.r0 -= m;
+                nxt.fi0++;
+            }
+            place(nxt);
+        } else {
+            const uint64_t un = D.next(cur.u);
+            nlive = un != kEnd;
+            if (nlive) start_unit(nxt, un);
+        }
+        if (nlive) dma_item<true>(slot, nxt.src, lane, nxt.need);
+
+        // ---- this item's segment values ----
+        uint32_t w[kChunkWords];
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ra);
+#pragma unroll
+        for (int i = 0; i < MW; i++) w[i] &= front ? mf[i] : mn[i];
+        constexpr int CL = kDmaChainWords;
+        uint32_t xs[kDmaChains];
+#pragma unroll
+        for (int hh = 0; hh < kDmaChains; hh++) xs[hh] = w[hh * CL] ^ (hh == 0 && front ? x0f : 0u);
+#pragma unroll
+        for (int i = 0; i < CL; i++)
+#pragma unroll
+            for (int hh = 0; hh < kDmaChains; hh++)
+                xs[hh] = step4_l8(lds, xs[hh], i < CL - 1 ? w[hh * CL + i + 1] : 0u, B, SEL);
+        uint32_t mv = xs[kDmaChains - 1];
+#pragma unroll
+        for (int hh = 0; hh < kDmaChains - 1; hh++) mv = merge_shift_dma(lds, kDmaChains - 2 - hh, xs[hh], mv);
+        uint32_t v = lane_shift_dma(lds, mv, lanebase);
+        v = act ? v : 0u;
+        v = row_xor(v);
+        // advanced over the segments of the same frame that follow in this item
+        const uint32_t tq = s < 3u - q ? s : 3u - q;
+        const uint32_t uq = seg_jump(lds, tq, v);
+
+#ifdef FCS_SEG_ABL_NOCOMB   // measurement-only: each quarter's value stored as is (wrong FCS)
+        emit<kDmaBad>(p, lds, c == 0 && act, cur.u * F + cur.fi0 + dfi, ~uq);
+        cur = nxt;
+        live = nlive;
+        continue;
+#endif
+        // ---- per-frame accumulation (wave-uniform) ----
+        uint32_t acc = 0;
+        if (cur.r0 != 0) {   // the frame open at the item start: advance its register over its k0 segments here
+            const uint32_t s0 = m - 1u - cur.r0;
+            const uint32_t k0 = s0 + 1u < 4u ? s0 + 1u : 4u;
+            acc = (uint32_t)__builtin_amdgcn_readfirstlane((int)seg_jump(lds, k0, C));
+        }
+        uint32_t rq = cur.r0, fq = cur.fi0;
+#pragma unroll
+        for (int qq = 0; qq < 4; qq++) {
+            if (fq >= cur.Fu) break;
+            const uint32_t vq = (uint32_t)__builtin_amdgcn_readlane((int)uq, 16 * qq);
+            acc = rq == 0 ? vq : (acc ^ vq);
+            if (rq == m - 1u) emit<kDmaBad>(p, lds, lane == 0, cur.u * F + fq, ~acc);
+            if (++rq == m) {
+                rq = 0;
+                fq++;
+            }
+        }
+        C = acc;
+
+        cur = nxt;
+        live = nlive;
+    }
     flush_bad<kDmaBad>(p, lds);
 }
 
@@ -1810,6 +2065,9 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
 #endif
         }
+    } else if (!tiny && fixed_dmaseg(p)) {
+        if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dmaseg_kernel<2>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+        else hipLaunchKernelGGL((fcs_dmaseg_kernel<kSingleMaskWords>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
     } else if (!tiny && fixed_dma(p)) {
         if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dma_kernel<2, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
         else hipLaunchKernelGGL((fcs_dma_kernel<kSingleMaskWords, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);

@@ -126,8 +126,28 @@ inline bool fixed_dma(const KParams &p) {
            3 * p.stride + p.flen <= kDmaItemBytes - 18 && p.hi4 - p.lo4 >= 2 * kDmaItemBytes;
 #endif
 }
+// Segmented LDS-DMA kernel (fcs_dmaseg_kernel): frames over kDmaCover bytes that split into
+// m = ceil(len / 1524) segments of Ls = floor(len / m) >= kDmaMinLen bytes with the remainder in
+// the front one (<= kDmaCover), packed (gaps of at most 8 bytes) so four consecutive segments fit
+// one slot; the arena holds two slots.
+// Up to 5 segments (7620 B): against the register-load generic kernel (tools/ab.py) 3000 B +10 %,
+// 4500 B +8 %, 6000 B +5 %, 7500 B +1.4 %; 9000 B +0.8 %, 9018 B +-0, 16500 B -4 % (its per-item
+// jumps and carry cost what the DMA gains once the generic kernel runs several segments per frame).
+#ifndef FCS_DMASEG_MAX_GAP   // measurement-only overrides (gap -1: never)
+#define FCS_DMASEG_MAX_GAP 8
+#endif
+#ifndef FCS_DMASEG_MAX_SEGS
+#define FCS_DMASEG_MAX_SEGS 5
+#endif
+inline bool fixed_dmaseg(const KParams &p) {
+    if ((int64_t)FCS_DMASEG_MAX_GAP < 0 || p.flen <= kDmaCover || p.stride < p.flen ||
+        p.stride - p.flen > (uint64_t)FCS_DMASEG_MAX_GAP || p.hi4 - p.lo4 < 2 * kDmaItemBytes)
+        return false;
+    const uint32_t m = (p.flen + kDmaCover - 1) / kDmaCover, ls = p.flen / m;
+    return m <= FCS_DMASEG_MAX_SEGS && ls >= kDmaMinLen && p.flen - ls * (m - 1) <= kDmaCover;
+}
 inline int fixed_threads(const KParams &p) {
-    if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;
+    if (!fixed_tiny(p) && (fixed_dma(p) || fixed_dmaseg(p))) return kDmaWgThreads;
     return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;
 }
 

@@ -89,7 +89,9 @@ constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
 constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][136] (C_c, LDS order)
 constexpr uint32_t kBlobLaneDma = kBlobFlat + kFlatBytes / 4;   // uint32 [8][16][32]: A_{e_c}
 constexpr uint32_t kBlobMerge = kBlobLaneDma + 8 * 16 * 32;     // uint32 [11][8][16]: A_{8k}, k = 1..11
-constexpr uint32_t kBlobWords = kBlobMerge + 11 * 8 * 16;
+constexpr uint32_t kSegLens = kDmaCover - kDmaMinLen + 1;       // segment lengths 1496..1524
+constexpr uint32_t kBlobSegJump = kBlobMerge + 11 * 8 * 16;     // uint32 [Ls][4][8][16]: A_{Ls k}, k = 1..4
+constexpr uint32_t kBlobWords = kBlobSegJump + kSegLens * 4 * 8 * 16;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -120,10 +122,17 @@ struct Tables {
         for (; n < 0; n++) s = zunstep(s);
         return s;
     }
-    // Nibble table of A_n: entry [t][e] = A_n(e << 4t).
+    // Nibble table of A_n: entry [t][e] = A_n(e << 4t). A_n is linear: the images of the 32 bits.
     void nibble_table(long n, uint32_t out[8][16]) const {
+        uint32_t img[32];
+        for (int b = 0; b < 32; b++) img[b] = shift(1u << b, n);
         for (int t = 0; t < 8; t++)
-            for (int e = 0; e < 16; e++) out[t][e] = shift((uint32_t)e << (4 * t), n);
+            for (int e = 0; e < 16; e++) {
+                uint32_t v = 0;
+                for (int b = 0; b < 4; b++)
+                    if (e >> b & 1) v ^= img[4 * t + b];
+                out[t][e] = v;
+            }
     }
     std::vector<uint32_t> blob() const {
         std::vector<uint32_t> b(kBlobWords, 0u);
@@ -162,6 +171,12 @@ struct Tables {
             for (int t = 0; t < 8; t++)
                 for (int e = 0; e < 16; e++) b[kBlobMerge + (k - 1) * 128 + t * 16 + e] = nt[t][e];
         }
+        for (uint32_t ls = 0; ls < kSegLens; ls++)   // segment jumps of the segmented LDS-DMA kernel
+            for (int k = 1; k <= 4; k++) {
+                nibble_table((long)(kDmaMinLen + ls) * k, nt);
+                for (int t = 0; t < 8; t++)
+                    for (int e = 0; e < 16; e++) b[kBlobSegJump + ls * 512 + (k - 1) * 128 + t * 16 + e] = nt[t][e];
+            }
         return b;
     }
     // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.
