@@ -2,7 +2,8 @@
 # Round profile bundle (GPU box): rocprofv3 kernel-trace stats of the default bench command (its
 # JSON line and the kernel statistics come from the same process), then separate PMC passes
 # (FETCH_SIZE, WRITE_SIZE; one counter group per run) for the HBM traffic of the headline kernel
-# (64 M x 1518 B) and of the IMIX flat kernel (BASELINE configs[2]). Outputs under $1.
+# (64 M x 1518 B), of the IMIX flat kernel (BASELINE configs[2]) and of the 9000-B jumbo frames
+# generic kernel (configs[3]). Outputs under $1.
 set -u
 OUT=${1:-gpurun_out/prof}; mkdir -p "$OUT"; export TMPDIR=/tmp
 step() {   # tag, timeout, command...
@@ -17,4 +18,6 @@ step pmc_fetch 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_fet
 step pmc_write 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/pmc_write" -o run --pmc WRITE_SIZE -- python3 tools/prof_fixed.py --reps 3
 step imix_fetch 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/imix_fetch" -o run --pmc FETCH_SIZE -- python3 tools/prof_fixed.py --reps 3 --imix --frames 134217728
 step imix_write 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/imix_write" -o run --pmc WRITE_SIZE -- python3 tools/prof_fixed.py --reps 3 --imix --frames 134217728
+step jumbo_fetch 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/jumbo_fetch" -o run --pmc FETCH_SIZE -- python3 tools/prof_fixed.py --reps 3 --len 9000 --frames 16777216
+step jumbo_write 300 rocprofv3 --kernel-trace --output-format csv -d "$OUT/jumbo_write" -o run --pmc WRITE_SIZE -- python3 tools/prof_fixed.py --reps 3 --len 9000 --frames 16777216
 exit 0
