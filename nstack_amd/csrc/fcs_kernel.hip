@@ -1615,6 +1615,16 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
 // accumulator (ds_xor). At the end of the window lane i stores frame i's FCS: one coalesced
 // store per window. Frames over 1536 bytes take the segment loop of fcs_var_kernel.
 // ---------------------------------------------------------------------------------------------
+// Lanes of one wave handing values to each other through LDS (marks, frame lists, accumulators):
+// under the HIP memory model that is a data race unless ordered, and the compiler did exploit it
+// (it moved a lane's read of mark[lane] into the branch where that lane itself writes a mark).
+// A wavefront-scope fence plus a wave barrier orders the writes before the other lanes' reads.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ uint32_t chunk_shift(const uint8_t *lds, uint32_t s, uint32_t c) {
     uint32_t r[8];
     const uint32_t base = kLdsFlat + c * kFlatStride;
@@ -1665,6 +1675,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
         const uint64_t fmask = __ballot(k != 0);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
         if (k) list[rank] = (uint8_t)lane;
+        wave_lds_sync();
         const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
 
         // one item = 64 chunks; resolve lane -> (frame, chunk) and issue its loads
@@ -1678,6 +1689,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
             // frame starts inside this item: mark their slot, then lane g finds its frame's rank
             // as (frames started before the item) + (marks at or below g) - 1
             if (k && P >= g0 && P < g0 + 64) mark[P - g0] = (uint8_t)tag;
+            wave_lds_sync();
             const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
             const uint64_t M = __ballot(mark[lane] == (uint8_t)tag);
             const uint32_t g = g0 + (uint32_t)lane;
@@ -1735,6 +1747,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
         if (nx) {
             const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
             if (multi) mark[rx] = (uint8_t)lane;   // the marks are free again: reuse them as the multi list
+            wave_lds_sync();
             for (uint32_t t = 0; t < nx; t += 4) {
                 const uint32_t rnk = t + (uint32_t)(lane >> 4);
                 const bool valid = rnk < nx;
@@ -1761,6 +1774,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
         }
 
         // ---- one coalesced store per window; clear the window state ----
+        wave_lds_sync();
         const uint32_t a = acc[lane];
         emit(p, lds, act, f, L ? ~a : 0u);
         acc[lane] = 0u;
@@ -1768,6 +1782,297 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     }
     flush_bad(p, lds);
 }
+
+#ifdef FCS_FLATDMA
+// ---------------------------------------------------------------------------------------------
+// MEASUREMENT-ONLY (-DFCS_FLATDMA; rejected: IMIX 4629 vs 5200 GB/s).
+// Variable-length frames, flat chunk stream, chunk windows staged through LDS by DMA
+// (fcs_flatdma_kernel; replaces fcs_flat_kernel<false> in -DFCS_FLATDMA builds).
+// The dealing of fcs_flat_kernel (64-frame windows, 64 chunks per item, frame-start marks), but
+// each lane copies its own 96-byte window into the wave's LDS slot with six
+// global_load_lds_dwordx4 at the window's exact byte address: gfx950's LDS-DMA honours any byte
+// alignment (tools/microbench/glds_align.hip), so no realignment is needed and no VGPR holds the
+// bytes in flight. Lane l's 16-byte piece i lands at slot + 1024 i + 16 l and comes back with one
+// ds_read_b128 per piece (16 lanes per 256-B bank row: 4 cycles, the minimum; random 16-B pieces
+// would cost 12, tools/microbench/lds_pat.hip). A wave deals its next item and issues that item's
+// DMA as soon as the current item's words are in registers, so the next item's bytes land while
+// the current item's CRC work runs (fcs_flat_kernel waits for each item's loads with nothing else
+// to do). An item whose windows reach before the arena start (the frames at the arena's first 96
+// bytes) is loaded into registers instead, with the arena-edge shift of the other kernels.
+// Tables: the 32 KiB slice tables of fcs_dma_kernel (step4_l8) and, in the row holes, the
+// c-indexed shift tables A_{96c} (nibble t of table c at hole 4c + t/2, +64 B for odd t), the A_48
+// merge table and INV of fcs_dma_kernel, A_1536 for frames over 1536 B, and each wave's window
+// scratch (accumulators, marks, frame lists).
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kFdJumpHole = 152;                  // A_1536: 4 holes
+constexpr uint32_t kFdWaveHole = 160;                  // 4 holes per wave: acc[0..31], acc[32..63], marks | list, multi list
+static_assert(kDmaInvHole + 4 <= kFdJumpHole && kFdWaveHole + 4 * 16 <= 256, "holes");
+constexpr uint32_t kFdSlotBytes = 6144;                // 64 lanes x 96 B, piece i of lane l at 1024 i + 16 l
+constexpr uint32_t kFlatDmaMinArena = 2 * kFdSlotBytes;
+
+__device__ __forceinline__ uint32_t fd_acc_addr(uint32_t wave, uint32_t i) {
+    return dma_hole(kFdWaveHole + 4u * wave + (i >> 5)) + (i & 31u) * 4u;
+}
+
+// A_{96c}(s), c = 0..15, from the c-indexed hole tables.
+__device__ __forceinline__ uint32_t fd_chunk_shift(const uint8_t *lds, uint32_t s, uint32_t c) {
+    uint32_t r[8];
+    const uint32_t base = dma_hole(4u * c);
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        r[t] = lds_rd(lds, base + (sh & 0x3Cu) + 256u * (uint32_t)(t >> 1) + 64u * (uint32_t)(t & 1));
+    }
+    return xor9(r, 0u);
+}
+
+// A_1536(s) ^ extra from its hole table.
+__device__ __forceinline__ uint32_t fd_jump(const uint8_t *lds, uint32_t s, uint32_t extra) {
+    uint32_t r[8];
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        r[t] = lds_rd(lds, dma_hole(kFdJumpHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) + (sh & 0x3Cu));
+    }
+    return xor9(r, extra);
+}
+
+__device__ __forceinline__ uint32_t fd_inv(const uint8_t *lds, int zr) {
+    const int zi = zr < 0 ? 0 : (zr > kChunkBytes - 1 ? kChunkBytes - 1 : zr);
+    const uint32_t iv = lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zi / 32u) + (uint32_t)(zi % 32) * 4u);
+    return (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
+}
+
+// The words of a register-loaded chunk, realigned to its start (arena edge undone).
+__device__ __forceinline__ void fd_chunk_words(const Chunk &c, uint32_t (&w)[kChunkWords]) {
+    uint32_t d[kChunkWords + 1];
+#pragma unroll
+    for (int q = 0; q < 6; q++) {
+        d[4 * q] = c.x[q].x;
+        d[4 * q + 1] = c.x[q].y;
+        d[4 * q + 2] = c.x[q].z;
+        d[4 * q + 3] = c.x[q].w;
+    }
+    d[kChunkWords] = c.x6;
+    if (__any(c.dlead)) shift_up(d, c.dlead);
+#pragma unroll
+    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], c.r);
+}
+
+// A chunk's register before its shift: bytes before the frame start masked (groups of 4 words up
+// to the wave's largest claim zb, as chunk_value), x0 injected, two 12-word chains on the 32 KiB
+// tables, A_48 merge.
+__device__ __forceinline__ uint32_t fd_value(const uint8_t *lds, uint32_t (&w)[kChunkWords], int zr, int zb, uint32_t x0,
+                                             const uint32_t (&B)[4], const uint32_t (&SEL)[4]) {
+    const int zr8 = 8 * zr;
+#pragma unroll
+    for (int g = 0; g < kChunkWords / 4; g++) {
+        if (!__any(zb > 16 * g)) break;
+#pragma unroll
+        for (int i = 4 * g; i < 4 * g + 4; i++) {
+            int t = zr8 - 32 * i;
+            t = t < 0 ? 0 : (t > 32 ? 32 : t);
+            w[i] &= (uint32_t)(0xFFFFFFFFull << t);
+        }
+    }
+    uint32_t xa = x0 ^ w[0], xb = w[12];
+#pragma unroll
+    for (int i = 0; i < 12; i++) {
+        xa = step4_l8(lds, xa, i < 11 ? w[i + 1] : 0u, B, SEL);
+        xb = step4_l8(lds, xb, i < 11 ? w[13 + i] : 0u, B, SEL);
+    }
+    return merge_shift_dma(lds, 0, xa, xb);
+}
+
+#ifndef FCS_FD_AUX   // cache policy of the window DMA (measurement-only override)
+#define FCS_FD_AUX 0
+#endif
+
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing + 16 * kFdSlotBytes];
+    static_assert(kWgThreads / 64 <= 16, "slots");
+    const int tid = threadIdx.x;
+    // ---- tables ----
+    for (int i = tid; i < 2048; i += kWgThreads) {   // slice tables as fcs_dma_kernel
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
+    }
+    for (int i = tid; i < 16 * 128; i += kWgThreads) {   // A_{96c}: table c, nibble t, entry e
+        const int c = i >> 7, t = (i >> 4) & 7, e = i & 15;
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * (uint32_t)c + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
+                                      4u * (uint32_t)e) = p.blob[kBlobFlat + c * (kFlatStride / 4) + t * 16 + e];
+    }
+    for (int i = tid; i < 128; i += kWgThreads) {   // A_48 (merge table 0 of fcs_dma_kernel) and A_1536
+        const int t = (i >> 4) & 7, e = i & 15;
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaMergeHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
+                                      4u * (uint32_t)e) = p.blob[kBlobMerge + (kDmaChainWords / 2 - 1) * 128 + i];
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdJumpHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
+                                      4u * (uint32_t)e) = p.blob[kBlobJump + i];
+    }
+    for (int i = tid; i < kChunkBytes; i += kWgThreads)
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
+            p.blob[kBlobInv + i];
+    for (int i = tid; i < 16 * 4 * 32; i += kWgThreads)   // window scratch of every wave: zero
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdWaveHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) = 0u;
+    init_bad<kDmaBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & (kGroup - 1);
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    uint8_t *slot = lds + kDmaRing + wave * kFdSlotBytes;
+    uint8_t *mark = lds + dma_hole(kFdWaveHole + 4u * wave + 2u);
+    uint8_t *list = mark + 64;
+    uint8_t *mlist = lds + dma_hole(kFdWaveHole + 4u * wave + 3u);
+    const uint32_t acc_lane = fd_acc_addr(wave, (uint32_t)lane);
+
+    struct It {
+        int src, zr;
+        uint32_t c;
+        int64_t cstart;
+        bool valid, rare;   // rare (wave-uniform): a window reaches before the arena start
+    };
+
+    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
+                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
+    uint32_t tagc = 0;   // mark tags: distinct within a window (reset with the marks)
+    for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
+        const uint64_t w0 = win * 64;
+        // ---- window metadata: lane i <-> frame w0 + i ----
+        const uint64_t f = w0 + lane;
+        const bool act = f < p.n;
+        const uint32_t L = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
+        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;
+        const bool multi = act && L > (uint32_t)kSegBytes;
+        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
+        uint32_t incl = k;   // inclusive prefix over the window
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t P = incl - k;
+        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+        const uint64_t fmask = __ballot(k != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+        mark[lane] = 0;
+        if (k) list[rank] = (uint8_t)lane;
+        wave_lds_sync();
+        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
+        tagc = 0;
+
+        // deal item g0: lane -> (frame, chunk), then issue its window DMA
+        auto prep = [&](uint32_t g0, It &it) {
+            const uint8_t tag = (uint8_t)++tagc;
+            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = tag;
+            wave_lds_sync();
+            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
+            const uint64_t M = __ballot(mark[lane] == tag);
+            const uint32_t g = g0 + (uint32_t)lane;
+            it.valid = g < K;
+            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
+            it.src = it.valid ? (int)list[rk & 63u] : 0;
+            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, it.src) << 32) | (uint32_t)__shfl((int)Elo, it.src);
+            const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
+            const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
+            it.c = it.valid ? g - Pg : 0u;   // chunk index back from the frame end
+            it.cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
+            it.zr = it.valid ? clamp_zr((int64_t)(Eg - Lg) - it.cstart) : kChunkBytes;
+            const bool need = it.valid && it.zr < kChunkBytes;
+            it.rare = __any(need && it.cstart < (int64_t)p.lo4);
+            if (!it.rare && need) {
+                typedef __attribute__((address_space(3))) void lds_void;
+                const uint64_t a = (uint64_t)it.cstart;
+#pragma unroll
+                for (int i = 0; i < 6; i++)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a + 16 * i),
+                                                     (lds_void *)(slot + 1024 * i), 16, 0, FCS_FD_AUX);
+            }
+        };
+        auto finish = [&](const It &it, uint32_t (&w)[kChunkWords]) {
+            // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
+            const uint32_t own = fd_value(lds, w, it.zr, it.zr < kChunkBytes ? it.zr : 0, it.valid ? fd_inv(lds, it.zr) : 0u,
+                                          B, SEL);
+            const uint32_t v = fd_chunk_shift(lds, own, it.c & 15u);
+            if (it.valid && v) atomicXor(reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)it.src)), v);
+        };
+
+        if (K) {
+            It cur;
+            prep(0, cur);
+            for (uint32_t g0 = 0; g0 < K; g0 += 64) {
+                uint32_t w[kChunkWords];
+                if (!cur.rare) {
+                    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's window DMA has landed
+#pragma unroll
+                    for (int i = 0; i < 6; i++) {
+                        const u32x4 x = *reinterpret_cast<const u32x4 *>(slot + 1024 * i + 16 * lane);
+                        w[4 * i] = x.x;
+                        w[4 * i + 1] = x.y;
+                        w[4 * i + 2] = x.z;
+                        w[4 * i + 3] = x.w;
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+                } else {   // the arena start: register loads with the edge shift
+                    Chunk ch;
+                    issue_any<false>(p, cur.cstart, cur.valid && cur.zr < kChunkBytes, ch);
+                    fd_chunk_words(ch, w);
+                }
+                It nxt;
+                nxt.valid = false;
+                if (g0 + 64 < K) prep(g0 + 64, nxt);
+                finish(cur, w);
+                cur = nxt;
+            }
+        }
+
+        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment (register loads) ----
+        const uint64_t xmask = __ballot(multi);
+        const uint32_t nx = (uint32_t)__popcll(xmask);
+        if (nx) {
+            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
+            if (multi) mlist[rx] = (uint8_t)lane;
+            wave_lds_sync();
+            for (uint32_t t = 0; t < nx; t += 4) {
+                const uint32_t rnk = t + (uint32_t)(lane >> 4);
+                const bool valid = rnk < nx;
+                const int src = valid ? (int)mlist[rnk] : 0;
+                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
+                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
+                uint32_t s = 0;
+                for (uint32_t q = 0; __any(q < m); q++) {
+                    const bool on = q < m;
+                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
+                                           (int64_t)kChunkBytes * (j + 1);
+                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
+                    Chunk cc;
+                    issue_any<false>(p, cstart, on && zr < kChunkBytes, cc);
+                    uint32_t w[kChunkWords];
+                    fd_chunk_words(cc, w);
+                    const uint32_t r = fd_value(lds, w, zr, on ? zr : 0, (on && q == 0) ? fd_inv(lds, zr) : 0u, B, SEL);
+                    s = on ? (q == 0 ? r : fd_jump(lds, s, r)) : s;
+                }
+                const uint32_t v = row_xor(fd_chunk_shift(lds, s, (uint32_t)j));
+                if (valid && j == 15) *reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)src)) = v;
+            }
+        }
+
+        // ---- one coalesced store per window; clear the accumulators ----
+        wave_lds_sync();
+        uint32_t *accp = reinterpret_cast<uint32_t *>(lds + acc_lane);
+        const uint32_t a = *accp;
+        emit<kDmaBad>(p, lds, act, f, L ? ~a : 0u);
+        *accp = 0u;
+    }
+    flush_bad<kDmaBad>(p, lds);
+}
+#endif  // FCS_FLATDMA
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -2059,8 +2364,10 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             hipLaunchKernelGGL((fcs_flat_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
 #endif
         } else {
-#ifdef FCS_VAR_HALFUNIT
+#if defined(FCS_VAR_HALFUNIT)
             hipLaunchKernelGGL((fcs_var_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+#elif defined(FCS_FLATDMA)   // measurement-only build: per-lane window DMA (rejected)
+            hipLaunchKernelGGL(fcs_flatdma_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
 #else
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
 #endif
