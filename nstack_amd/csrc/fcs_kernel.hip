@@ -26,6 +26,7 @@
 
 #include "fcs_launch.hpp"
 #include "fcs_tables.hpp"
+#include "wave_sync.hpp"
 
 namespace fcs {
 
@@ -1615,16 +1616,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
 // accumulator (ds_xor). At the end of the window lane i stores frame i's FCS: one coalesced
 // store per window. Frames over 1536 bytes take the segment loop of fcs_var_kernel.
 // ---------------------------------------------------------------------------------------------
-// Lanes of one wave handing values to each other through LDS (marks, frame lists, accumulators):
-// under the HIP memory model that is a data race unless ordered, and the compiler did exploit it
-// (it moved a lane's read of mark[lane] into the branch where that lane itself writes a mark).
-// A wavefront-scope fence plus a wave barrier orders the writes before the other lanes' reads.
-__device__ __forceinline__ void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 __device__ __forceinline__ uint32_t chunk_shift(const uint8_t *lds, uint32_t s, uint32_t c) {
     uint32_t r[8];
     const uint32_t base = kLdsFlat + c * kFlatStride;
@@ -2259,7 +2250,7 @@ __device__ __forceinline__ uint32_t one_frame_reg(uint32_t *t, const uint32_t *b
             w[i] = v & (uint32_t)(0xFFFFFFFFull << (8 * z));
         }
     }
-    __builtin_amdgcn_wave_barrier();                   // window reads done before the next frame's copy
+    wave_lds_sync();                                   // window reads done before the next frame's copy
     uint32_t x = w[0];
 #pragma unroll
     for (int i = 0; i < 6; i++) x = one_step(t, x, i < 5 ? w[i + 1] : 0u);

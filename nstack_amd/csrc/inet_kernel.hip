@@ -28,6 +28,7 @@
 #include <stdint.h>
 
 #include "inet_launch.hpp"
+#include "wave_sync.hpp"
 
 namespace inet {
 
@@ -225,6 +226,7 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
         const uint64_t fmask = __ballot(k != 0);
         const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
         if (k) list[rank] = (uint8_t)lane;
+        wave_lds_sync();
         const uint32_t c0lo = (uint32_t)c0, c0hi = (uint32_t)(c0 >> 32);
         const uint32_t edges = (uint32_t)(start & 15) | ((uint32_t)((start + len) & 15) << 8);
 
@@ -232,8 +234,10 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
             // a long packet spans any number of items, so marks are cleared after use (not tagged)
             const bool starts = k && P >= g0 && P < g0 + 64;
             if (starts) mark[P - g0] = 1;
+            wave_lds_sync();
             const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
             const uint64_t M = __ballot(mark[lane] != 0);
+            wave_lds_sync();
             if (starts) mark[P - g0] = 0;
             const uint32_t g = g0 + (uint32_t)lane;
             const bool valid = g < K;
@@ -278,6 +282,7 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
         }
 
         // ---- packet i: fold, odd-start swap, pseudo header and init, complement; clear state ----
+        wave_lds_sync();
         const uint32_t m0 = fold64(acc[lane]);
         const uint32_t m = (start & 1) ? swap16(m0) : m0;   // odd start: P = swap16(fold(M))
         if (act) p.out[i] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, i, len) + m);
