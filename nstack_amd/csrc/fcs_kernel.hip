@@ -1668,6 +1668,17 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
         if (k) list[rank] = (uint8_t)lane;
         wave_lds_sync();
         const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
+#ifndef FCS_FLAT_NO_SHORTCUTS   // measurement-only: always the list read and four bpermutes
+        // common windows: no frame over 1536 B (the frames with chunks are lanes 0, 1, ..., so a
+        // chunk's frame rank is its frame's lane: no list read), and all frame ends in one 4 GiB
+        // page of addresses (the high word is shared: one bpermute fewer)
+        const bool dense = __ballot(multi) == 0;
+        const uint32_t Ehi0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)Ehi);
+        const bool onehi = __ballot(Ehi != Ehi0) == 0;
+#else
+        const bool dense = false, onehi = false;
+        const uint32_t Ehi0 = 0;
+#endif
 
         // one item = 64 chunks; resolve lane -> (frame, chunk) and issue its loads
         struct FlatItem {
@@ -1686,8 +1697,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
             const uint32_t g = g0 + (uint32_t)lane;
             it.valid = g < K;
             const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
-            it.src = it.valid ? (int)list[rk & 63u] : 0;
-            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, it.src) << 32) | (uint32_t)__shfl((int)Elo, it.src);
+            it.src = it.valid ? (dense ? (int)(rk & 63u) : (int)list[rk & 63u]) : 0;
+            const uint32_t Eghi = onehi ? Ehi0 : (uint32_t)__shfl((int)Ehi, it.src);
+            const uint64_t Eg = ((uint64_t)Eghi << 32) | (uint32_t)__shfl((int)Elo, it.src);
             const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
             const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
             it.c = it.valid ? g - Pg : 0u;   // chunk index back from the frame end
