@@ -1938,6 +1938,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
         int src, zr;
         uint32_t c;
         int64_t cstart;
+        uint64_t base;      // chunk-major DMA: lane 0's window start, and this lane's offset from it
+        int relv;
         bool valid, rare;   // rare (wave-uniform): a window reaches before the arena start
     };
 
@@ -1987,17 +1989,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
             it.cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
             it.zr = it.valid ? clamp_zr((int64_t)(Eg - Lg) - it.cstart) : kChunkBytes;
             const bool need = it.valid && it.zr < kChunkBytes;
-#ifdef FCS_FD_PERLANE   // measurement-only: each lane DMAs its own window (scattered 16-B pieces)
-            it.rare = __any(need && it.cstart < (int64_t)p.lo4);
-            if (!it.rare && need) {
-                typedef __attribute__((address_space(3))) void lds_void;
-                const uint64_t a = (uint64_t)it.cstart;
-#pragma unroll
-                for (int i = 0; i < 6; i++)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a + 16 * i),
-                                                     (lds_void *)(slot + 1024 * i), 16, 0, FCS_FD_AUX);
-            }
-#else
             // chunk-major DMA: instruction i, lane l copies piece m of chunk q (6 q + m = 64 i + l)
             // to slot + 96 q + 16 m, so the 6 lanes of a chunk read its 96 contiguous bytes and
             // consecutive chunks of a frame are adjacent runs; chunk addresses travel as 32-bit
@@ -2007,19 +1998,22 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
             const int64_t rel = it.cstart - (int64_t)base;
             const bool far = rel < -(int64_t)0x3FFFFFFF || rel > (int64_t)0x3FFFFFFF;
             it.rare = __any(need && (it.cstart < (int64_t)p.lo4 || far));
+            it.base = base;
+            it.relv = need ? (int)rel : (int)0x80000000;
+        };
+        // the item's window DMA (after its dealing, once the slot is free)
+        auto dma = [&](const It &it) {
             if (!it.rare) {
                 typedef __attribute__((address_space(3))) void lds_void;
-                const int relv = need ? (int)rel : (int)0x80000000;
 #pragma unroll
                 for (int i = 0; i < 6; i++) {
                     const uint32_t t = 64u * (uint32_t)i + (uint32_t)lane, q = t / 6u, m = t - 6u * q;
-                    const int rq = __shfl(relv, (int)q);
+                    const int rq = __shfl(it.relv, (int)q);
                     if (rq != (int)0x80000000)
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(base + (int64_t)rq + 16 * m),
+                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(it.base + (int64_t)rq + 16 * m),
                                                          (lds_void *)(slot + 1024 * i), 16, 0, FCS_FD_AUX);
                 }
             }
-#endif
         };
         auto finish = [&](const It &it, uint32_t (&w)[kChunkWords]) {
             // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
@@ -2032,17 +2026,19 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
         if (K) {
             It cur;
             prep(0, cur);
+            dma(cur);
             for (uint32_t g0 = 0; g0 < K; g0 += 64) {
                 uint32_t w[kChunkWords];
+                // the next item's dealing first: its LDS round trips overlap this item's DMA wait
+                It nxt;
+                nxt.valid = false;
+                const bool more = g0 + 64 < K;
+                if (more) prep(g0 + 64, nxt);
                 if (!cur.rare) {
                     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's window DMA has landed
 #pragma unroll
                     for (int i = 0; i < 6; i++) {
-#ifdef FCS_FD_PERLANE
-                        const u32x4 x = *reinterpret_cast<const u32x4 *>(slot + 1024 * i + 16 * lane);
-#else
                         const u32x4 x = *reinterpret_cast<const u32x4 *>(slot + 96 * lane + 16 * i);
-#endif
                         w[4 * i] = x.x;
                         w[4 * i + 1] = x.y;
                         w[4 * i + 2] = x.z;
@@ -2054,9 +2050,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
                     issue_any<false>(p, cur.cstart, cur.valid && cur.zr < kChunkBytes, ch);
                     fd_chunk_words(ch, w);
                 }
-                It nxt;
-                nxt.valid = false;
-                if (g0 + 64 < K) prep(g0 + 64, nxt);
+                if (more) dma(nxt);
                 finish(cur, w);
                 cur = nxt;
             }
