@@ -295,7 +295,9 @@ def main():
         # gloo on the host: the barrier and the 8-byte max-over-ranks of the elapsed time are the
         # only cross-rank traffic; frames never leave their GPU (no RCCL, BASELINE north_star)
         import torch.distributed as dist
-        torch.cuda.set_device(local)
+        # one GPU per rank; on a box with fewer GPUs than ranks (a rehearsal of the N > 1 path)
+        # ranks share them round-robin
+        torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
         dist.init_process_group("gloo")
     else:
         torch.cuda.set_device(0)
