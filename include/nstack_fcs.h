@@ -65,6 +65,9 @@ uint64_t fcs_engine_set_var_threshold(uint64_t frames);
  * succeeded, and lanes (stream + result word) dropped after a failure. Any pointer may be NULL. */
 void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t *dropin_recovered,
                       uint64_t *lane_resets);
+/* Host batch paths: calls that were split over more than one engine device, and the shard jobs
+ * those calls ran (one host thread and pipeline each). Any pointer may be NULL. */
+void fcs_engine_host_stats(uint64_t *sharded_calls, uint64_t *shard_jobs);
 /* Shard planner of the host batch paths (and of bench.py's ranks): cut[0..parts] such that part g
  * is frames [cut[g], cut[g+1]). len == NULL: equal frame counts (cut[g] = n g / parts); otherwise
  * byte-balanced contiguous ranges (cut[g] = first index whose length prefix reaches g/parts of the

@@ -26,7 +26,7 @@ EXPORTS = [
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
-    "fcs_tables_blob", "fcs_engine_stats", "fcs_shard_plan", "fcs_dma_stream_dev",
+    "fcs_tables_blob", "fcs_engine_stats", "fcs_engine_host_stats", "fcs_shard_plan", "fcs_dma_stream_dev",
     # include/nstack_txq.h — batched TX call site
     "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
@@ -88,6 +88,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_timed_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, i32, c.POINTER(c.c_float)]),
         "fcs_tables_blob": (i32, [vp, u64]),
         "fcs_engine_stats": (None, [c.POINTER(u64)] * 4),
+        "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
         "fcs_txq_create": (vp, [vp, u32, u32, vp, vp]),
@@ -271,6 +272,14 @@ def engine_stats() -> dict:
     v = [c.c_uint64(0) for _ in range(4)]
     load().fcs_engine_stats(*[c.byref(x) for x in v])
     return dict(zip(("dropin_calls", "dropin_retries", "dropin_recovered", "lane_resets"), (x.value for x in v)))
+
+
+def engine_host_stats() -> dict:
+    """Host batch calls split over several engine devices, and their shard jobs (fcs_engine_host_stats)."""
+    import ctypes as c
+    v = [c.c_uint64(0) for _ in range(2)]
+    load().fcs_engine_host_stats(*[c.byref(x) for x in v])
+    return {"sharded_calls": v[0].value, "shard_jobs": v[1].value}
 
 
 def shard_plan(n: int, parts: int, lengths=None):

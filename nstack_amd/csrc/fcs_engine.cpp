@@ -175,6 +175,38 @@ const std::vector<uint32_t> &kinit_table() {
     return k;
 }
 
+// A device's state: the table images, counters and (lazily) its streams and staging buffers.
+int make_dev_state(int dev, std::unique_ptr<DevState> *out) {
+    auto st = std::make_unique<DevState>();
+    st->dev = dev;
+    int cur = 0;
+    HIPTRY(hipGetDevice(&cur), "hipGetDevice");
+    HIPTRY(hipSetDevice(dev), "hipSetDevice");
+    hipDeviceProp_t prop;
+    hipError_t pe = hipGetDeviceProperties(&prop, dev);
+    if (pe != hipSuccess) { hipSetDevice(cur); return hip_fail(pe, "hipGetDeviceProperties"); }
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        hipSetDevice(cur);
+        return fail(ENODEV, "device %d is %s; this engine is built for gfx950 only", dev, prop.gcnArchName);
+    }
+    st->cus = prop.multiProcessorCount;
+    const std::vector<uint32_t> blob = tables().blob();
+    hipError_t ae = hipMalloc(&st->d_blob, blob.size() * 4);
+    if (ae == hipSuccess) ae = hipMemcpy(st->d_blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice);
+    const std::vector<uint32_t> one = tables().one_blob();
+    if (ae == hipSuccess) ae = hipMalloc(&st->d_one_blob, one.size() * 4);
+    if (ae == hipSuccess) ae = hipMemcpy(st->d_one_blob, one.data(), one.size() * 4, hipMemcpyHostToDevice);
+    const std::vector<uint32_t> &ki = kinit_table();
+    if (ae == hipSuccess) ae = hipMalloc(&st->d_kinit, ki.size() * 4);
+    if (ae == hipSuccess) ae = hipMemcpy(st->d_kinit, ki.data(), ki.size() * 4, hipMemcpyHostToDevice);
+    if (ae == hipSuccess) ae = hipMalloc(&st->d_ctr, DevState::kCtrSlots * 64);
+    if (ae == hipSuccess) ae = hipMemset(st->d_ctr, 0, DevState::kCtrSlots * 64);
+    hipSetDevice(cur);
+    if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
+    *out = std::move(st);
+    return 0;
+}
+
 int dev_state(int dev, DevState **out) {
     std::lock_guard<std::mutex> lk(g_mu);
     int ndev = 0;
@@ -183,36 +215,32 @@ int dev_state(int dev, DevState **out) {
     if (dev < 0 || dev >= ndev) return fail(EINVAL, "device %d out of range (%d devices)", dev, ndev);
     if ((int)g_dev.size() < ndev) g_dev.resize(ndev);
     if (!g_dev[dev]) {
-        auto st = std::make_unique<DevState>();
-        st->dev = dev;
-        int cur = 0;
-        HIPTRY(hipGetDevice(&cur), "hipGetDevice");
-        HIPTRY(hipSetDevice(dev), "hipSetDevice");
-        hipDeviceProp_t prop;
-        hipError_t pe = hipGetDeviceProperties(&prop, dev);
-        if (pe != hipSuccess) { hipSetDevice(cur); return hip_fail(pe, "hipGetDeviceProperties"); }
-        if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
-            hipSetDevice(cur);
-            return fail(ENODEV, "device %d is %s; this engine is built for gfx950 only", dev, prop.gcnArchName);
-        }
-        st->cus = prop.multiProcessorCount;
-        const std::vector<uint32_t> blob = tables().blob();
-        hipError_t ae = hipMalloc(&st->d_blob, blob.size() * 4);
-        if (ae == hipSuccess) ae = hipMemcpy(st->d_blob, blob.data(), blob.size() * 4, hipMemcpyHostToDevice);
-        const std::vector<uint32_t> one = tables().one_blob();
-        if (ae == hipSuccess) ae = hipMalloc(&st->d_one_blob, one.size() * 4);
-        if (ae == hipSuccess) ae = hipMemcpy(st->d_one_blob, one.data(), one.size() * 4, hipMemcpyHostToDevice);
-        const std::vector<uint32_t> &ki = kinit_table();
-        if (ae == hipSuccess) ae = hipMalloc(&st->d_kinit, ki.size() * 4);
-        if (ae == hipSuccess) ae = hipMemcpy(st->d_kinit, ki.data(), ki.size() * 4, hipMemcpyHostToDevice);
-        if (ae == hipSuccess) ae = hipMalloc(&st->d_ctr, DevState::kCtrSlots * 64);
-        if (ae == hipSuccess) ae = hipMemset(st->d_ctr, 0, DevState::kCtrSlots * 64);
-        hipSetDevice(cur);
-        if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
-        g_dev[dev] = std::move(st);
+        int rc = make_dev_state(dev, &g_dev[dev]);
+        if (rc) return rc;
     }
     *out = g_dev[dev].get();
     return 0;
+}
+
+// Engine device ids at or past the device count (only with NSTACK_FCS_ALIAS_DEVICES=1, a test
+// hook): a state of their own on HIP device id mod count, so the multi-device host path (shard
+// plan, one thread and pipeline per device, result assembly) runs on a one-GPU box.
+std::map<int, std::unique_ptr<DevState>> g_alias;
+
+int alias_state(int id, int ndev, DevState **out) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto &slot = g_alias[id];
+    if (!slot) {
+        int rc = make_dev_state(id % ndev, &slot);
+        if (rc) return rc;
+    }
+    *out = slot.get();
+    return 0;
+}
+
+bool alias_devices_enabled() {
+    const char *e = std::getenv("NSTACK_FCS_ALIAS_DEVICES");
+    return e && std::atoi(e) != 0;
 }
 
 int current_dev_state(DevState **out) {
@@ -869,10 +897,13 @@ int engine_devices(std::vector<DevState *> *out) {
         std::lock_guard<std::mutex> lk(g_mu);
         devs = g_engine_devs;
     }
+    int ndev = 0;
+    hipError_t e = hipGetDeviceCount(&ndev);
+    if (e != hipSuccess || ndev <= 0) return fail(ENODEV, "no HIP device visible (%s)", hipGetErrorString(e));
     out->clear();
     for (int d : devs) {
         DevState *ds = nullptr;
-        int rc = dev_state(d, &ds);
+        int rc = d < ndev ? dev_state(d, &ds) : alias_state(d, ndev, &ds);
         if (rc) return rc;
         out->push_back(ds);
     }
@@ -892,6 +923,8 @@ int tx_one(uint8_t *frame, uint32_t len) {
 }
 
 
+std::atomic<uint64_t> g_sharded_calls{0}, g_shard_jobs{0};
+
 // Shard [0, n) over the engine devices (contiguous ranges, byte-balanced when lengths are known:
 // fcs_shard_plan).
 int run_host_sharded(HostJob job, uint64_t n) {
@@ -907,6 +940,8 @@ int run_host_sharded(HostJob job, uint64_t n) {
         job.i1 = n;
         return run_host_job(devs[0], job);
     }
+    g_sharded_calls.fetch_add(1, std::memory_order_relaxed);
+    g_shard_jobs.fetch_add(G, std::memory_order_relaxed);
     std::vector<int> rcs(G, 0);
     std::vector<std::string> errs(G);
     std::vector<std::thread> th;
@@ -1127,17 +1162,15 @@ int fcs_engine_init(int ndev) {
     int total = 0;
     hipError_t e = hipGetDeviceCount(&total);
     if (e != hipSuccess || total <= 0) return fail(ENODEV, "no HIP device visible (%s)", hipGetErrorString(e));
-    const int use = (ndev <= 0 || ndev > total) ? total : ndev;
+    const int use = ndev <= 0 ? total : ((ndev > total && !alias_devices_enabled()) ? total : ndev);
     {
         std::lock_guard<std::mutex> lk(g_mu);
         g_engine_devs.clear();
         for (int d = 0; d < use; d++) g_engine_devs.push_back(d);
     }
-    for (int d = 0; d < use; d++) {
-        DevState *ds = nullptr;
-        int rc = dev_state(d, &ds);
-        if (rc) return rc;
-    }
+    std::vector<DevState *> devs;
+    int rc = engine_devices(&devs);
+    if (rc) return rc;
     return use;
 }
 
@@ -1145,9 +1178,12 @@ void fcs_engine_fini(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     int cur = 0;
     (void)hipGetDevice(&cur);
-    for (auto &up : g_dev) {
-        if (!up) continue;
-        DevState *ds = up.get();
+    std::vector<DevState *> all;
+    for (auto &up : g_dev)
+        if (up) all.push_back(up.get());
+    for (auto &kv : g_alias)
+        if (kv.second) all.push_back(kv.second.get());
+    for (DevState *ds : all) {
         hipSetDevice(ds->dev);
         Pipe &pp = ds->pipe;
         for (int b = 0; b < Pipe::kDepth; b++) {
@@ -1186,6 +1222,7 @@ void fcs_engine_fini(void) {
         if (ds->d_ctr) hipFree(ds->d_ctr);
     }
     g_dev.clear();
+    g_alias.clear();
     g_engine_devs.clear();
     hipSetDevice(cur);
 }
@@ -1361,6 +1398,11 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
     std::fprintf(stderr, "nstack_fcs: ether_fcs: %s (first attempt: %s); no usable GPU engine, aborting\n",
                  g_last_error.c_str(), first.c_str());
     std::abort();
+}
+
+void fcs_engine_host_stats(uint64_t *sharded_calls, uint64_t *shard_jobs) {
+    if (sharded_calls) *sharded_calls = g_sharded_calls.load(std::memory_order_relaxed);
+    if (shard_jobs) *shard_jobs = g_shard_jobs.load(std::memory_order_relaxed);
 }
 
 void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t *dropin_recovered,
