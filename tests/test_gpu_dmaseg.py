@@ -75,7 +75,7 @@ def test_dmaseg_many_units(dev, oracle, L, stride):
         assert np.array_equal(got, exp), int(np.argmax(got != exp))
 
 
-@pytest.mark.parametrize("L", [3000, 9000, 9022])
+@pytest.mark.parametrize("L", [3000, 4500, 6000, 7500, 9000, 9022])
 def test_dmaseg_verify_mode(dev, L):
     """RX residue check through the segmented kernel: frames of L bytes carrying their FCS, a few
     corrupted; ok[] and the bad count against zlib."""
