@@ -1185,6 +1185,19 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
                                       64u * (uint32_t)(t & 1) + 4u * (uint32_t)e) =
             p.blob[kBlobSegJump + (Ls - kDmaMinLen) * 512u + (uint32_t)i];
     }
+#ifdef FCS_SEG_ABS
+    // A_{Ls k} for k = 5 .. m - 1: composed here as A_{Ls 4} o A_{Ls (k - 4)}, one k at a time
+    for (uint32_t k = 5; k < m; k++) {
+        __syncthreads();
+        if (tid < 128) {
+            const uint32_t t = (uint32_t)tid >> 4, e = (uint32_t)tid & 15u;
+            const uint32_t at = 64u * (t & 1u) + 4u * e;
+            const uint32_t prev = lds_rd(lds, dma_hole(kDmaSegJumpHole + 4u * (k - 5u) + (t >> 1)) + at);
+            const uint32_t v = seg_jump(lds, 4u, prev);
+            *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaSegJumpHole + 4u * (k - 1u) + (t >> 1)) + at) = v;
+        }
+    }
+#endif
     init_bad<kDmaBad>(lds);
     __syncthreads();
 
@@ -1336,7 +1349,14 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
         v = row_xor(v);
         // advanced over the segments of the same frame that follow in this item
         const uint32_t tq = s < 3u - q ? s : 3u - q;
+#if defined(FCS_SEG_ABL_NOJUMP)   // measurement-only: no advance over the following segments (wrong FCS)
+        const uint32_t uq = v ^ tq;
+#elif defined(FCS_SEG_ABS)
+        (void)tq;
+        const uint32_t uq = seg_jump(lds, act ? s : 0u, v);   // A_{Ls s}: its place in the frame
+#else
         const uint32_t uq = seg_jump(lds, tq, v);
+#endif
 
 #ifdef FCS_SEG_ABL_NOCOMB   // measurement-only: each quarter's value stored as is (wrong FCS)
         emit<kDmaBad>(p, lds, c == 0 && act, cur.u * F + cur.fi0 + dfi, ~uq);
@@ -1346,11 +1366,15 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
 #endif
         // ---- per-frame accumulation (wave-uniform) ----
         uint32_t acc = 0;
+#ifdef FCS_SEG_ABS
+        if (cur.r0 != 0) acc = C;
+#else
         if (cur.r0 != 0) {   // the frame open at the item start: advance its register over its k0 segments here
             const uint32_t s0 = m - 1u - cur.r0;
             const uint32_t k0 = s0 + 1u < 4u ? s0 + 1u : 4u;
             acc = (uint32_t)__builtin_amdgcn_readfirstlane((int)seg_jump(lds, k0, C));
         }
+#endif
         uint32_t rq = cur.r0, fq = cur.fi0;
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {

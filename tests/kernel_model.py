@@ -321,3 +321,41 @@ def model_dmaseg_frame(lds, blob, frame: bytes, garbage: bytes):
         v = model_segment_value(lds, cover, DMA_COVER - seg_len, r == 0)
         acc = (seg_jump(blob, ls, 1, acc) if r else 0) ^ v
     return ~acc & 0xFFFFFFFF
+
+
+def seg_place_tables(blob, ls, m):
+    """The kernel's place tables A_{Ls k}, k = 1 .. m - 1, as 8 x 16 nibble tables: k <= 4 from the
+    blob, k >= 5 composed at staging as A_{Ls 4} o A_{Ls (k - 4)}, entry by entry."""
+    tabs = {}
+    for k in range(1, min(m, 5)):
+        base = BLOB_SEG_JUMP + (ls - SEG_MIN) * 512 + (k - 1) * 128
+        tabs[k] = [int(x) for x in blob[base:base + 128]]
+    for k in range(5, m):
+        tabs[k] = [seg_jump(blob, ls, 4, e) for e in tabs[k - 4]]
+    return tabs
+
+
+def apply_nibbles(tab, s):
+    r = 0
+    for t in range(8):
+        r ^= tab[t * 16 + ((s >> (4 * t)) & 15)]
+    return r
+
+
+def model_dmaseg_frame_abs(lds, blob, frame: bytes, garbage: bytes):
+    """FCS of one frame with every segment placed directly: XOR_s A_{Ls s}(v_s), s counted from the
+    frame's last segment, with the place tables of seg_place_tables (no carry to advance)."""
+    L = len(frame)
+    m = -(-L // DMA_COVER)
+    ls = L // m
+    lf = L - ls * (m - 1)
+    tabs = seg_place_tables(blob, ls, m)
+    padded = bytes(garbage[:DMA_COVER]) + frame
+    acc = 0
+    for r in range(m):
+        end = DMA_COVER + lf + ls * r
+        seg_len = lf if r == 0 else ls
+        v = model_segment_value(lds, padded[end - DMA_COVER:end], DMA_COVER - seg_len, r == 0)
+        s_ = m - 1 - r
+        acc ^= apply_nibbles(tabs[s_], v) if s_ else v
+    return ~acc & 0xFFFFFFFF

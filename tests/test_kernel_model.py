@@ -184,3 +184,15 @@ def test_dmaseg_jump_tables_compose():
             for k in range(1, 5):
                 one = km.seg_jump(blob, ls, 1, one)
                 assert km.seg_jump(blob, ls, k, s) == one, (ls, k)
+
+
+@pytest.mark.parametrize("L", [3000, 9000, 16500, 41148])
+def test_dmaseg_place_model(lds_dma, L):
+    """The segmented kernel's placement form: each segment shifted by A_{Ls s} for its place s from
+    the frame end (tables for s >= 5 composed from the blob's A_{Ls 4}), the frame the XOR of its
+    placed segments, reproduces the CRC (zlib = src/ether_fcs.c:4-19) up to 27 segments."""
+    blob = na.tables_blob()
+    rng = np.random.default_rng(L + 1)
+    frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+    garbage = rng.integers(0, 256, 1524, dtype=np.uint8).tobytes()
+    assert km.model_dmaseg_frame_abs(lds_dma[2], blob, frame, garbage) == zlib.crc32(frame)

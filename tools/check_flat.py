@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
-"""Parity spot check of a library variant's flat (windowed) paths against zlib (measurement tool):
-fixed short frames and an IMIX batch, every frame compared. usage: NSTACK_FCS_LIB=... check_flat.py"""
+"""Parity spot check of a library variant against zlib (measurement tool): fixed short frames and an
+IMIX batch through the flat (windowed) paths, every frame compared; with --lens L1,L2,... fixed-length
+batches of those lengths instead (gaps 0 and 8, odd base), e.g. jumbo frames for the segmented kernel.
+usage: NSTACK_FCS_LIB=... check_flat.py [--lens 9000,16500]"""
 import numpy as np
 import torch
 import zlib
@@ -12,6 +14,23 @@ torch.cuda.set_device(0)
 na.load()
 dev = torch.device("cuda:0")
 bad_total = 0
+if len(sys.argv) > 2 and sys.argv[1] == "--lens":
+    for L in (int(x) for x in sys.argv[2].split(",")):
+        for gap in (0, 8):
+            stride = L + gap
+            n = max(64, (96 << 20) // stride)
+            host = np.random.default_rng(L + gap).integers(0, 256, n * stride + 64, dtype=np.uint8)
+            d = torch.from_numpy(host).to(dev)
+            out = torch.empty(n, dtype=torch.int32, device=dev)
+            na.fixed_dev(d.data_ptr() + 3, stride, L, n, out)
+            torch.cuda.synchronize()
+            got = out.cpu().numpy().view(np.uint32)
+            exp = np.array([zlib.crc32(host[3 + i * stride:3 + i * stride + L].tobytes()) for i in range(n)],
+                           dtype=np.uint32)
+            bad = int((got != exp).sum())
+            bad_total += bad
+            print("fixed", L, "stride", stride, "n", n, "bad", bad, flush=True)
+    sys.exit(1 if bad_total else 0)
 for L in (64, 100, 576, 1000, 1503):
     n = 40000
     host = np.random.default_rng(L).integers(0, 256, n * L + 64, dtype=np.uint8)
