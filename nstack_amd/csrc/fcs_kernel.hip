@@ -1140,19 +1140,24 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
 // frame's register is XOR_s A_{Ls s}(v_s), s = 0 for the frame's last segment.
 // The segments of a unit of F frames (F m a multiple of 4, F = 1, 2 or 4) form a stream; a wave's
 // item is 4 consecutive stream segments, one per quarter-wave, in one 6 KiB slot DMA (consecutive
-// segments of packed frames are contiguous). Quarter q advances its segment value over the
-// segments of its frame that follow in the item (A_{Ls t}, t <= 3); the frame open at the item
-// start carries its register C from the previous item, advanced by A_{Ls k} over its k segments
-// here (wave-uniform code on the four quarter values). Units come from the dispenser, so a
-// frame's segments are all processed by one wave, in order.
+// segments of packed frames are contiguous). Quarter q places its segment value in its frame with
+// one table shift, A_{Ls s} (the place tables for s = 1 .. m - 1: s <= 4 from the blob, the rest
+// composed at staging); a frame's register is then the plain XOR of its placed segments, summed
+// over the items by wave-uniform code on the four quarter values (the frame open at the item start
+// carries its partial XOR C). Units come from the dispenser, so a frame's segments are all
+// processed by one wave, in order.
+// An earlier form advanced each quarter only over the segments of its frame that follow in the
+// item (A_{Ls t}, t <= 3) and the carried register by A_{Ls k}: a second table shift per item,
+// 1.7 % slower at 9000 B.
 // A first version cut frames into 1524-B segments from the frame end (one short front segment,
 // lanes above its first byte zeroed, a partial lane masked per item): the per-item mask code
 // broke the chain block's scheduling and ran 2-12 % slower than the register-load kernel.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kDmaSegJumpHole = kDmaInvHole + 4;   // 4 holes per table: A_{Ls k}, k = 1..4
-static_assert(kDmaSegJumpHole + 16 <= 256, "holes");
+constexpr uint32_t kDmaSegJumpHole = kDmaInvHole + 4;   // 4 holes per table: A_{Ls k}, k = 1 .. m - 1
+static_assert(kDmaSegJumpHole + 4 * (kDmaSegMaxSegs - 1) <= 256, "place tables overrun the table holes");
+static_assert(FCS_DMASEG_MAX_SEGS <= kDmaSegMaxSegs, "segment limit");
 
-// A_{Ls k}(s) for k = 1..4; k = 0 returns s. Nibble table t of A_{Ls k} at hole
+// A_{Ls k}(s) for k = 1 .. m - 1; k = 0 returns s. Nibble table t of A_{Ls k} at hole
 // kDmaSegJumpHole + 4 (k - 1) + t / 2, +64 B for odd t.
 __device__ __forceinline__ uint32_t seg_jump(const uint8_t *lds, uint32_t k, uint32_t s) {
     uint32_t r[8];
@@ -1179,13 +1184,12 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
     const uint32_t Ls = L / m, Lf = L - Ls * (m - 1);                        // segment, front segment
 
     stage_dma_tables(p, lds, tid);
-    for (int i = tid; i < 4 * 128; i += kDmaWgThreads) {   // segment jumps A_{Ls k}, k = 1..4
+    for (int i = tid; i < 4 * 128; i += kDmaWgThreads) {   // place tables A_{Ls k}, k = 1..4, from the blob
         const int k = i >> 7, t = (i >> 4) & 7, e = i & 15;
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaSegJumpHole + 4u * (uint32_t)k + (uint32_t)(t >> 1)) +
                                       64u * (uint32_t)(t & 1) + 4u * (uint32_t)e) =
             p.blob[kBlobSegJump + (Ls - kDmaMinLen) * 512u + (uint32_t)i];
     }
-#ifdef FCS_SEG_ABS
     // A_{Ls k} for k = 5 .. m - 1: composed here as A_{Ls 4} o A_{Ls (k - 4)}, one k at a time
     for (uint32_t k = 5; k < m; k++) {
         __syncthreads();
@@ -1197,7 +1201,6 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
             *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaSegJumpHole + 4u * (k - 1u) + (t >> 1)) + at) = v;
         }
     }
-#endif
     init_bad<kDmaBad>(lds);
     __syncthreads();
 
@@ -1347,15 +1350,11 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
         uint32_t v = lane_shift_dma(lds, mv, lanebase);
         v = act ? v : 0u;
         v = row_xor(v);
-        // advanced over the segments of the same frame that follow in this item
-        const uint32_t tq = s < 3u - q ? s : 3u - q;
-#if defined(FCS_SEG_ABL_NOJUMP)   // measurement-only: no advance over the following segments (wrong FCS)
-        const uint32_t uq = v ^ tq;
-#elif defined(FCS_SEG_ABS)
-        (void)tq;
-        const uint32_t uq = seg_jump(lds, act ? s : 0u, v);   // A_{Ls s}: its place in the frame
+        // placed in its frame: A_{Ls s}, s segments before the frame end
+#ifdef FCS_SEG_ABL_NOJUMP   // measurement-only: no placement shift (wrong FCS)
+        const uint32_t uq = v ^ s;
 #else
-        const uint32_t uq = seg_jump(lds, tq, v);
+        const uint32_t uq = seg_jump(lds, act ? s : 0u, v);
 #endif
 
 #ifdef FCS_SEG_ABL_NOCOMB   // measurement-only: each quarter's value stored as is (wrong FCS)
@@ -1366,15 +1365,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
 #endif
         // ---- per-frame accumulation (wave-uniform) ----
         uint32_t acc = 0;
-#ifdef FCS_SEG_ABS
-        if (cur.r0 != 0) acc = C;
-#else
-        if (cur.r0 != 0) {   // the frame open at the item start: advance its register over its k0 segments here
-            const uint32_t s0 = m - 1u - cur.r0;
-            const uint32_t k0 = s0 + 1u < 4u ? s0 + 1u : 4u;
-            acc = (uint32_t)__builtin_amdgcn_readfirstlane((int)seg_jump(lds, k0, C));
-        }
-#endif
+        if (cur.r0 != 0) acc = C;   // the frame open at the item start: its placed segments so far
         uint32_t rq = cur.r0, fq = cur.fi0;
 #pragma unroll
         for (int qq = 0; qq < 4; qq++) {

@@ -130,14 +130,14 @@ inline bool fixed_dma(const KParams &p) {
 // m = ceil(len / 1524) segments of Ls = floor(len / m) >= kDmaMinLen bytes with the remainder in
 // the front one (<= kDmaCover), packed (gaps of at most 8 bytes) so four consecutive segments fit
 // one slot; the arena holds two slots.
-// Up to 5 segments (7620 B): against the register-load generic kernel (tools/ab.py) 3000 B +10 %,
-// 4500 B +8 %, 6000 B +5 %, 7500 B +1.4 %; 9000 B +0.8 %, 9018 B +-0, 16500 B -4 % (its per-item
-// jumps and carry cost what the DMA gains once the generic kernel runs several segments per frame).
+// Up to 27 segments (41148 B; the place tables fill the table holes). Against the register-load
+// generic kernel (tools/ab.py): 3000 B +10 %, 4500 B +8 %, 6000 B +5 %, 9000 B +4.5 %, 16500 B +1.7 %.
 #ifndef FCS_DMASEG_MAX_GAP   // measurement-only overrides (gap -1: never)
 #define FCS_DMASEG_MAX_GAP 8
 #endif
+constexpr uint32_t kDmaSegMaxSegs = 27;
 #ifndef FCS_DMASEG_MAX_SEGS
-#define FCS_DMASEG_MAX_SEGS 5
+#define FCS_DMASEG_MAX_SEGS 27
 #endif
 inline bool fixed_dmaseg(const KParams &p) {
     if ((int64_t)FCS_DMASEG_MAX_GAP < 0 || p.flen <= kDmaCover || p.stride < p.flen ||

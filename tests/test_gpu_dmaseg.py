@@ -1,13 +1,15 @@
 """GPU parity of the segmented LDS-DMA kernel (fcs_dmaseg_kernel).
 
-Fixed-length frames over 1524 B that split into m = ceil(len / 1524) <= 5 segments of
+Fixed-length frames over 1524 B that split into m = ceil(len / 1524) <= 27 segments of
 Ls = floor(len / m) >= 1496 bytes (front segment Ls + len mod m <= 1524) and are packed
-(stride - len <= 8) take this kernel: four consecutive segments of the stream per wave item, the frame register carried from
-item to item. Every case is checked bit-exact against the oracle (the CPU restatement of
-src/ether_fcs.c:4-19): both ends of every m's band, m = 2..5, all base alignments, strides with
-and without gaps, frame counts that leave partial units and partial items, batches large enough for
-the dynamic schedule, and verify mode. Lengths outside the bands or over 5 segments (1530, 2000,
-9000, 9143, 16000, 65536, ...) take the register-load kernels and are checked the same way.
+(stride - len <= 8) take this kernel: four consecutive segments of the stream per wave item, each
+placed in its frame by A_{Ls s} (place tables for s >= 5 composed at staging), the frame's partial
+XOR carried from item to item. Every case is checked bit-exact against the oracle (the CPU
+restatement of src/ether_fcs.c:4-19): both ends of the bands of m = 2..6, 11, 13 and 27, all base
+alignments, strides with and without gaps, frame counts that leave partial units and partial items,
+batches large enough for the dynamic schedule, and verify mode. Lengths outside the bands or over 27
+segments (1530, 2000, 9143, 10000, 16000, 41149, 65536, ...) take the register-load kernels and are
+checked the same way.
 """
 import struct
 import zlib
@@ -44,9 +46,11 @@ def run(dev, d, lead, stride, L, n):
     return out.cpu().numpy().view(np.uint32)
 
 
-# bands [1496 m, 1524 m]: m = 2, 3, 4, 5 (this kernel), 6 (jumbo), 7, 11, 43; lengths outside every band
+# bands [1496 m, 1524 m]: m = 2 .. 6 (6: jumbo), 7, 11, 13, 27 (this kernel), 43 (over the segment
+# limit); lengths outside every band
 LENS = [2992, 2993, 3000, 3047, 3048, 4488, 4500, 4572, 5984, 6000, 6096, 7480, 7500, 8976, 9000,
-        9018, 9142, 9144, 10472, 16500, 64400, 1530, 2000, 9143, 16000, 65536]
+        9018, 9142, 9144, 10472, 16500, 19448, 19812, 40392, 41148, 64400, 1530, 2000, 9143, 10000,
+        16000, 41149, 65536]
 
 
 @pytest.mark.parametrize("L", LENS)
@@ -62,11 +66,12 @@ def test_dmaseg_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(3000, 3000), (3040, 3048), (4500, 4500), (6000, 6001), (7500, 7500), (9000, 9000)])
+@pytest.mark.parametrize("L,stride", [(3000, 3000), (3040, 3048), (4500, 4500), (6000, 6001), (7500, 7500), (9000, 9000),
+                                      (16500, 16500), (41148, 41150)])
 def test_dmaseg_many_units(dev, oracle, L, stride):
     """More units than the grid's waves (every wave walks several units; the dynamic schedule for
     the larger batches), and a second launch reusing the counter ring."""
-    n = max(40001, (300 << 20) // stride) if L < 60000 else 2100
+    n = max(40001, (300 << 20) // stride) if L < 10000 else 20001
     host = np.random.default_rng(L + stride).integers(0, 256, n * stride + 8, dtype=np.uint8)
     d = torch.from_numpy(host).to(dev)
     exp = oracle_fixed(oracle, host[3:], stride, L, n)
@@ -75,7 +80,7 @@ def test_dmaseg_many_units(dev, oracle, L, stride):
         assert np.array_equal(got, exp), int(np.argmax(got != exp))
 
 
-@pytest.mark.parametrize("L", [3000, 4500, 6000, 7500, 9000, 9022])
+@pytest.mark.parametrize("L", [3000, 4500, 6000, 7500, 9000, 9022, 16500, 41148])
 def test_dmaseg_verify_mode(dev, L):
     """RX residue check through the segmented kernel: frames of L bytes carrying their FCS, a few
     corrupted; ok[] and the bad count against zlib."""
