@@ -352,6 +352,12 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
             const int rc = take_counter(ds, st, p);
             if (rc) return rc;
         }
+    } else if (fcs::fixed_segil(p)) {   // frame-interleaved segments: units of 4 frames
+        const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kSegilWgThreads / 64);
+        if (units >= kFixedDynMinUnitsPerWave * waves) {
+            const int rc = take_counter(ds, st, p);
+            if (rc) return rc;
+        }
     } else if (!fcs::fixed_tiny(p) && fcs::fixed_dmaseg(p)) {   // segmented LDS-DMA kernel: units of F frames
         const uint32_t m = (len + fcs::kDmaCover - 1) / fcs::kDmaCover;
         p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len / m);   // lane 15's mask bytes (the front masks fewer)

@@ -951,21 +951,22 @@ __device__ __forceinline__ void dma_item(const uint8_t *slot, uint64_t src, int 
 
 // Table image of the LDS-DMA kernels: slice tables (16-B stores of one value: 4 replicas), lane
 // tables, merge tables, INV.
+template <int NT = kDmaWgThreads>
 __device__ __forceinline__ void stage_dma_tables(const KParams &p, uint8_t *lds, int tid) {
-    for (int i = tid; i < 2048; i += kDmaWgThreads) {   // row e = i >> 3; store j = i & 7 -> slot j >> 1
+    for (int i = tid; i < 2048; i += NT) {   // row e = i >> 3; store j = i & 7 -> slot j >> 1
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
     }
-    for (int i = tid; i < 4096; i += kDmaWgThreads)   // [t][n][slot]: hole 16 t + n
+    for (int i = tid; i < 4096; i += NT)   // [t][n][slot]: hole 16 t + n
         *reinterpret_cast<uint32_t *>(lds + dma_hole((uint32_t)i >> 5) + (uint32_t)(i & 31) * 4u) = p.blob[kBlobLaneDma + i];
-    for (int i = tid; i < 128 * (kDmaChains - 1); i += kDmaWgThreads) {   // merge table m = A_{4 CL (m + 1)}
+    for (int i = tid; i < 128 * (kDmaChains - 1); i += NT) {   // merge table m = A_{4 CL (m + 1)}
         const int m = i >> 7, t = (i >> 4) & 7, e = i & 15;
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaMergeHole + 4u * (uint32_t)m + (uint32_t)(t >> 1)) +
                                       64u * (uint32_t)(t & 1) + 4u * (uint32_t)e) =
             p.blob[kBlobMerge + ((m + 1) * (kDmaChainWords / 2) - 1) * 128 + (i & 127)];
     }
-    for (int i = tid; i < kChunkBytes; i += kDmaWgThreads)
+    for (int i = tid; i < kChunkBytes; i += NT)
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
             p.blob[kBlobInv + i];
 }
@@ -1129,9 +1130,11 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     flush_bad<kDmaBad>(p, lds);
 }
 
+#ifdef FCS_DMASEG
 // ---------------------------------------------------------------------------------------------
-// Fixed length over 1524 B (jumbo frames, e.g. 9000 B), staged through LDS by DMA
-// (fcs_dmaseg_kernel; host-selected by fixed_dmaseg(): packed frames, stride - len <= 8, and a
+// MEASUREMENT-ONLY (-DFCS_DMASEG -DFCS_NO_SEGIL; superseded by fcs_segil_kernel below, DESIGN.md
+// §3.2c). Fixed length over 1524 B (jumbo frames, e.g. 9000 B), staged through LDS by DMA
+// (fcs_dmaseg_kernel; selected by fixed_dmaseg(): packed frames, stride - len <= 8, and a
 // split into m = ceil(len / 1524) segments of Ls = floor(len / m) >= 1496 bytes, the front one
 // Lf = Ls + len mod m <= 1524 bytes).
 // Every segment is then shaped like a frame of fcs_dma_kernel: its 16 lane windows end e_c bytes
@@ -1382,6 +1385,180 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p)
 
         cur = nxt;
         live = nlive;
+    }
+    flush_bad<kDmaBad>(p, lds);
+}
+#endif  // FCS_DMASEG
+
+// ---------------------------------------------------------------------------------------------
+// Fixed length over 1524 B, any stride: frame-interleaved segments staged through LDS by DMA
+// (fcs_segil_kernel; host-selected by fixed_segil()).
+// A frame of L bytes is cut from its front into m = ceil(L / 1524) segments: a front segment of
+// Lf = L - 1524 (m - 1) bytes, then m - 1 segments of exactly 1524 bytes. A wave's unit is four
+// frames, one per quarter-wave; item r of a unit is segment r of its four frames: four runs of at
+// most 97 16-B pieces (the segment plus the alignment of its ends), each DMAed into its own 2 KiB
+// part of the wave's 8 KiB slot (two rows: 64 + 33 lanes). A 1524-B segment is exactly the cover
+// of fcs_dma_kernel's 16 lane windows, so it needs no mask beyond the short lanes' overlap word,
+// and the frame's CRC state after the previous segment enters through lane 15's chain start (a CRC
+// state is the same as XORing it into the next four data bytes). No shift is needed between
+// segments: the quarter's row XOR after segment r is its frame's CRC state after that segment,
+// and stays in a register until the next item. The front item (1 in m) masks each lane's bytes
+// before the frame start (loop-invariant per lane: Lf is fixed), drops lanes wholly before it and
+// injects INV at the frame's first byte.
+// LDS: the 64 KiB table image of fcs_dma_kernel, then 12 slots of 8 KiB (160 KiB).
+// ---------------------------------------------------------------------------------------------
+constexpr int kSegilWaves = 12;
+constexpr int kSegilThreads = kSegilWgThreads;
+static_assert(kSegilThreads == 64 * kSegilWaves, "12 waves");
+constexpr uint32_t kSegilRunBytes = 2048;                      // one run's part of a slot
+constexpr uint32_t kSegilSlotBytes = 4 * kSegilRunBytes;
+constexpr uint32_t kSegilLdsBytes = kDmaRing + (uint32_t)kSegilWaves * kSegilSlotBytes;
+static_assert(kSegilLdsBytes <= 163840, "LDS per CU");
+static_assert(kSegilWaves <= 16, "verify counters: 16 waves");
+#ifndef FCS_SEGIL_TAIL_AUX   // cache policy of a run's second row (it holds the line the next segment shares)
+#define FCS_SEGIL_TAIL_AUX 0
+#endif
+#ifndef FCS_SEGIL_SKEW   // bytes added to odd runs' LDS base (bank phase of their windows)
+#define FCS_SEGIL_SKEW 16
+#endif
+
+// One run's DMA: pieces 0..63 in row 0 (non-temporal), 64..need-1 in row 1.
+__device__ __forceinline__ void segil_run(const uint8_t *dst, uint64_t src, int lane, uint32_t pieces) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    const uint64_t a = src + 16 * (uint64_t)lane;
+    lds_void *l = (lds_void *)dst;
+    if ((uint32_t)lane < pieces) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), l, 16, 0, FCS_DMA_AUX);
+    if ((uint32_t)lane + 64u < pieces)
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), l, 16, 1024, FCS_SEGIL_TAIL_AUX);
+}
+
+__global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kSegilLdsBytes];
+    const int tid = threadIdx.x;
+    stage_dma_tables<kSegilThreads>(p, lds, tid);
+    init_bad<kDmaBad>(lds);
+    __syncthreads();
+
+    // ---- frame geometry (wave-uniform) ----
+    const uint32_t L = p.flen;
+    const uint32_t m = (L + kDmaCover - 1) / kDmaCover;   // segments, >= 2
+    const uint32_t Lf = L - kDmaCover * (m - 1);          // front segment, 1 .. 1524
+
+    const int lane = tid & 63;
+    const int c = lane & (kGroup - 1);        // window index back from the segment end
+    const uint32_t q = (uint32_t)lane >> 4;   // quarter: frame 4 u + q of unit u
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kSegilSlotBytes;
+    const uint8_t *run = slot + q * kSegilRunBytes + (q & 1u) * FCS_SEGIL_SKEW;
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
+    const uint32_t ec = dma_end_off(c);
+
+    // loop invariants. Other segments: the short lanes' overlap word. Front segment: zr bytes of
+    // the lane's window lie before the frame start (>= 96: the whole window, the lane is dropped);
+    // the lane holding the first byte in its unmasked part starts its chain from INV there.
+    const uint32_t mn0 = dma_short_lane(c) ? 0u : 0xFFFFFFFFu;
+    const int zr = (int)(kDmaCover - Lf) - (int)(kDmaCover - ec - kChunkBytes);
+    const bool fdead = zr >= kChunkBytes;
+    int zf = zr < 0 ? 0 : (zr > kChunkBytes ? kChunkBytes : zr);
+    if (dma_short_lane(c) && zf < 4) zf = 4;
+    const uint32_t x0f = (!fdead && zr >= 0 && zf == zr)
+                             ? lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zr / 32u) + (uint32_t)(zr % 32) * 4u)
+                             : 0u;
+    const int zb = fdead ? 0 : zf;   // the wave masks word groups up to its largest live claim
+
+    const uint64_t n = p.n, units = (n + 3) >> 2;
+    const uint32_t cmax = m >= 64 ? 1u : 64u / m;
+    Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kSegilWaves, (uint64_t)blockIdx.x * kSegilWaves + (uint64_t)wave,
+                lane, 100, 1, cmax);
+    constexpr uint64_t kEnd = Dispenser::kEnd;
+    // segment r of frame f: [start, start + len); the run starts at the 16-B boundary below it
+    auto seg_start = [&](uint64_t f, uint32_t r) {
+        return p.base + f * p.stride + (r ? (uint64_t)Lf + (uint64_t)kDmaCover * (r - 1) : 0ull);
+    };
+    auto issue = [&](uint64_t u, uint32_t r) {   // the item's four runs (wave-uniform control)
+        const uint32_t len = r ? kDmaCover : Lf;
+#pragma unroll
+        for (uint32_t qq = 0; qq < 4; qq++) {
+            const uint64_t f = 4 * u + qq;
+            if (f < n) {
+                const uint64_t s0 = seg_start(f, r), a = s0 & ~15ull;
+                const uint32_t pieces = (uint32_t)((((s0 + len) + 15) & ~15ull) - a) >> 4;
+                segil_run(slot + qq * kSegilRunBytes + (qq & 1u) * FCS_SEGIL_SKEW, a, lane, pieces);
+            }
+        }
+    };
+
+    uint64_t u = D.first();
+    uint32_t r = 0;
+    if (u != kEnd) issue(u, 0);
+    uint32_t acc = 0;   // this quarter's frame: CRC state after its segments so far
+    while (u != kEnd) {   // wave-uniform
+        const uint64_t f = 4 * u + q;
+        const bool act = f < n;
+        const uint64_t s0 = act ? seg_start(f, r) : 0ull;
+        const uint32_t len = r ? kDmaCover : Lf;
+        const int64_t x = (int64_t)(s0 & 15ull) + (int64_t)len - (int64_t)ec - kChunkBytes;   // window start in the run
+        const uint32_t ra = (uint32_t)x & 3u;
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's runs have landed
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(run + (x & ~3ll));
+        uint32_t d[kChunkWords + 1];
+#pragma unroll
+        for (int i = 0; i <= kChunkWords; i++) d[i] = wp[i];
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+
+        // ---- the next item: the next segment of the unit, or the dispenser's next unit ----
+        uint64_t un = u;
+        uint32_t rn = r + 1;
+        if (rn == m) {
+            un = D.next(u);
+            rn = 0;
+        }
+        if (un != kEnd) issue(un, rn);
+
+        // ---- this item ----
+        uint32_t w[kChunkWords];
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ra);
+        uint32_t x0;
+        if (r == 0) {
+            const int zf8 = 8 * zf;
+#pragma unroll
+            for (int g = 0; g < kChunkWords / 4; g++) {
+                if (!__any(zb > 16 * g)) break;
+#pragma unroll
+                for (int i = 4 * g; i < 4 * g + 4; i++) {
+                    int t = zf8 - 32 * i;
+                    t = t < 0 ? 0 : (t > 32 ? 32 : t);
+                    w[i] &= (uint32_t)(0xFFFFFFFFull << t);
+                }
+            }
+            x0 = x0f;
+        } else {
+            w[0] &= mn0;
+            x0 = c == kGroup - 1 ? acc : 0u;
+        }
+        constexpr int CL = kDmaChainWords;
+        uint32_t xs[kDmaChains];
+#pragma unroll
+        for (int hh = 0; hh < kDmaChains; hh++) xs[hh] = w[hh * CL] ^ (hh == 0 ? x0 : 0u);
+#pragma unroll
+        for (int i = 0; i < CL; i++)
+#pragma unroll
+            for (int hh = 0; hh < kDmaChains; hh++)
+                xs[hh] = step4_l8(lds, xs[hh], i < CL - 1 ? w[hh * CL + i + 1] : 0u, B, SEL);
+        uint32_t mv = xs[kDmaChains - 1];
+#pragma unroll
+        for (int hh = 0; hh < kDmaChains - 1; hh++) mv = merge_shift_dma(lds, kDmaChains - 2 - hh, xs[hh], mv);
+        uint32_t v = lane_shift_dma(lds, mv, lanebase);
+        if (r == 0 && fdead) v = 0u;
+        acc = row_xor(v);
+        if (r == m - 1) emit<kDmaBad>(p, lds, c == kGroup - 1 && act, f, ~acc);
+        u = un;
+        r = rn;
     }
     flush_bad<kDmaBad>(p, lds);
 }
@@ -2412,9 +2589,13 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
 #endif
         }
+    } else if (fixed_segil(p)) {
+        hipLaunchKernelGGL(fcs_segil_kernel, dim3(grid), dim3(kSegilThreads), 0, st, p);
+#ifdef FCS_DMASEG
     } else if (!tiny && fixed_dmaseg(p)) {
         if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dmaseg_kernel<2>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
         else hipLaunchKernelGGL((fcs_dmaseg_kernel<kSingleMaskWords>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+#endif
     } else if (!tiny && fixed_dma(p)) {
         if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dma_kernel<2, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
         else hipLaunchKernelGGL((fcs_dma_kernel<kSingleMaskWords, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);

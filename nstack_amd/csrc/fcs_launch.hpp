@@ -126,12 +126,27 @@ inline bool fixed_dma(const KParams &p) {
            3 * p.stride + p.flen <= kDmaItemBytes - 18 && p.hi4 - p.lo4 >= 2 * kDmaItemBytes;
 #endif
 }
-// Segmented LDS-DMA kernel (fcs_dmaseg_kernel): frames over kDmaCover bytes that split into
-// m = ceil(len / 1524) segments of Ls = floor(len / m) >= kDmaMinLen bytes with the remainder in
-// the front one (<= kDmaCover), packed (gaps of at most 8 bytes) so four consecutive segments fit
-// one slot; the arena holds two slots.
-// Up to 27 segments (41148 B; the place tables fill the table holes). Against the register-load
-// generic kernel (tools/ab.py): 3000 B +10 %, 4500 B +8 %, 6000 B +5 %, 9000 B +4.5 %, 16500 B +1.7 %.
+// Frame-interleaved segment kernel (fcs_segil_kernel): fixed lengths over kDmaCover bytes, any
+// stride; units of 4 frames, 12 waves per workgroup (8 KiB LDS slots). A frame costs
+// m = ceil(len / 1524) items whatever its front segment holds, so it is selected when
+// len >= 0.75 * 1524 m (tools/ab.py against the register-load generic kernel: 2500 B +4.8 %,
+// 4573 B +0.6 %, 6100 B +3.6 %, 9000 B +8.5 %, 10000 B +10 %, 65536 B +16 %; below the bound 1530 B
+// -30 %, 1600 B -5 %, 2000 B -1.3 %, 3049 B -9 %, which keep the generic kernel).
+constexpr int kSegilWgThreads = 768;
+inline bool fixed_segil(const KParams &p) {
+#ifdef FCS_NO_SEGIL   // measurement-only build
+    (void)p;
+    return false;
+#else
+    const uint64_t m = (p.flen + kDmaCover - 1) / kDmaCover;
+    return p.flen > kDmaCover && !fixed_tiny(p) && 4ull * p.flen >= 3ull * kDmaCover * m;
+#endif
+}
+// Segmented LDS-DMA kernel (fcs_dmaseg_kernel, MEASUREMENT-ONLY: -DFCS_DMASEG with -DFCS_NO_SEGIL;
+// superseded by fcs_segil_kernel, which matches it in its bands and has none): frames over
+// kDmaCover bytes that split into m = ceil(len / 1524) <= 27 segments of Ls = floor(len / m) >=
+// kDmaMinLen bytes with the remainder in the front one (<= kDmaCover), packed (gaps of at most 8
+// bytes) so four consecutive segments fit one slot; the arena holds two slots.
 #ifndef FCS_DMASEG_MAX_GAP   // measurement-only overrides (gap -1: never)
 #define FCS_DMASEG_MAX_GAP 8
 #endif
@@ -140,13 +155,19 @@ constexpr uint32_t kDmaSegMaxSegs = 27;
 #define FCS_DMASEG_MAX_SEGS 27
 #endif
 inline bool fixed_dmaseg(const KParams &p) {
+#ifndef FCS_DMASEG
+    (void)p;
+    return false;
+#else
     if ((int64_t)FCS_DMASEG_MAX_GAP < 0 || p.flen <= kDmaCover || p.stride < p.flen ||
         p.stride - p.flen > (uint64_t)FCS_DMASEG_MAX_GAP || p.hi4 - p.lo4 < 2 * kDmaItemBytes)
         return false;
     const uint32_t m = (p.flen + kDmaCover - 1) / kDmaCover, ls = p.flen / m;
     return m <= FCS_DMASEG_MAX_SEGS && ls >= kDmaMinLen && p.flen - ls * (m - 1) <= kDmaCover;
+#endif
 }
 inline int fixed_threads(const KParams &p) {
+    if (fixed_segil(p)) return kSegilWgThreads;
     if (!fixed_tiny(p) && (fixed_dma(p) || fixed_dmaseg(p))) return kDmaWgThreads;
     return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;
 }

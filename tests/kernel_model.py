@@ -359,3 +359,60 @@ def model_dmaseg_frame_abs(lds, blob, frame: bytes, garbage: bytes):
         s_ = m - 1 - r
         acc ^= apply_nibbles(tabs[s_], v) if s_ else v
     return ~acc & 0xFFFFFFFF
+
+
+def model_segil_window_value(lds, win: bytes, lane: int, z: int, x0: int, chains=DMA_CHAINS):
+    """One lane window of fcs_segil_kernel (as fcs_dma_kernel's): 96 bytes, the first z masked,
+    x0 XORed into chain 0's start; two chains merged, shifted by the lane table A_{e_c}."""
+    cl = 24 // chains
+    w = [int.from_bytes(win[4 * i:4 * i + 4], "little") for i in range(24)]
+    for i in range(24):
+        t = max(0, min(4, z - 4 * i))
+        w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
+    xs = [w[h * cl] ^ (x0 if h == 0 else 0) for h in range(chains)]
+    for i in range(cl):
+        for h in range(chains):
+            xs[h] = step4_l8(lds, xs[h], lane) ^ (w[h * cl + i + 1] if i < cl - 1 else 0)
+    m = xs[chains - 1]
+    for h in range(chains - 1):
+        m = merge_shift(lds, chains - 2 - h, xs[h]) ^ m
+    lanebase = 128 + (lane & 31) * 4
+    s = 0
+    for t in range(8):
+        sh = (m >> (4 * t - 8)) if 4 * t >= 8 else ((m << (8 - 4 * t)) & 0xFFFFFFFF)
+        s ^= int(lds[(((sh & 0xF00) | lanebase) + t * 4096) // 4])
+    return s
+
+
+def model_segil_frame(lds, frame: bytes, garbage: bytes):
+    """FCS of one frame by fcs_segil_kernel's decomposition: a front segment of Lf = L - 1524 (m - 1)
+    bytes, then 1524-B segments. Each segment is a 1524-B cover of 16 lane windows ending at the
+    segment end. Front: lane c masks the zr = (1524 - Lf) - ws_c bytes of its window before the frame
+    start (whole window: dropped), short lanes at least their 4-byte overlap, and the lane holding
+    the first byte unmasked starts from INV[zr]. Other segments: only the short lanes' overlap word;
+    lane 15 starts from the frame's CRC state after the previous segment (the row XOR)."""
+    L = len(frame)
+    m = -(-L // DMA_COVER)
+    lf = L - DMA_COVER * (m - 1)
+    padded = bytes(garbage[:DMA_COVER]) + frame
+    acc = 0
+    for r in range(m):
+        end = DMA_COVER + lf + DMA_COVER * r
+        cover = padded[end - DMA_COVER:end]
+        v = 0
+        for c in range(16):
+            ws = DMA_COVER - dma_end_off(c) - CHUNK
+            win = cover[ws:ws + CHUNK]
+            short = 4 if dma_short_lane(c) else 0
+            if r == 0:
+                zr = (DMA_COVER - lf) - ws
+                if zr >= CHUNK:
+                    continue
+                z = max(max(zr, 0), short)
+                x0 = int(lds[(hole(INV_HOLE + zr // 32) + (zr % 32) * 4) // 4]) if (zr >= 0 and z == zr) else 0
+            else:
+                z = short
+                x0 = acc if c == 15 else 0
+            v ^= model_segil_window_value(lds, win, c, z, x0)
+        acc = v
+    return ~acc & 0xFFFFFFFF

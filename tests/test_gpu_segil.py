@@ -1,15 +1,14 @@
-"""GPU parity of the segmented LDS-DMA kernel (fcs_dmaseg_kernel).
+"""GPU parity of the frame-interleaved segment kernel (fcs_segil_kernel).
 
-Fixed-length frames over 1524 B that split into m = ceil(len / 1524) <= 27 segments of
-Ls = floor(len / m) >= 1496 bytes (front segment Ls + len mod m <= 1524) and are packed
-(stride - len <= 8) take this kernel: four consecutive segments of the stream per wave item, each
-placed in its frame by A_{Ls s} (place tables for s >= 5 composed at staging), the frame's partial
-XOR carried from item to item. Every case is checked bit-exact against the oracle (the CPU
-restatement of src/ether_fcs.c:4-19): both ends of the bands of m = 2..6, 11, 13 and 27, all base
-alignments, strides with and without gaps, frame counts that leave partial units and partial items,
-batches large enough for the dynamic schedule, and verify mode. Lengths outside the bands or over 27
-segments (1530, 2000, 9143, 10000, 16000, 41149, 65536, ...) take the register-load kernels and are
-checked the same way.
+Fixed-length frames over 1524 B with len >= 0.75 * 1524 m (m = ceil(len / 1524)) take this kernel,
+at any stride: a front segment of len - 1524 (m - 1) bytes, then 1524-B segments; item r of a
+wave's unit is segment r of its four frames (one per quarter-wave, four DMA runs), and a frame's
+CRC state goes from item to item through lane 15's chain start. Every case is checked bit-exact
+against the oracle (the CPU restatement of src/ether_fcs.c:4-19): front segments of 1 to 1524
+bytes, both sides of the selection bound (2285 / 2286, 3428 / 3429 B: the shorter ones keep the
+register-load generic kernel), up to 688 segments (1 MiB), all base alignments, strides with no
+gap, odd gaps and large gaps, frame counts that leave partial units, batches large enough for the
+dynamic schedule, and verify mode.
 """
 import struct
 import zlib
@@ -46,18 +45,18 @@ def run(dev, d, lead, stride, L, n):
     return out.cpu().numpy().view(np.uint32)
 
 
-# bands [1496 m, 1524 m]: m = 2 .. 6 (6: jumbo), 7, 11, 13, 27 (this kernel), 43 (over the segment
-# limit); lengths outside every band
-LENS = [2992, 2993, 3000, 3047, 3048, 4488, 4500, 4572, 5984, 6000, 6096, 7480, 7500, 8976, 9000,
-        9018, 9142, 9144, 10472, 16500, 19448, 19812, 40392, 41148, 64400, 1530, 2000, 9143, 10000,
-        16000, 41149, 65536]
+# front segments of 1 .. 1524 B; the selection bound (2286 = 0.75 * 3048, 3429 = 0.75 * 4572) and one
+# byte below it; the old segmented kernel's bands (2992-3048, 8976-9144, 40392-41148)
+LENS = [1525, 1530, 1536, 1537, 2000, 2285, 2286, 2500, 2992, 3000, 3048, 3049, 3428, 3429, 4572, 4573,
+        6000, 6096, 7500, 8976, 9000, 9018, 9143, 9144, 10000, 10472, 16000, 16500, 40392, 41148, 41149,
+        64400, 65536, 100000]
 
 
 @pytest.mark.parametrize("L", LENS)
-def test_dmaseg_lengths(dev, oracle, L):
-    for gap in (0, 1, 8):
+def test_segil_lengths(dev, oracle, L):
+    for gap in (0, 1, 8, 1001):
         stride = L + gap
-        for n in (1, 3, 6, 13, 257):
+        for n in ((1, 3, 6, 13, 257) if L < 20000 else (1, 5, 33)):
             host = np.random.default_rng(L * 7 + gap * 3 + n).integers(0, 256, n * stride + 16, dtype=np.uint8)
             d = torch.from_numpy(host).to(dev)
             for lead in (0, 1, 2, 3):
@@ -66,9 +65,10 @@ def test_dmaseg_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(3000, 3000), (3040, 3048), (4500, 4500), (6000, 6001), (7500, 7500), (9000, 9000),
-                                      (16500, 16500), (41148, 41150)])
-def test_dmaseg_many_units(dev, oracle, L, stride):
+@pytest.mark.parametrize("L,stride", [(2500, 2500), (3000, 3000), (3040, 3048), (4500, 4500), (6000, 6001), (7500, 7500),
+                                      (9000, 9000), (9000, 9216), (10000, 10003), (16500, 16500), (41148, 41150),
+                                      (65536, 65536)])
+def test_segil_many_units(dev, oracle, L, stride):
     """More units than the grid's waves (every wave walks several units; the dynamic schedule for
     the larger batches), and a second launch reusing the counter ring."""
     n = max(40001, (300 << 20) // stride) if L < 10000 else 20001
@@ -80,9 +80,9 @@ def test_dmaseg_many_units(dev, oracle, L, stride):
         assert np.array_equal(got, exp), int(np.argmax(got != exp))
 
 
-@pytest.mark.parametrize("L", [3000, 4500, 6000, 7500, 9000, 9022, 16500, 41148])
-def test_dmaseg_verify_mode(dev, L):
-    """RX residue check through the segmented kernel: frames of L bytes carrying their FCS, a few
+@pytest.mark.parametrize("L", [2500, 3000, 4500, 6000, 7500, 9000, 9022, 10000, 16500, 41148, 65536])
+def test_segil_verify_mode(dev, L):
+    """RX residue check through the interleaved segment kernel: frames of L bytes carrying their FCS, a few
     corrupted; ok[] and the bad count against zlib."""
     n = 4099
     rng = np.random.default_rng(L)

@@ -196,3 +196,15 @@ def test_dmaseg_place_model(lds_dma, L):
     frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
     garbage = rng.integers(0, 256, 1524, dtype=np.uint8).tobytes()
     assert km.model_dmaseg_frame_abs(lds_dma[2], blob, frame, garbage) == zlib.crc32(frame)
+
+
+@pytest.mark.parametrize("L", [1525, 1530, 2000, 3048, 3049, 4573, 9000, 10000])
+def test_segil_decomposition_model(lds_dma, L):
+    """fcs_segil_kernel's decomposition: a front segment of L - 1524 (m - 1) bytes with per-lane
+    front masks and INV at the frame's first byte, then 1524-B segments whose lane 15 starts from
+    the frame's CRC state after the previous segment (no shift tables between segments), reproduces
+    the CRC (zlib = src/ether_fcs.c:4-19); the cover bytes before the frame are random garbage."""
+    rng = np.random.default_rng(L + 2)
+    frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+    garbage = rng.integers(0, 256, 1524, dtype=np.uint8).tobytes()
+    assert km.model_segil_frame(lds_dma[2], frame, garbage) == zlib.crc32(frame)
