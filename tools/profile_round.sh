@@ -2,8 +2,8 @@
 # Round profile bundle (GPU box): rocprofv3 kernel-trace stats of the default bench command (its
 # JSON line and the kernel statistics come from the same process), then separate PMC passes
 # (FETCH_SIZE, WRITE_SIZE; one counter group per run) for the HBM traffic of the headline kernel
-# (64 M x 1518 B), of the IMIX flat kernel (BASELINE configs[2]) and of the 9000-B jumbo frames
-# generic kernel (configs[3]). Outputs under $1.
+# (64 M x 1518 B), of the IMIX flat kernel (BASELINE configs[2]) and of the 9000-B jumbo frames'
+# interleaved segment kernel (configs[3]). Outputs under $1.
 set -u
 OUT=${1:-gpurun_out/prof}; mkdir -p "$OUT"; export TMPDIR=/tmp
 step() {   # tag, timeout, command...
