@@ -258,7 +258,7 @@ def model_dma_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f
     return out
 
 
-# ---- fcs_dmaseg_kernel: equal segments shaped like 1518-B frames ----
+# ---- fcs_dmaseg_kernel (measurement build): equal segments shaped like 1518-B frames ----
 BLOB_SEG_JUMP = BLOB_MERGE + 11 * 8 * 16     # fcs_tables.hpp kBlobSegJump: [Ls - 1496][k - 1][t][e]
 SEG_MIN = 1496
 

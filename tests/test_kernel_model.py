@@ -163,7 +163,8 @@ def test_dma_table_lookups_bank_distinct():
 
 @pytest.mark.parametrize("L", [2992, 3000, 3048, 4488, 4500, 4572, 6000, 7500, 7620])
 def test_dmaseg_decomposition_model(lds_dma, L):
-    """fcs_dmaseg_kernel's split into equal segments shaped like 1518-B frames, with the blob's
+    """fcs_dmaseg_kernel's (measurement build, superseded by fcs_segil_kernel) split into equal
+    segments shaped like 1518-B frames, with the blob's
     segment-jump tables A_{Ls k}, reproduces the CRC (zlib = src/ether_fcs.c:4-19); the cover
     bytes before each segment are random garbage that the masks must remove."""
     blob = na.tables_blob()
@@ -188,7 +189,7 @@ def test_dmaseg_jump_tables_compose():
 
 @pytest.mark.parametrize("L", [3000, 9000, 16500, 41148])
 def test_dmaseg_place_model(lds_dma, L):
-    """The segmented kernel's placement form: each segment shifted by A_{Ls s} for its place s from
+    """The segmented kernel's (measurement build) placement form: each segment shifted by A_{Ls s} for its place s from
     the frame end (tables for s >= 5 composed from the blob's A_{Ls 4}), the frame the XOR of its
     placed segments, reproduces the CRC (zlib = src/ether_fcs.c:4-19) up to 27 segments."""
     blob = na.tables_blob()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Parity spot check of a library variant against zlib (measurement tool): fixed short frames and an
 IMIX batch through the flat (windowed) paths, every frame compared; with --lens L1,L2,... fixed-length
-batches of those lengths instead (gaps 0 and 8, odd base), e.g. jumbo frames for the segmented kernel.
+batches of those lengths instead (gaps 0 and 8, odd base), e.g. jumbo frames for the segment kernels.
 usage: NSTACK_FCS_LIB=... check_flat.py [--lens 9000,16500]"""
 import numpy as np
 import torch
