@@ -22,8 +22,9 @@ Printed (rank 0, one JSON line): the contract fields plus
   configs      — (N = 1) the other single-GPU BASELINE configs, each timed in this process after the
                  headline and freed before the next: imix_128M (configs[2]), jumbo_16M_x_9000
                  (configs[3]) and host_inclusive_1518 (frames in pinned host memory -> H2D -> kernel
-                 -> D2H, PCIe-bound; never `value`), each with ms, GB/s, roofline frac and a zlib
-                 spot check of sampled frames.
+                 -> D2H, PCIe-bound; never `value`; its ceiling h2d_copy_gbs = plain async copies of
+                 the same pinned arena), each with ms, GB/s, roofline frac and a zlib spot check of
+                 sampled frames.
 For N > 1 the timing barrier and the max-over-ranks use gloo on the host: no RCCL collective
 anywhere (BASELINE north_star), and nothing but 8 bytes of timing crosses ranks.
 """
@@ -186,13 +187,29 @@ def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
         secs = time.perf_counter() - t0
         idx = rng.integers(0, n, 128)
         bad = _spot(hout, lambda i: pinned[i * L:(i + 1) * L].tobytes(), idx)
+        # the measured ceiling: plain async H2D copies of the same pinned arena, 1 GiB at a time
+        src = torch.from_numpy(pinned)
+        chunk = min(nbytes, int(GIB))
+        dbuf = torch.empty(chunk, dtype=torch.uint8, device=dev)
+        dbuf.copy_(src[:chunk], non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for o in range(0, nbytes, chunk):
+            m = min(chunk, nbytes - o)
+            dbuf[:m].copy_(src[o:o + m], non_blocking=True)
+        torch.cuda.synchronize()
+        h2d = nbytes / (time.perf_counter() - t0) / 1e9
+        del dbuf, src
+        torch.cuda.empty_cache()
         res["host_inclusive_1518"] = {"what": "pinned host frames -> chunked H2D -> kernel -> D2H of CRCs "
                                               "(ether_fcs_fixed_host); PCIe Gen5 x16 bound, never `value`",
                                       "frames": n, "bytes": nbytes, "ms": round(secs * 1e3, 3),
                                       "GB_s": round(nbytes / secs / 1e9, 2), "GiB_s": round(nbytes / secs / GIB, 2),
                                       "roofline": {"bound": "pcie", "achieved": round(nbytes / secs / 1e9, 2),
                                                    "peak": 63.0, "unit": "GB/s",
-                                                   "frac": round(nbytes / secs / 1e9 / 63.0, 4)},
+                                                   "frac": round(nbytes / secs / 1e9 / 63.0, 4),
+                                                   "h2d_copy_gbs": round(h2d, 2),
+                                                   "frac_of_h2d_copy": round(nbytes / secs / 1e9 / h2d, 4)},
                                       "spot_checked": len(idx), "spot_bad": bad}
         del pinned, hout
         lib.fcs_host_free(p)

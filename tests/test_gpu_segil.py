@@ -102,3 +102,20 @@ def test_segil_verify_mode(dev, L):
     exp[bad_idx] = 0
     assert np.array_equal(ok.cpu().numpy(), exp)
     assert int(bad.item()) == len(bad_idx)
+
+
+hyp = pytest.importorskip("hypothesis")
+from hypothesis import given, settings, strategies as hst  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, derandomize=True)
+@given(hst.integers(1525, 70000), hst.integers(0, 3000), hst.integers(1, 600), hst.integers(0, 15))
+def test_segil_fuzz(dev, oracle, L, gap, n, lead):
+    """Random fixed lengths over 1524 B (either kernel, by the selection bound), gaps, frame counts
+    and base alignments against the oracle."""
+    stride = L + gap
+    host = np.random.default_rng(L ^ (gap << 17) ^ (n << 33) ^ lead).integers(0, 256, n * stride + 32, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    got = run(dev, d, lead, stride, L, n)
+    exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+    assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
