@@ -23,7 +23,8 @@ Printed (rank 0, one JSON line): the contract fields plus
                  headline and freed before the next: imix_128M (configs[2]), jumbo_16M_x_9000
                  (configs[3]) and host_inclusive_1518 (frames in pinned host memory -> H2D -> kernel
                  -> D2H, PCIe-bound; never `value`; its ceiling h2d_copy_gbs = plain async copies of
-                 the same pinned arena), each with ms, GB/s, roofline frac and a zlib spot check of
+                 the same pinned arena), each with ms, GB/s, roofline frac (the HBM-bound ones also
+                 against the headline run's two measured read ceilings) and a zlib spot check of
                  sampled frames.
 For N > 1 the timing barrier and the max-over-ranks use gloo on the host: no RCCL collective
 anywhere (BASELINE north_star), and nothing but 8 bytes of timing crosses ranks.
@@ -428,6 +429,11 @@ def main():
         del arena, out
         torch.cuda.empty_cache()
         configs = extra_configs(torch, na, dev, stream)
+        for c in configs.values():   # the headline run's measured read ceilings, for comparison
+            rf = c.get("roofline", {})
+            if rf.get("bound") == "hbm":
+                rf["frac_of_read_stream"] = round(rf["achieved"] / read_gbs, 4)
+                rf["frac_of_dma_stream"] = round(rf["achieved"] / dma_gbs, 4)
 
     if dist:
         dist.barrier()
