@@ -116,6 +116,11 @@ def test_dropin_every_length(dev, golden):
     for L in (60, 1514, 1532):
         f = buf[:L]
         assert na.ether_fcs(f + struct.pack("<I", zlib.crc32(f))) == 0x2144DF1C
+    # longer buffers: both sides of the interleaved segment kernel's bound, jumbo, 64 KiB, odd sizes
+    big = rng.integers(0, 256, 100020, dtype=np.uint8).tobytes()
+    for L in (2285, 2286, 3000, 3049, 9000, 9001, 65536, 100003):
+        a = L % 7
+        assert na.ether_fcs(big[a:a + L]) == zlib.crc32(big[a:a + L]), L
 
 
 # ---------------------------------------------------------------- edge lengths / alignment
