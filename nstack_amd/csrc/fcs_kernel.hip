@@ -1978,23 +1978,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     flush_bad(p, lds);
 }
 
-#ifdef FCS_FLATDMA
 // ---------------------------------------------------------------------------------------------
-// MEASUREMENT-ONLY (-DFCS_FLATDMA; rejected: IMIX 4629 vs 5200 GB/s, DESIGN.md §3.3).
-// Variable-length frames, flat chunk stream, chunk windows staged through LDS by DMA
-// (fcs_flatdma_kernel; replaces fcs_flat_kernel<false> in -DFCS_FLATDMA builds).
-// The dealing of fcs_flat_kernel (64-frame windows, 64 chunks per item, frame-start marks), but
-// each lane copies its own 96-byte window into the wave's LDS slot with six
-// global_load_lds_dwordx4 at the window's exact byte address: gfx950's LDS-DMA honours any byte
-// alignment (tools/microbench/glds_align.hip), so no realignment is needed and no VGPR holds the
-// bytes in flight. Lane l's 16-byte piece i lands at slot + 1024 i + 16 l and comes back with one
-// ds_read_b128 per piece (16 lanes per 256-B bank row: 4 cycles, the minimum; random 16-B pieces
-// would cost 12, tools/microbench/lds_pat.hip). A wave deals its next item and issues that item's
-// DMA as soon as the current item's words are in registers, so the next item's bytes land while
-// the current item's CRC work runs (fcs_flat_kernel waits for each item's loads with nothing else
-// to do). An item whose windows reach before the arena start (the frames at the arena's first 96
-// bytes) is loaded into registers instead, with the arena-edge shift of the other kernels.
-// Tables: the 32 KiB slice tables of fcs_dma_kernel (step4_l8) and, in the row holes, the
+// Shared by the LDS-DMA variable-length kernels (fcs_span_kernel, and the measurement-only
+// fcs_flatdma_kernel): the 32 KiB slice tables of fcs_dma_kernel and, in the row holes, the
 // c-indexed shift tables A_{96c} (nibble t of table c at hole 4c + t/2, +64 B for odd t), the A_48
 // merge table and INV of fcs_dma_kernel, A_1536 for frames over 1536 B, and each wave's window
 // scratch (accumulators, marks, frame lists).
@@ -2002,8 +1988,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 constexpr uint32_t kFdJumpHole = 152;                  // A_1536: 4 holes
 constexpr uint32_t kFdWaveHole = 160;                  // 4 holes per wave: acc[0..31], acc[32..63], marks | list, multi list
 static_assert(kDmaInvHole + 4 <= kFdJumpHole && kFdWaveHole + 4 * 16 <= 256, "holes");
-constexpr uint32_t kFdSlotBytes = 6144;                // 64 lanes x 96 B, piece i of lane l at 1024 i + 16 l
-constexpr uint32_t kFlatDmaMinArena = 2 * kFdSlotBytes;
 
 __device__ __forceinline__ uint32_t fd_acc_addr(uint32_t wave, uint32_t i) {
     return dma_hole(kFdWaveHole + 4u * wave + (i >> 5)) + (i & 31u) * 4u;
@@ -2079,15 +2063,8 @@ __device__ __forceinline__ uint32_t fd_value(const uint8_t *lds, uint32_t (&w)[k
     return merge_shift_dma(lds, 0, xa, xb);
 }
 
-#ifndef FCS_FD_AUX   // cache policy of the window DMA (measurement-only override)
-#define FCS_FD_AUX 0
-#endif
-
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing + 16 * kFdSlotBytes];
-    static_assert(kWgThreads / 64 <= 16, "slots");
-    const int tid = threadIdx.x;
-    // ---- tables ----
+// Table image of the variable-length LDS-DMA kernels (layout above); zeroes every wave's scratch.
+__device__ __forceinline__ void stage_fd_tables(const KParams &p, uint8_t *lds, int tid) {
     for (int i = tid; i < 2048; i += kWgThreads) {   // slice tables as fcs_dma_kernel
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
@@ -2110,6 +2087,39 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
             p.blob[kBlobInv + i];
     for (int i = tid; i < 16 * 4 * 32; i += kWgThreads)   // window scratch of every wave: zero
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdWaveHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) = 0u;
+}
+
+#ifdef FCS_FLATDMA
+constexpr uint32_t kFdSlotBytes = 6144;                // 64 lanes x 96 B, piece i of lane l at 1024 i + 16 l
+// ---------------------------------------------------------------------------------------------
+// MEASUREMENT-ONLY (-DFCS_FLATDMA; rejected: IMIX 4629 vs 5200 GB/s, DESIGN.md §3.3).
+// Variable-length frames, flat chunk stream, chunk windows staged through LDS by DMA
+// (fcs_flatdma_kernel; replaces fcs_flat_kernel<false> in -DFCS_FLATDMA builds).
+// The dealing of fcs_flat_kernel (64-frame windows, 64 chunks per item, frame-start marks), but
+// each lane copies its own 96-byte window into the wave's LDS slot with six
+// global_load_lds_dwordx4 at the window's exact byte address: gfx950's LDS-DMA honours any byte
+// alignment (tools/microbench/glds_align.hip), so no realignment is needed and no VGPR holds the
+// bytes in flight. Lane l's 16-byte piece i lands at slot + 1024 i + 16 l and comes back with one
+// ds_read_b128 per piece (16 lanes per 256-B bank row: 4 cycles, the minimum; random 16-B pieces
+// would cost 12, tools/microbench/lds_pat.hip). A wave deals its next item and issues that item's
+// DMA as soon as the current item's words are in registers, so the next item's bytes land while
+// the current item's CRC work runs (fcs_flat_kernel waits for each item's loads with nothing else
+// to do). An item whose windows reach before the arena start (the frames at the arena's first 96
+// bytes) is loaded into registers instead, with the arena-edge shift of the other kernels.
+// Tables: the 32 KiB slice tables of fcs_dma_kernel (step4_l8) and, in the row holes, the
+// c-indexed shift tables A_{96c} (nibble t of table c at hole 4c + t/2, +64 B for odd t), the A_48
+// merge table and INV of fcs_dma_kernel, A_1536 for frames over 1536 B, and each wave's window
+// scratch (accumulators, marks, frame lists).
+// ---------------------------------------------------------------------------------------------
+#ifndef FCS_FD_AUX   // cache policy of the window DMA (measurement-only override)
+#define FCS_FD_AUX 0
+#endif
+
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing + 16 * kFdSlotBytes];
+    static_assert(kWgThreads / 64 <= 16, "slots");
+    const int tid = threadIdx.x;
+    stage_fd_tables(p, lds, tid);
     init_bad<kDmaBad>(lds);
     __syncthreads();
 
@@ -2290,6 +2300,327 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
     flush_bad<kDmaBad>(p, lds);
 }
 #endif  // FCS_FLATDMA
+
+#ifdef FCS_SPAN
+// ---------------------------------------------------------------------------------------------
+// MEASUREMENT-ONLY (-DFCS_SPAN; rejected: IMIX 4408 vs 4977 GB/s for fcs_flat_kernel in one
+// process). Its loads alone run at 5734-6130 GB/s against the flat kernel's 5344,
+// but its CRC work is not hidden behind them: per item it adds the LDS-DMA writes, seven 16-B
+// window reads and a 16-B realignment to the chain's table lookups, and the CU's VALU and LDS
+// pipes then limit it.
+// Variable-length frames, flat chunk stream staged through LDS by span DMA (fcs_span_kernel;
+// replaces fcs_flat_kernel<false> for windowed batches in -DFCS_SPAN builds).
+// The dealing of fcs_flat_kernel (64-frame windows, 64 chunks per item, frame-start marks), with a
+// frame's chunks dealt front to back: window chunk g is chunk k - 1 - (g - P) back from its frame's
+// end (k chunks, P the frame's first chunk). An item's 64 chunks then lie in arena order, and for
+// packed frames inside one span of at most 64 x 96 bytes (frame-aligned chunks overlap at frame
+// fronts, they never leave gaps). That span is one LDS-DMA of up to six 1 KiB rows into the wave's
+// 6 KiB slot: the coalesced rows of fcs_dma_kernel instead of 64 scattered 96-B windows. Its start
+// and end are wave-uniform scalar work (the frames holding the item's first and last chunk: a
+// ballot over the prefix, readlanes), independent of the per-lane dealing, so the next item's DMA
+// is issued as soon as the current item's windows are in registers; the current item's CRC work
+// and the next item's dealing (marks, ballots, bpermutes) run while it flies. A lane reads its
+// 96-B window at its byte offset in the slot (25 dwords, realigned as in fcs_dma_kernel).
+// An item whose windows do not all lie in its slot (gaps between frames, offsets out of order, a
+// frame over 1536 B between two others) loads them into registers instead (issue_any, the
+// arena-edge path of the other kernels). Frames over 1536 B take the segment loop of
+// fcs_flat_kernel. The next window's offsets and lengths are loaded at the start of the current one.
+// ---------------------------------------------------------------------------------------------
+struct SpanDma {
+    uint64_t src;    // 16-B aligned address of the slot's first byte
+    uint32_t need;   // slot bytes up to the end of the item's last chunk
+    bool rare;       // wave-uniform: the item's chunks do not fit the slot (register loads, no DMA)
+};
+
+// The item's span: 1 KiB rows as far as its bytes reach. The first and the last row keep the
+// default cache policy (their 128-B lines are shared with the neighbouring items), the rows
+// between are non-temporal, as in dma_item.
+__device__ __forceinline__ void span_dma(const uint8_t *slot, const SpanDma &sd, int lane) {
+    typedef __attribute__((address_space(3))) void lds_void;
+    const uint64_t a = sd.src + 16 * (uint64_t)lane, b = a + 4096;
+    lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
+    const uint32_t o = 16u * (uint32_t)lane, need = sd.need;
+    const uint32_t last = (need - 1u) >> 10;   // wave-uniform
+    if (o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_EDGE_AUX);
+    if (1024u + o < need) {
+        if (last == 1) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_EDGE_AUX);
+        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_AUX);
+    }
+    if (2048u + o < need) {
+        if (last == 2) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_EDGE_AUX);
+        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
+    }
+    if (3072u + o < need) {
+        if (last == 3) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_EDGE_AUX);
+        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
+    }
+    if (4096u + o < need) {
+        if (last == 4) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_EDGE_AUX);
+        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
+    }
+    if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_EDGE_AUX);
+}
+
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_span_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing + 16 * kDmaItemBytes];
+    static_assert(kWgThreads / 64 <= 16, "slots");
+    const int tid = threadIdx.x;
+    stage_fd_tables(p, lds, tid);
+    init_bad<kDmaBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & (kGroup - 1);
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    const uint8_t *slot = lds + kDmaRing + wave * kDmaItemBytes;
+    uint8_t *mark = lds + dma_hole(kFdWaveHole + 4u * wave + 2u);
+    uint8_t *list = mark + 64;
+    uint8_t *mlist = lds + dma_hole(kFdWaveHole + 4u * wave + 3u);
+    const uint32_t acc_lane = fd_acc_addr(wave, (uint32_t)lane);
+    const uint64_t lo16 = p.lo4 & ~15ull;
+    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start (host: arena >= 2 slots)
+
+    struct It {
+        int src, zr;
+        uint32_t c;
+        int64_t cstart;
+        bool valid, rare;
+    };
+
+    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
+                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
+    // window metadata, loaded one window ahead (raw: the loads stay in flight): lane i <-> frame 64 win + i
+    auto load_meta = [&](uint64_t win, uint32_t &Lr, uint64_t &Or) {
+        const uint64_t f = win * 64 + (uint64_t)lane;
+        const bool act = win != Dispenser::kEnd && f < p.n;
+        Lr = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
+        Or = act ? (p.off ? p.off[f] : f * p.stride) : 0u;
+    };
+    uint64_t win = D.first();
+    uint32_t Ln;
+    uint64_t On;
+    load_meta(win, Ln, On);
+    uint32_t tagc = 0;   // mark tags: distinct within a window (reset with the marks)
+    while (win != Dispenser::kEnd) {
+        const uint64_t w0 = win * 64;
+        const uint64_t f = w0 + lane;
+        const bool act = f < p.n;
+        const uint32_t L = Ln;
+        const uint64_t E = act ? p.base + On + L : p.lo4;
+        const uint64_t nwin = D.next(win);
+        load_meta(nwin, Ln, On);
+        const bool multi = act && L > (uint32_t)kSegBytes;
+        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
+        uint32_t incl = k;   // inclusive prefix over the window
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t P = incl - k;
+        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+        const uint64_t fmask = __ballot(k != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+        mark[lane] = 0;
+        if (k) list[rank] = (uint8_t)lane;
+        wave_lds_sync();
+        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
+        // no frame over 1536 B: the frames with chunks are lanes 0, 1, ..., so a rank is a lane
+        const bool dense = __ballot(multi) == 0;
+        tagc = 0;
+
+        // wave-uniform: start address of window chunk g < K
+        auto chunk_at = [&](uint32_t g) -> int64_t {
+            const uint32_t rk = (uint32_t)__popcll(__ballot(k != 0 && P <= g)) - 1u;
+            const int fl = dense ? (int)rk : __builtin_amdgcn_readfirstlane((int)list[rk & 63u]);
+            const uint64_t Ef = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Ehi, fl) << 32) |
+                                (uint32_t)__builtin_amdgcn_readlane((int)Elo, fl);
+            const uint32_t Lf = (uint32_t)__builtin_amdgcn_readlane((int)L, fl);
+            const uint32_t Pf = (uint32_t)__builtin_amdgcn_readlane((int)P, fl);
+            const uint32_t kf = Lf ? (Lf + kChunkBytes - 1) / kChunkBytes : 1u;
+            return (int64_t)Ef - (int64_t)kChunkBytes * (int64_t)(kf - (g - Pf));
+        };
+        // the slot of item g0: from its first chunk's 16-B line to its last chunk's end
+        auto span = [&](uint32_t g0) -> SpanDma {
+            const uint32_t g1 = (g0 + 64 < K ? g0 + 64 : K) - 1u;
+            const int64_t s0 = chunk_at(g0), e1 = chunk_at(g1) + kChunkBytes;
+            SpanDma sd;
+            const uint64_t a = (uint64_t)s0 & ~15ull;
+            sd.src = a < lo16 ? lo16 : (a > smax ? smax : a);
+            const int64_t need = e1 - (int64_t)sd.src;
+            sd.rare = need <= 0 || need > (int64_t)kDmaItemBytes;
+            sd.need = (uint32_t)__builtin_amdgcn_readfirstlane((int)(sd.rare ? 1u : (uint32_t)need));
+            sd.src = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sd.src >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sd.src);
+            return sd;
+        };
+        // deal item g0: lane -> (frame, chunk); the item stays on the DMA path only if every lane's
+        // frame bytes lie in the slot
+        auto prep = [&](uint32_t g0, const SpanDma &sd, It &it) {
+            const uint8_t tag = (uint8_t)++tagc;
+            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = tag;
+            wave_lds_sync();
+            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
+            const uint64_t M = __ballot(mark[lane] == tag);
+            const uint32_t g = g0 + (uint32_t)lane;
+            it.valid = g < K;
+            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
+            it.src = it.valid ? (dense ? (int)(rk & 63u) : (int)list[rk & 63u]) : 0;
+            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, it.src) << 32) | (uint32_t)__shfl((int)Elo, it.src);
+            const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
+            const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
+            const uint32_t kg = Lg ? (Lg + kChunkBytes - 1) / kChunkBytes : 1u;
+            it.c = it.valid ? kg - 1u - (g - Pg) : 0u;   // chunk index back from the frame end
+            it.cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
+            const int64_t fs = (int64_t)(Eg - Lg);
+            it.zr = it.valid ? clamp_zr(fs - it.cstart) : kChunkBytes;
+            const int64_t lo = it.cstart > fs ? it.cstart : fs;
+            const bool in = !it.valid || it.zr >= kChunkBytes ||
+                            (lo >= (int64_t)sd.src && it.cstart + kChunkBytes <= (int64_t)sd.src + (int64_t)sd.need);
+            it.rare = sd.rare || __any(!in);
+        };
+
+        if (K) {
+            SpanDma sp = span(0);
+            if (!sp.rare) span_dma(slot, sp, lane);
+            It cur;
+            prep(0, sp, cur);
+            for (uint32_t g0 = 0; g0 < K; g0 += 64) {
+                const bool more = g0 + 64 < K;
+                SpanDma sn{0, 1u, true};
+                if (more) sn = span(g0 + 64);
+                uint32_t w[kChunkWords];
+#ifdef FCS_SPAN_B32   // measurement-only: 25 dword reads at the window's 4-B address (bank conflicts)
+                if (!cur.rare) {
+                    const int x = cur.valid ? (int)(cur.cstart - (int64_t)sp.src) : 0;
+                    const uint32_t r = (uint32_t)x & 3u;
+                    const uint8_t *wp = slot + (x & ~3);
+                    uint32_t d[kChunkWords + 1];
+                    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+                    for (int q = 0; q < kChunkWords; q++) d[q] = *reinterpret_cast<const uint32_t *>(wp + 4 * q);
+                    {
+                        const uint8_t *a24 = wp + 4 * kChunkWords, *lim = slot + kDmaItemBytes - 4;
+                        d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xC07F);
+#pragma unroll
+                    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+                } else
+#endif
+                if (!cur.rare) {
+                    // the window at its byte offset x in the slot (x >= -95: a front window reaching
+                    // before the arena start reads LDS below the slot, bytes that get masked), read
+                    // as seven 16-B pieces from x rounded down to 16 B: packed windows sit at 64..96-B
+                    // strides, where ds_read_b32 would put 16-32 lanes on one bank (25 reads), and
+                    // ds_read_b128 8-16 lanes on one 16-B group (7 reads; tools/microbench/lds_pat.hip)
+                    const int x = cur.valid ? (int)(cur.cstart - (int64_t)sp.src) : 0;
+                    const uint8_t *wp = slot + (x & ~15);
+                    u32x4 q[7];
+                    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the item's span has landed
+#pragma unroll
+                    for (int i = 0; i < 6; i++) q[i] = *reinterpret_cast<const u32x4 *>(wp + 16 * i);
+                    {   // the 7th piece matters only when x is not 16-B aligned, and then lies in the slot
+                        const uint8_t *a6 = wp + 96, *lim = slot + kDmaItemBytes - 16;
+                        q[6] = *reinterpret_cast<const u32x4 *>(a6 < lim ? a6 : lim);
+                    }
+                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next span
+                    uint32_t d[28];
+#pragma unroll
+                    for (int i = 0; i < 7; i++) {
+                        d[4 * i] = q[i].x;
+                        d[4 * i + 1] = q[i].y;
+                        d[4 * i + 2] = q[i].z;
+                        d[4 * i + 3] = q[i].w;
+                    }
+                    // realign: dword shift s = (x >> 2) & 3 in two select stages, then the byte shift.
+                    // The selects are v_perm (whole dword from either source): written as ?: the
+                    // compiler turns the stages into an indexed array in scratch memory.
+#ifdef FCS_SPAN_ABL_NOALIGN   // measurement-only: no realignment (wrong FCS unless x is 16-B aligned)
+#pragma unroll
+                    for (int i = 0; i < kChunkWords; i++) w[i] = d[i];
+#else
+                    const uint32_t p1 = (x & 4) ? 0x07060504u : 0x03020100u, p2 = (x & 8) ? 0x07060504u : 0x03020100u;
+#pragma unroll
+                    for (int i = 0; i < 26; i++) d[i] = __builtin_amdgcn_perm(d[i + 2], d[i], p2);
+#pragma unroll
+                    for (int i = 0; i < 25; i++) d[i] = __builtin_amdgcn_perm(d[i + 1], d[i], p1);
+                    const uint32_t r = (uint32_t)x & 3u;
+#pragma unroll
+                    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#endif
+                } else {   // register loads (with the arena-edge shift)
+                    Chunk ch;
+                    issue_any<false>(p, cur.cstart, cur.valid && cur.zr < kChunkBytes, ch);
+                    fd_chunk_words(ch, w);
+                    __builtin_amdgcn_s_waitcnt(0x0F70);   // and a span DMA issued for this item, if any
+                }
+                if (more && !sn.rare) span_dma(slot, sn, lane);
+                {
+#ifdef FCS_SPAN_NOCRC   // measurement-only build: the span DMA, reads and dealing without the CRC work
+                    uint32_t v = cur.c;
+#pragma unroll
+                    for (int i = 0; i < kChunkWords; i++) v ^= w[i];
+#else
+                    // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
+                    const uint32_t own = fd_value(lds, w, cur.zr, cur.zr < kChunkBytes ? cur.zr : 0,
+                                                  cur.valid ? fd_inv(lds, cur.zr) : 0u, B, SEL);
+                    const uint32_t v = fd_chunk_shift(lds, own, cur.c & 15u);
+#endif
+                    if (cur.valid && v) atomicXor(reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)cur.src)), v);
+                }
+                if (more) prep(g0 + 64, sn, cur);
+                sp = sn;
+            }
+        }
+
+        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment (register loads) ----
+        const uint64_t xmask = __ballot(multi);
+        const uint32_t nx = (uint32_t)__popcll(xmask);
+        if (nx) {
+            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
+            if (multi) mlist[rx] = (uint8_t)lane;
+            wave_lds_sync();
+            for (uint32_t t = 0; t < nx; t += 4) {
+                const uint32_t rnk = t + (uint32_t)(lane >> 4);
+                const bool valid = rnk < nx;
+                const int src = valid ? (int)mlist[rnk] : 0;
+                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
+                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
+                uint32_t s = 0;
+                for (uint32_t q = 0; __any(q < m); q++) {
+                    const bool on = q < m;
+                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
+                                           (int64_t)kChunkBytes * (j + 1);
+                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
+                    Chunk cc;
+                    issue_any<false>(p, cstart, on && zr < kChunkBytes, cc);
+                    uint32_t w[kChunkWords];
+                    fd_chunk_words(cc, w);
+                    const uint32_t r = fd_value(lds, w, zr, on ? zr : 0, (on && q == 0) ? fd_inv(lds, zr) : 0u, B, SEL);
+                    s = on ? (q == 0 ? r : fd_jump(lds, s, r)) : s;
+                }
+                const uint32_t v = row_xor(fd_chunk_shift(lds, s, (uint32_t)j));
+                if (valid && j == 15) *reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)src)) = v;
+            }
+        }
+
+        // ---- one coalesced store per window; clear the accumulators ----
+        wave_lds_sync();
+        uint32_t *accp = reinterpret_cast<uint32_t *>(lds + acc_lane);
+        const uint32_t a = *accp;
+        emit<kDmaBad>(p, lds, act, f, L ? ~a : 0u);
+        *accp = 0u;
+        win = nwin;
+    }
+    flush_bad<kDmaBad>(p, lds);
+}
+#endif  // FCS_SPAN
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -2586,6 +2917,10 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #elif defined(FCS_FLATDMA)   // measurement-only build: per-lane window DMA (rejected)
             hipLaunchKernelGGL(fcs_flatdma_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
 #else
+#ifdef FCS_SPAN   // measurement-only build: span DMA (rejected)
+            if (var_span(p)) hipLaunchKernelGGL(fcs_span_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
+            else
+#endif
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
 #endif
         }

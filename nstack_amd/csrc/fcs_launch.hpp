@@ -106,6 +106,17 @@ inline bool fixed_single(const KParams &p) {
     return p.fseg == 1 && p.zmax <= kSingleMaxLead;
 #endif
 }
+// Windowed variable-length batches (and the short fixed-length route) take fcs_flat_kernel.
+// Measurement-only (-DFCS_SPAN): the span-DMA kernel (fcs_span_kernel) instead when the arena
+// holds two 6 KiB slots (its slots are clamped to the arena's last 6 KiB). DESIGN.md §3.3.
+inline bool var_span(const KParams &p) {
+#ifdef FCS_SPAN
+    return p.hi4 - p.lo4 >= 2 * 6144ull;
+#else
+    (void)p;
+    return false;
+#endif
+}
 // LDS-DMA kernel (fcs_dma_kernel): one-segment frames of kDmaMinLen..kDmaCover bytes whose four
 // consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
 // frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
