@@ -855,7 +855,7 @@ constexpr uint32_t kDmaInvHole = kDmaMergeHole + 4 * 5;             // 3 holes: 
 constexpr uint32_t kDmaBad = dma_hole(kDmaInvHole + 3);            // 16 x 8 B
 constexpr uint32_t kDmaRing = 65536;                                // slots start after the tables
 constexpr int kDmaWaves = kDmaWgThreads / 64;
-constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)kDmaWaves * kDmaItemBytes;
+constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)kDmaWaves * (kDmaPair ? 2u : 1u) * kDmaItemBytes;
 static_assert(kDmaLdsBytes <= 163840, "LDS per CU");
 static_assert(kDmaChains - 1 <= 5, "merge holes");
 #ifndef FCS_DMA_AUX   // cache policy of the slot DMA (2 = nt; measurement-only override)
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     const int c = lane & (kGroup - 1);     // chunk index back from the frame end
     const int g = lane >> 4;               // frame of the item
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
+    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)wave * (kDmaPair ? 2u : 1u) * kDmaItemBytes;
     const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
     const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
     const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
@@ -1019,14 +1019,105 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     constexpr uint64_t kEnd = Dispenser::kEnd;
     Dispenser D(p.ctr, (p.n + 3) >> 2, (uint64_t)gridDim.x * kDmaWaves,
                 (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
-    uint64_t it = D.first();
     auto item_start = [&](uint64_t i) { return p.base + 4 * i * p.stride; };   // first frame of item i
     // slot bytes an item's windows read: up to its last frame's end plus the realignment dword
     auto item_need = [&](uint64_t S, uint64_t src) {
         const uint64_t e = S + 3 * p.stride + p.flen + 4 - src;
         return (uint32_t)(e < (uint64_t)kDmaItemBytes ? e : (uint64_t)kDmaItemBytes);
     };
-    if (it != kEnd) dma_item(slot0, slot_src(item_start(it)), lane, item_need(item_start(it), slot_src(item_start(it))));
+    auto dma_of = [&](const uint8_t *slot, uint64_t i) {
+#ifdef FCS_DMA_PRIO   // measurement-only: the slot DMA issued at raised wave priority
+        LoadPriority lp;
+#endif
+        const uint64_t S = item_start(i), sn = slot_src(S);
+        dma_item(slot, sn, lane, item_need(S, sn));
+    };
+    // this lane's window of item i, realigned and front-masked (d: 25 raw dwords from the slot)
+    auto read_window = [&](const uint8_t *slot, uint64_t i, uint32_t (&d)[kChunkWords + 1]) -> uint32_t {
+        const uint64_t S = item_start(i), src = slot_src(S);
+        const int64_t x = (int64_t)(S - src) + klane;   // window start within the slot (>= -28)
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
+#pragma unroll
+        for (int q = 0; q < kChunkWords; q++) d[q] = wp[q];
+        // the 25th dword matters only when r != 0; then it lies inside the slot. Clamped so the
+        // last slot in LDS is never read past its end.
+        const uint64_t a24 = (uint64_t)(wp + kChunkWords), lim = (uint64_t)(slot + kDmaItemBytes - 4);
+        d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
+        return (uint32_t)x & 3u;
+    };
+    auto realign = [&](const uint32_t (&d)[kChunkWords + 1], uint32_t r, uint32_t (&w)[kChunkWords]) {
+#pragma unroll
+        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#pragma unroll
+        for (int i = 0; i < MW; i++) w[i] &= m[i];
+    };
+
+    if constexpr (kDmaPair) {
+        // ---- two items per wave at once (8 waves per CU, one slot each): half the DMA streams
+        //      of 16 one-slot waves with the same bytes in flight, and both items' chains
+        //      interleaved (2 kDmaChains independent chains per lane) ----
+        const uint8_t *slot1 = slot0 + kDmaItemBytes;
+        uint64_t ia = D.first();
+        uint64_t ib = ia != kEnd ? D.next(ia) : kEnd;
+        if (ia != kEnd) dma_of(slot0, ia);
+        if (ib != kEnd) dma_of(slot1, ib);
+        while (ia != kEnd) {   // wave-uniform
+            const bool hb = ib != kEnd;
+            uint32_t da[kChunkWords + 1], db[kChunkWords + 1];
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): both slots have landed
+            const uint32_t ra = read_window(slot0, ia, da);
+            const uint32_t rb = read_window(slot1, hb ? ib : ia, db);
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): both slots are free for the next DMAs
+            uint64_t na = kEnd, nb = kEnd;
+            if (hb) {
+                na = D.next(ib);
+                if (na != kEnd) nb = D.next(na);
+            }
+            if (na != kEnd) dma_of(slot0, na);
+            if (nb != kEnd) dma_of(slot1, nb);
+            if (STREAM) {
+                uint32_t acc = ra ^ rb;
+#pragma unroll
+                for (int q = 0; q <= kChunkWords; q++) acc ^= da[q] ^ db[q];
+                if (acc == 0x9E3779B9u) p.out[0] = acc;   // keeps the reads live; practically never stores
+            } else {
+                uint32_t wa[kChunkWords], wb[kChunkWords];
+                realign(da, ra, wa);
+                realign(db, rb, wb);
+                constexpr int CL = kDmaChainWords;
+                uint32_t xa[kDmaChains], xb[kDmaChains];
+#pragma unroll
+                for (int hh = 0; hh < kDmaChains; hh++) {
+                    xa[hh] = wa[hh * CL] ^ (hh == 0 ? x0 : 0u);
+                    xb[hh] = wb[hh * CL] ^ (hh == 0 ? x0 : 0u);
+                }
+#pragma unroll
+                for (int i = 0; i < CL; i++)
+#pragma unroll
+                    for (int hh = 0; hh < kDmaChains; hh++) {
+                        xa[hh] = step4_l8(lds, xa[hh], i < CL - 1 ? wa[hh * CL + i + 1] : 0u, B, SEL);
+                        xb[hh] = step4_l8(lds, xb[hh], i < CL - 1 ? wb[hh * CL + i + 1] : 0u, B, SEL);
+                    }
+                uint32_t ma = xa[kDmaChains - 1], mb = xb[kDmaChains - 1];
+#pragma unroll
+                for (int hh = 0; hh < kDmaChains - 1; hh++) {
+                    ma = merge_shift_dma(lds, kDmaChains - 2 - hh, xa[hh], ma);
+                    mb = merge_shift_dma(lds, kDmaChains - 2 - hh, xb[hh], mb);
+                }
+                const uint32_t va = row_xor(lane_shift_dma(lds, ma, lanebase));
+                const uint32_t vb = row_xor(lane_shift_dma(lds, mb, lanebase));
+                emit<kDmaBad>(p, lds, c == kGroup - 1 && 4 * ia + g < p.n, 4 * ia + g, ~va);
+                emit<kDmaBad>(p, lds, hb && c == kGroup - 1 && 4 * ib + g < p.n, 4 * ib + g, ~vb);
+            }
+            ia = na;
+            ib = nb;
+        }
+        flush_bad<kDmaBad>(p, lds);
+        return;
+    }
+
+    uint64_t it = D.first();
+    if (it != kEnd) dma_of(slot0, it);
 
 #ifdef FCS_STAMPS   // measurement-only: per-wave cycles waiting for the slot vs. the whole item
     uint64_t st_wait = 0, st_all = 0, st_items = 0;
@@ -1062,10 +1153,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
         const uint64_t nxt = D.next(it);
-        if (nxt != kEnd) {
-            const uint64_t Sn = item_start(nxt), sn = slot_src(Sn);
-            dma_item(slot, sn, lane, item_need(Sn, sn));
-        }
+        if (nxt != kEnd) dma_of(slot, nxt);
 
         if (STREAM) {   // read ceiling: the words are only XORed together
             uint32_t acc = r;

@@ -121,10 +121,14 @@ inline bool var_span(const KParams &p) {
 // consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
 // frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
 // and the arena must hold a whole slot (the last items' slots are clamped to its end).
-#ifndef FCS_DMA_WG_THREADS   // measurement-only override
-#define FCS_DMA_WG_THREADS 1024
+#ifndef FCS_DMA_PAIR   // 1: each wave works on two items at once, one 6 KiB slot each (8 waves per CU)
+#define FCS_DMA_PAIR 0
 #endif
-constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;  // one 6 KiB LDS slot per wave
+constexpr bool kDmaPair = FCS_DMA_PAIR != 0;
+#ifndef FCS_DMA_WG_THREADS   // measurement-only override
+#define FCS_DMA_WG_THREADS (FCS_DMA_PAIR ? 512 : 1024)
+#endif
+constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;  // one 6 KiB LDS slot per wave (two in pair mode)
 static_assert(kDmaWgThreads % 64 == 0 && kDmaWgThreads <= 1024, "LDS holds 16 slots next to the 64 KiB tables");
 // Batches of at least this many items (4 frames) per wave of the grid hand their tail out
 // dynamically (KParams::ctr): below it the static share alone balances well enough.
