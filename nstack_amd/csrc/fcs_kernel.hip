@@ -1966,8 +1966,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
             int src, zr;
             uint32_t c;
             bool valid;
+            int64_t cstart;
         };
-        auto prep = [&](uint32_t g0, uint32_t tag, FlatItem &it) {
+        auto deal = [&](uint32_t g0, uint32_t tag, FlatItem &it) {
             // frame starts inside this item: mark their slot, then lane g finds its frame's rank
             // as (frames started before the item) + (marks at or below g) - 1
             if (k && P >= g0 && P < g0 + 64) mark[P - g0] = (uint8_t)tag;
@@ -1983,9 +1984,13 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
             const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
             const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
             it.c = it.valid ? g - Pg : 0u;   // chunk index back from the frame end
-            const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
-            it.zr = it.valid ? clamp_zr((int64_t)(Eg - Lg) - cstart) : kChunkBytes;
-            issue_any<TINY>(p, cstart, it.valid && it.zr < kChunkBytes, it.ch);
+            it.cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
+            it.zr = it.valid ? clamp_zr((int64_t)(Eg - Lg) - it.cstart) : kChunkBytes;
+        };
+        auto issue = [&](FlatItem &it) { issue_any<TINY>(p, it.cstart, it.valid && it.zr < kChunkBytes, it.ch); };
+        auto prep = [&](uint32_t g0, uint32_t tag, FlatItem &it) {
+            deal(g0, tag, it);
+            issue(it);
         };
         auto finish = [&](const FlatItem &it) {
 #ifdef FCS_FLAT_NOCRC   // measurement-only build: loads and dealing without the CRC work (wrong FCS)
@@ -2014,6 +2019,24 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
                 prep(g0, tag, A);
                 finish(B);
                 g0 += 64; tag++;
+            }
+        }
+#elif defined(FCS_FLAT_DEAL_AHEAD)   // measurement-only: the next item dealt while this item's loads fly
+        if (K) {
+            FlatItem it, nx;
+            deal(0, 1, it);
+            for (uint32_t g0 = 0, tag = 1; g0 < K; g0 += 64, tag++) {
+                issue(it);
+                const bool more = g0 + 64 < K;
+                if (more) deal(g0 + 64, tag + 1, nx);
+                finish(it);
+                if (more) {
+                    it.src = nx.src;
+                    it.zr = nx.zr;
+                    it.c = nx.c;
+                    it.valid = nx.valid;
+                    it.cstart = nx.cstart;
+                }
             }
         }
 #else
