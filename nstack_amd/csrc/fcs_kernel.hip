@@ -2175,30 +2175,163 @@ __device__ __forceinline__ uint32_t fd_value(const uint8_t *lds, uint32_t (&w)[k
 }
 
 // Table image of the variable-length LDS-DMA kernels (layout above); zeroes every wave's scratch.
+template <int NT = kWgThreads>
 __device__ __forceinline__ void stage_fd_tables(const KParams &p, uint8_t *lds, int tid) {
-    for (int i = tid; i < 2048; i += kWgThreads) {   // slice tables as fcs_dma_kernel
+    for (int i = tid; i < 2048; i += NT) {   // slice tables as fcs_dma_kernel
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
     }
-    for (int i = tid; i < 16 * 128; i += kWgThreads) {   // A_{96c}: table c, nibble t, entry e
+    for (int i = tid; i < 16 * 128; i += NT) {   // A_{96c}: table c, nibble t, entry e
         const int c = i >> 7, t = (i >> 4) & 7, e = i & 15;
         *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * (uint32_t)c + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
                                       4u * (uint32_t)e) = p.blob[kBlobFlat + c * (kFlatStride / 4) + t * 16 + e];
     }
-    for (int i = tid; i < 128; i += kWgThreads) {   // A_48 (merge table 0 of fcs_dma_kernel) and A_1536
+    for (int i = tid; i < 128; i += NT) {   // A_48 (merge table 0 of fcs_dma_kernel) and A_1536
         const int t = (i >> 4) & 7, e = i & 15;
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaMergeHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
                                       4u * (uint32_t)e) = p.blob[kBlobMerge + (kDmaChainWords / 2 - 1) * 128 + i];
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdJumpHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
                                       4u * (uint32_t)e) = p.blob[kBlobJump + i];
     }
-    for (int i = tid; i < kChunkBytes; i += kWgThreads)
+    for (int i = tid; i < kChunkBytes; i += NT)
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
             p.blob[kBlobInv + i];
-    for (int i = tid; i < 16 * 4 * 32; i += kWgThreads)   // window scratch of every wave: zero
+    for (int i = tid; i < 16 * 4 * 32; i += NT)   // window scratch of every wave: zero
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdWaveHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) = 0u;
 }
+
+#ifdef FCS_FLAT2
+// ---------------------------------------------------------------------------------------------
+// MEASUREMENT-ONLY (-DFCS_FLAT2; rejected, DESIGN.md §3.3: 2 x 8 waves IMIX +2 %, 576 B -2 %;
+// 2 x 10 and 2 x 12 waves slower or mixed).
+// The flat chunk stream at two workgroups per CU (fcs_flat2_kernel). fcs_flat_kernel runs slower
+// with fewer waves per CU (IMIX, one process: 12 waves 4828, 14 waves 5078, 16 waves 5286 GB/s),
+// and 16 is one workgroup's limit. This form
+// keeps the flat kernel's dealing and chunk work but takes the compact 64 KiB table image of the
+// LDS-DMA kernels (32 KiB of 8-replica slice tables; A_{96c}, A_48, A_1536, INV and each wave's
+// accumulators, marks and lists in the row holes: stage_fd_tables), so two workgroups of
+// kFlat2Threads fit one CU's LDS, and its registers are held to kFlat2Waves / 4 waves per SIMD.
+// ---------------------------------------------------------------------------------------------
+template <int NT>
+__global__ __launch_bounds__(NT, 2) void fcs_flat2_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing];
+    static_assert(NT / 64 <= 16, "wave scratch holds 16 waves");
+    const int tid = threadIdx.x;
+    stage_fd_tables<NT>(p, lds, tid);
+    init_bad<kDmaBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const int j = lane & (kGroup - 1);
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    uint8_t *mark = lds + dma_hole(kFdWaveHole + 4u * wave + 2u);
+    uint8_t *list = mark + 64;
+    uint8_t *mlist = lds + dma_hole(kFdWaveHole + 4u * wave + 3u);
+    auto acc = [&](uint32_t i) { return reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, i)); };
+
+    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (NT / 64),
+                (uint64_t)blockIdx.x * (NT / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
+    for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
+        const uint64_t w0 = win * 64;
+        // ---- window metadata: lane i <-> frame w0 + i ----
+        const uint64_t f = w0 + lane;
+        const bool act = f < p.n;
+        const uint32_t L = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
+        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;
+        const bool multi = act && L > (uint32_t)kSegBytes;
+        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
+        uint32_t incl = k;   // inclusive prefix over the window
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+            if (lane >= d) incl += y;
+        }
+        const uint32_t P = incl - k;
+        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+        const uint64_t fmask = __ballot(k != 0);
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+        mark[lane] = 0;
+        if (k) list[rank] = (uint8_t)lane;
+        wave_lds_sync();
+        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
+        // no frame over 1536 B: a chunk's frame rank is its frame's lane; frame ends in one 4 GiB page
+        const bool dense = __ballot(multi) == 0;
+        const uint32_t Ehi0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)Ehi);
+        const bool onehi = __ballot(Ehi != Ehi0) == 0;
+
+        // one item = 64 chunks: lane -> (frame, chunk), its loads, its chunk value into the frame
+        for (uint32_t g0 = 0, tag = 1; g0 < K; g0 += 64, tag++) {
+            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = (uint8_t)tag;
+            wave_lds_sync();
+            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
+            const uint64_t M = __ballot(mark[lane] == (uint8_t)tag);
+            const uint32_t g = g0 + (uint32_t)lane;
+            const bool valid = g < K;
+            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
+            const int src = valid ? (dense ? (int)(rk & 63u) : (int)list[rk & 63u]) : 0;
+            const uint32_t Eghi = onehi ? Ehi0 : (uint32_t)__shfl((int)Ehi, src);
+            const uint64_t Eg = ((uint64_t)Eghi << 32) | (uint32_t)__shfl((int)Elo, src);
+            const uint32_t Lg = (uint32_t)__shfl((int)L, src);
+            const uint32_t Pg = (uint32_t)__shfl((int)P, src);
+            const uint32_t c = valid ? g - Pg : 0u;   // chunk index back from the frame end
+            const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(c + 1);
+            const int zr = valid ? clamp_zr((int64_t)(Eg - Lg) - cstart) : kChunkBytes;
+            Chunk ch;
+            issue_any<false>(p, cstart, valid && zr < kChunkBytes, ch);
+            uint32_t w[kChunkWords];
+            fd_chunk_words(ch, w);
+            // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
+            const uint32_t own = fd_value(lds, w, zr, zr < kChunkBytes ? zr : 0, valid ? fd_inv(lds, zr) : 0u, B, SEL);
+            const uint32_t v = fd_chunk_shift(lds, own, c & 15u);
+            if (valid && v) atomicXor(acc((uint32_t)src), v);
+        }
+
+        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment ----
+        const uint64_t xmask = __ballot(multi);
+        const uint32_t nx = (uint32_t)__popcll(xmask);
+        if (nx) {
+            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
+            if (multi) mlist[rx] = (uint8_t)lane;
+            wave_lds_sync();
+            for (uint32_t t = 0; t < nx; t += 4) {
+                const uint32_t rnk = t + (uint32_t)(lane >> 4);
+                const bool valid = rnk < nx;
+                const int src = valid ? (int)mlist[rnk] : 0;
+                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
+                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
+                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
+                uint32_t s = 0;
+                for (uint32_t q = 0; __any(q < m); q++) {
+                    const bool on = q < m;
+                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
+                                           (int64_t)kChunkBytes * (j + 1);
+                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
+                    Chunk cc;
+                    issue_any<false>(p, cstart, on && zr < kChunkBytes, cc);
+                    uint32_t w[kChunkWords];
+                    fd_chunk_words(cc, w);
+                    const uint32_t r = fd_value(lds, w, zr, on ? zr : 0, (on && q == 0) ? fd_inv(lds, zr) : 0u, B, SEL);
+                    s = on ? (q == 0 ? r : fd_jump(lds, s, r)) : s;
+                }
+                const uint32_t v = row_xor(fd_chunk_shift(lds, s, (uint32_t)j));
+                if (valid && j == 15) *acc((uint32_t)src) = v;
+            }
+        }
+
+        // ---- one coalesced store per window; clear the accumulators ----
+        wave_lds_sync();
+        const uint32_t a = *acc((uint32_t)lane);
+        emit<kDmaBad>(p, lds, act, f, L ? ~a : 0u);
+        *acc((uint32_t)lane) = 0u;
+    }
+    flush_bad<kDmaBad>(p, lds);
+}
+#endif  // FCS_FLAT2
 
 #ifdef FCS_FLATDMA
 constexpr uint32_t kFdSlotBytes = 6144;                // 64 lanes x 96 B, piece i of lane l at 1024 i + 16 l
@@ -3028,6 +3161,10 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #elif defined(FCS_FLATDMA)   // measurement-only build: per-lane window DMA (rejected)
             hipLaunchKernelGGL(fcs_flatdma_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
 #else
+#ifdef FCS_FLAT2
+            if (var_flat2(p)) hipLaunchKernelGGL(fcs_flat2_kernel<kFlat2Threads>, dim3(2 * grid), dim3(kFlat2Threads), 0, st, p);
+            else
+#endif
 #ifdef FCS_SPAN   // measurement-only build: span DMA (rejected)
             if (var_span(p)) hipLaunchKernelGGL(fcs_span_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
             else

@@ -117,6 +117,13 @@ inline bool var_span(const KParams &p) {
     return false;
 #endif
 }
+// Measurement-only (-DFCS_FLAT2): windowed batches at two workgroups of kFlat2Threads per CU
+// (fcs_flat2_kernel; the host's grid counts CUs, the launcher doubles it) when the arena is not tiny.
+#ifndef FCS_FLAT2_THREADS
+#define FCS_FLAT2_THREADS 640
+#endif
+constexpr int kFlat2Threads = FCS_FLAT2_THREADS;
+inline bool var_flat2(const KParams &p) { return p.hi4 - p.lo4 >= 2 * (uint64_t)kChunkBytes; }
 // LDS-DMA kernel (fcs_dma_kernel): one-segment frames of kDmaMinLen..kDmaCover bytes whose four
 // consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
 // frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
