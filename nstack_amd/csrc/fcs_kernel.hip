@@ -57,6 +57,18 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
 }
 
+// Clears the low t bits of w, t clamped to 0..32 (bytes of a window before the frame start). The
+// clamp is one v_med3_i32: written as min/max the compiler proves t >= 0 after the max, turns the
+// min unsigned and keeps two instructions.
+__device__ __forceinline__ uint32_t clear_low_bits(uint32_t w, int t) {
+#ifdef FCS_MASK_MINMAX   // measurement-only: the two-instruction clamp
+    t = t < 0 ? 0 : (t > 32 ? 32 : t);
+#else
+    asm("v_med3_i32 %0, %1, 0, 32" : "=v"(t) : "v"(t));
+#endif
+    return w & (uint32_t)(0xFFFFFFFFull << t);
+}
+
 __device__ __forceinline__ uint32_t lds_rd(const uint8_t *lds, uint32_t byte_addr) {
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
@@ -1619,9 +1631,7 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
                 if (!__any(zb > 16 * g)) break;
 #pragma unroll
                 for (int i = 4 * g; i < 4 * g + 4; i++) {
-                    int t = zf8 - 32 * i;
-                    t = t < 0 ? 0 : (t > 32 ? 32 : t);
-                    w[i] &= (uint32_t)(0xFFFFFFFFull << t);
+                    w[i] = clear_low_bits(w[i], zf8 - 32 * i);
                 }
             }
             x0 = x0f;
@@ -1728,9 +1738,7 @@ __device__ __forceinline__ uint32_t chunk_value(const uint8_t *lds, const Chunk 
         if (!__any(zb > 16 * g)) break;
 #pragma unroll
         for (int i = 4 * g; i < 4 * g + 4; i++) {
-            int t = zr8 - 32 * i;
-            t = t < 0 ? 0 : (t > 32 ? 32 : t);
-            w[i] &= (uint32_t)(0xFFFFFFFFull << t);
+            w[i] = clear_low_bits(w[i], zr8 - 32 * i);
         }
     }
 #endif
@@ -2160,9 +2168,7 @@ __device__ __forceinline__ uint32_t fd_value(const uint8_t *lds, uint32_t (&w)[k
         if (!__any(zb > 16 * g)) break;
 #pragma unroll
         for (int i = 4 * g; i < 4 * g + 4; i++) {
-            int t = zr8 - 32 * i;
-            t = t < 0 ? 0 : (t > 32 ? 32 : t);
-            w[i] &= (uint32_t)(0xFFFFFFFFull << t);
+            w[i] = clear_low_bits(w[i], zr8 - 32 * i);
         }
     }
     uint32_t xa = x0 ^ w[0], xb = w[12];
