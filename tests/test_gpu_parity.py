@@ -252,6 +252,70 @@ def test_baseline_size_properties(dev, oracle):
     torch.cuda.empty_cache()
 
 
+def test_baseline_imix_size_properties(dev, oracle):
+    """BASELINE configs[2]: 128 M IMIX frames (7:4:1 of 64/576/1518, shuffled, packed; 47.8 GB) in
+    one launch of the windowed kernel: sampled frames == oracle, the two halves of the frame list
+    launched separately == one launch, and a second launch is bit-identical."""
+    n = 128 << 20
+    rng = np.random.default_rng(2027)
+    ln = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), [n * 7 // 12, n * 4 // 12, n - n * 7 // 12 - n * 4 // 12])
+    rng.shuffle(ln)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1], dtype=np.uint64, out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    free, _ = torch.cuda.mem_get_info()
+    if free < total + 12 * n + (4 << 30):
+        pytest.skip("not enough HBM")
+    arena = torch.empty(total, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, total, 2027, 0)
+    o = to_dev(off.view(np.int64), dev)
+    l_ = to_dev(ln.view(np.int32), dev)
+
+    def launch(lo, hi):
+        out = torch.empty(hi - lo, dtype=torch.int32, device=dev)
+        na.batch_dev(arena, total, o[lo:], l_[lo:], out, hi - lo)
+        torch.cuda.synchronize()
+        return out.cpu().numpy().view(np.uint32)
+
+    a = launch(0, n)
+    h = n // 2
+    assert np.array_equal(a, np.concatenate([launch(0, h), launch(h, n)]))
+    assert np.array_equal(a, launch(0, n))
+    idx = np.unique(np.concatenate([rng.integers(0, n, 3000), [0, 1, n - 2, n - 1]]))
+    buf = np.empty(1518, dtype=np.uint8)
+    for i in idx:
+        L = int(ln[i])
+        oracle.oracle_splitmix_fill(buf.ctypes.data, L, 2027, int(off[i]))
+        assert int(a[i]) == oracle.oracle_crc32_fast(buf.ctypes.data, L), int(i)
+    del arena, o, l_
+    torch.cuda.empty_cache()
+
+
+def test_baseline_jumbo_size_properties(dev, oracle):
+    """BASELINE configs[3]: 16 M x 9000-B frames (151 GB) in one launch of the interleaved segment
+    kernel: sampled frames == oracle, two half launches == one launch, determinism."""
+    n, L = 16 << 20, 9000
+    free, _ = torch.cuda.mem_get_info()
+    if free < n * L + (4 << 30):
+        pytest.skip("not enough HBM")
+    arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, n * L, 2028, 0)
+    a = run_fixed(dev, arena, L, L, n)
+    h = n // 2 + 1   # an odd split: the second half starts inside a 4-frame unit of the first launch
+    b0 = run_fixed(dev, arena, L, L, h)
+    b1 = run_fixed(dev, arena.data_ptr() + h * L, L, L, n - h)
+    assert np.array_equal(a, np.concatenate([b0, b1]))
+    assert np.array_equal(a, run_fixed(dev, arena, L, L, n))
+    rng = np.random.default_rng(3)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 2000), [0, 1, n - 2, n - 1]]))
+    buf = np.empty(L, dtype=np.uint8)
+    for i in idx:
+        oracle.oracle_splitmix_fill(buf.ctypes.data, L, 2028, int(i) * L)
+        assert int(a[i]) == oracle.oracle_crc32_fast(buf.ctypes.data, L), int(i)
+    del arena
+    torch.cuda.empty_cache()
+
+
 # ---------------------------------------------------------------- host-side entry points
 def test_fixed_host_and_batch_host(dev, var_kernel, oracle):
     n, L = 300000, 1518
