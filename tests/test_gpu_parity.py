@@ -291,6 +291,46 @@ def test_baseline_imix_size_properties(dev, oracle):
     torch.cuda.empty_cache()
 
 
+def test_more_than_2_32_frames(dev, oracle):
+    """2^32 + 1001 one-byte frames in one launch (the flat route without a length array): frame
+    indices, window numbers and output offsets past 32 bits. Sampled frames, the frames on both
+    sides of index 2^32 and the last frames are checked against the oracle."""
+    n = (1 << 32) + 1001
+    free, _ = torch.cuda.mem_get_info()
+    if free < 5 * n + (4 << 30):
+        pytest.skip("not enough HBM")
+    arena = torch.empty(n, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, n, 2029, 0)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    na.fixed_dev(arena, 1, 1, n, out)
+    torch.cuda.synchronize()
+    rng = np.random.default_rng(4)
+    idx = np.unique(np.concatenate([rng.integers(0, n, 2000), np.arange((1 << 32) - 70, (1 << 32) + 70),
+                                    np.arange(n - 70, n), [0, 1]]))
+    it = torch.from_numpy(idx.astype(np.int64)).to(dev)
+    data = arena[it].cpu().numpy()
+    exp = np.array([oracle.oracle_crc32_fast(np.array([b], dtype=np.uint8).ctypes.data, 1) for b in data],
+                   dtype=np.uint32)
+    assert np.array_equal(out[it].cpu().numpy().view(np.uint32), exp)
+    # the same frames as a variable-length batch (offsets and lengths built on the device: 51 GB).
+    # torch.arange over more than 2^32 elements returns zeros past index 1023 on this ROCm build of
+    # PyTorch, so the offsets are written in pieces of 2^30 and spot-checked before use.
+    if free >= 17 * n + (4 << 30):
+        off = torch.empty(n, dtype=torch.int64, device=dev)
+        for s0 in range(0, n, 1 << 30):
+            s1 = min(n, s0 + (1 << 30))
+            off[s0:s1] = torch.arange(s0, s1, dtype=torch.int64, device=dev)
+        assert np.array_equal(off[it].cpu().numpy(), idx.astype(np.int64))
+        ln = torch.ones(n, dtype=torch.int32, device=dev)
+        out.zero_()
+        na.batch_dev(arena, n, off, ln, out, n)
+        torch.cuda.synchronize()
+        assert np.array_equal(out[it].cpu().numpy().view(np.uint32), exp)
+        del off, ln
+    del arena, out
+    torch.cuda.empty_cache()
+
+
 def test_baseline_jumbo_size_properties(dev, oracle):
     """BASELINE configs[3]: 16 M x 9000-B frames (151 GB) in one launch of the interleaved segment
     kernel: sampled frames == oracle, two half launches == one launch, determinism."""
