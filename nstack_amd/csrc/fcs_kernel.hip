@@ -1631,7 +1631,10 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
                 if (!__any(zb > 16 * g)) break;
 #pragma unroll
                 for (int i = 4 * g; i < 4 * g + 4; i++) {
-                    w[i] = clear_low_bits(w[i], zf8 - 32 * i);
+                    // zf is a loop invariant: the compiler hoists this clamp (no v_med3 asm here)
+                    int t = zf8 - 32 * i;
+                    t = t < 0 ? 0 : (t > 32 ? 32 : t);
+                    w[i] &= (uint32_t)(0xFFFFFFFFull << t);
                 }
             }
             x0 = x0f;
