@@ -358,15 +358,6 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
             const int rc = take_counter(ds, st, p);
             if (rc) return rc;
         }
-    } else if (!fcs::fixed_tiny(p) && fcs::fixed_dmaseg(p)) {   // segmented LDS-DMA kernel: units of F frames
-        const uint32_t m = (len + fcs::kDmaCover - 1) / fcs::kDmaCover;
-        p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len / m);   // lane 15's mask bytes (the front masks fewer)
-        const uint64_t F = (m & 3u) == 0 ? 1 : ((m & 1u) == 0 ? 2 : 4);
-        const uint64_t units = (n + F - 1) / F, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
-        if (units >= kFixedDynMinUnitsPerWave * waves) {
-            const int rc = take_counter(ds, st, p);
-            if (rc) return rc;
-        }
     } else if (!fcs::fixed_tiny(p) && !fcs::fixed_single(p)) {
         // generic kernel: units of 4 frames (one per quarter-wave), dynamic for large batches
         const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);

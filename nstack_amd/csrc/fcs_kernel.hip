@@ -73,21 +73,12 @@ __device__ __forceinline__ uint32_t lds_rd(const uint8_t *lds, uint32_t byte_add
     return *reinterpret_cast<const uint32_t *>(lds + byte_addr);
 }
 
-// Per-lane table bases for step4. Default: 32 replicas (replica = lane & 31), base0 = r*4 (T3 at
-// +0, T2 at +128), base1 = 0x10000 | r*4 (T1, T0). FCS_LDS16 (measurement-only): one 256-B row per
-// byte value e holding table slot b (the table of word byte b, T_{3-b}) x 16 replicas at
-// e*256 + b*64 + (lane & 15)*4; lanes 16-31 of each half-wave rotate the chain word by 16 bits, so
-// their lookup k uses slot k ^ 2 and the 32 lanes of one LDS pass hit 32 distinct banks.
+// Per-lane table bases for step4: 32 replicas (replica = lane & 31), base0 = r*4 (T3 at +0, T2 at
+// +128), base1 = 0x10000 | r*4 (T1, T0).
 __device__ __forceinline__ void table_bases(int lane, uint32_t &base0, uint32_t &base1) {
-#ifdef FCS_LDS16
-    const uint32_t r = (uint32_t)(lane & 15) * 4u, G = (lane & 16) ? 2u : 0u;
-    base0 = r + G * 64u;
-    base1 = r + (2u - G) * 64u;
-#else
     const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
     base0 = r4;
     base1 = 0x10000u | r4;
-#endif
 }
 
 // One 4-byte step with the next word folded in: returns A_4(x) ^ wn, where
@@ -95,18 +86,6 @@ __device__ __forceinline__ void table_bases(int lane, uint32_t &base0, uint32_t 
 // base0 = r*4 (half 0: T3 at +0, T2 at +128), base1 = 0x10000 | r*4 (half 1: T1, T0).
 __device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32_t wn, uint32_t base0,
                                           uint32_t base1) {
-#ifdef FCS_LDS16   // measurement-only build: 64 KiB table set (see table_bases)
-    const uint32_t xr = __builtin_amdgcn_perm(x, x, (threadIdx.x & 16) ? 0x01000302u : 0x03020100u);
-    const uint32_t a0 = __builtin_amdgcn_perm(xr, base0, 0x0C0C0400u);
-    const uint32_t a1 = __builtin_amdgcn_perm(xr, base0, 0x0C0C0500u);
-    const uint32_t a2 = __builtin_amdgcn_perm(xr, base1, 0x0C0C0600u);
-    const uint32_t a3 = __builtin_amdgcn_perm(xr, base1, 0x0C0C0700u);
-    const uint32_t t3 = lds_rd(lds, a0);
-    const uint32_t t2 = lds_rd(lds, a1 + 64);
-    const uint32_t t1 = lds_rd(lds, a2);
-    const uint32_t t0 = lds_rd(lds, a3 + 64);
-    return xor3(xor3(t3, t2, t1), t0, wn);
-#else
     const uint32_t a0 = __builtin_amdgcn_perm(x, base0, 0x0C020400u);
     const uint32_t a1 = __builtin_amdgcn_perm(x, base0, 0x0C020500u);
     const uint32_t a2 = __builtin_amdgcn_perm(x, base1, 0x0C020600u);
@@ -119,7 +98,6 @@ __device__ __forceinline__ uint32_t step4(const uint8_t *lds, uint32_t x, uint32
     const uint32_t t1 = lds_rd(lds, a2);
     const uint32_t t0 = lds_rd(lds, a3 + 128);
     return xor3(xor3(t3, t2, t1), t0, wn);
-#endif
 #endif
 }
 
@@ -288,21 +266,6 @@ __device__ __forceinline__ void issue_chunk(const KParams &p, const Item &it, ui
         c.dlead = a < p.lo4 ? (int)((p.lo4 - a) >> 2) : 0;
         ab = a < p.lo4 ? p.lo4 : a;
     }
-#ifdef FCS_ABL_COALESCED   // measurement-only build: same bytes per quarter, coalesced 256-B rows
-    {
-        // quarter's segment start, 16-B aligned, clamped to the arena: every read stays in
-        // [lo16, sb + 1536) with sb + 1536 <= frame end (or lo16 + 1536 for idle/edge lanes).
-        const uint64_t seg0 = (uint64_t)cstart + (uint64_t)kChunkBytes * (j + 1) - kSegBytes;
-        const uint64_t lo16 = (p.lo4 + 15) & ~15ull;
-        uint64_t sb = seg0 & ~15ull;
-        sb = (need && sb >= lo16) ? sb : lo16;
-        const uint64_t cb = sb + 16 * (uint64_t)j;
-#pragma unroll
-        for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(cb + 256 * q);
-        c.x6 = gload<uint32_t>(cb + 4);
-        return;
-    }
-#endif
 #pragma unroll
     for (int q = 0; q < 6; q++) c.x[q] = gload<u32x4a4>(ab + 16 * q);
     c.x6 = gload<uint32_t>(ab + ((c.r || c.dlead) ? 96 : 92));
@@ -513,13 +476,6 @@ template <int NT>
 __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
     const int tid = threadIdx.x;
     // data: 8192 x 16 B; each b128 store = 4 replicas of one entry
-#ifdef FCS_LDS16
-    for (int i = tid; i < 4096; i += NT) {   // row e = i >> 4; 16-B store q = i & 15 -> slot q >> 2
-        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)];
-        u32x4 vv = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
-    }
-#else
     for (int i = tid; i < 8192; i += NT) {
         const int h = i >> 12;            // 64 KiB half
         const int b = (i >> 4) & 255;     // entry
@@ -530,7 +486,6 @@ __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
     }
-#endif
     const uint32_t *src = p.blob + kBlobLane;
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsLane);
     for (int i = tid; i < (int)(kBlobFlat - kBlobLane); i += NT) dst[i] = src[i];
@@ -541,13 +496,6 @@ __device__ __forceinline__ void stage_tables(const KParams &p, uint8_t *lds) {
 // tables C_c in place of the per-lane tables.
 __device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds) {
     const int tid = threadIdx.x;
-#ifdef FCS_LDS16
-    for (int i = tid; i < 4096; i += kWgThreads) {
-        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 15) >> 2)) + (i >> 4)];
-        u32x4 vv = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
-    }
-#else
     for (int i = tid; i < 8192; i += kWgThreads) {
         const int h = i >> 12, b = (i >> 4) & 255, odd = (i >> 3) & 1;
         const int k = h == 0 ? (odd ? 2 : 3) : (odd ? 0 : 1);
@@ -555,7 +503,6 @@ __device__ __forceinline__ void stage_tables_flat(const KParams &p, uint8_t *lds
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + kLdsData + (uint32_t)i * 16) = vv;
     }
-#endif
     uint32_t *dst = reinterpret_cast<uint32_t *>(lds + kLdsJump);
     for (int i = tid; i < (int)(kBlobFlat - kBlobJump); i += kWgThreads) dst[i] = p.blob[kBlobJump + i];
     uint32_t *fl = reinterpret_cast<uint32_t *>(lds + kLdsFlat);
@@ -867,7 +814,7 @@ constexpr uint32_t kDmaInvHole = kDmaMergeHole + 4 * 5;             // 3 holes: 
 constexpr uint32_t kDmaBad = dma_hole(kDmaInvHole + 3);            // 16 x 8 B
 constexpr uint32_t kDmaRing = 65536;                                // slots start after the tables
 constexpr int kDmaWaves = kDmaWgThreads / 64;
-constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)kDmaWaves * (kDmaPair ? 2u : 1u) * kDmaItemBytes;
+constexpr uint32_t kDmaLdsBytes = kDmaRing + (uint32_t)kDmaWaves * kDmaItemBytes;
 static_assert(kDmaLdsBytes <= 163840, "LDS per CU");
 static_assert(kDmaChains - 1 <= 5, "merge holes");
 #ifndef FCS_DMA_AUX   // cache policy of the slot DMA (2 = nt; measurement-only override)
@@ -999,7 +946,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     const int c = lane & (kGroup - 1);     // chunk index back from the frame end
     const int g = lane >> 4;               // frame of the item
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)wave * (kDmaPair ? 2u : 1u) * kDmaItemBytes;
+    const uint8_t *slot0 = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
     const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
     const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
     const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
@@ -1044,89 +991,6 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         const uint64_t S = item_start(i), sn = slot_src(S);
         dma_item(slot, sn, lane, item_need(S, sn));
     };
-    // this lane's window of item i, realigned and front-masked (d: 25 raw dwords from the slot)
-    auto read_window = [&](const uint8_t *slot, uint64_t i, uint32_t (&d)[kChunkWords + 1]) -> uint32_t {
-        const uint64_t S = item_start(i), src = slot_src(S);
-        const int64_t x = (int64_t)(S - src) + klane;   // window start within the slot (>= -28)
-        const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
-#pragma unroll
-        for (int q = 0; q < kChunkWords; q++) d[q] = wp[q];
-        // the 25th dword matters only when r != 0; then it lies inside the slot. Clamped so the
-        // last slot in LDS is never read past its end.
-        const uint64_t a24 = (uint64_t)(wp + kChunkWords), lim = (uint64_t)(slot + kDmaItemBytes - 4);
-        d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
-        return (uint32_t)x & 3u;
-    };
-    auto realign = [&](const uint32_t (&d)[kChunkWords + 1], uint32_t r, uint32_t (&w)[kChunkWords]) {
-#pragma unroll
-        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
-#pragma unroll
-        for (int i = 0; i < MW; i++) w[i] &= m[i];
-    };
-
-    if constexpr (kDmaPair) {
-        // ---- two items per wave at once (8 waves per CU, one slot each): half the DMA streams
-        //      of 16 one-slot waves with the same bytes in flight, and both items' chains
-        //      interleaved (2 kDmaChains independent chains per lane) ----
-        const uint8_t *slot1 = slot0 + kDmaItemBytes;
-        uint64_t ia = D.first();
-        uint64_t ib = ia != kEnd ? D.next(ia) : kEnd;
-        if (ia != kEnd) dma_of(slot0, ia);
-        if (ib != kEnd) dma_of(slot1, ib);
-        while (ia != kEnd) {   // wave-uniform
-            const bool hb = ib != kEnd;
-            uint32_t da[kChunkWords + 1], db[kChunkWords + 1];
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): both slots have landed
-            const uint32_t ra = read_window(slot0, ia, da);
-            const uint32_t rb = read_window(slot1, hb ? ib : ia, db);
-            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): both slots are free for the next DMAs
-            uint64_t na = kEnd, nb = kEnd;
-            if (hb) {
-                na = D.next(ib);
-                if (na != kEnd) nb = D.next(na);
-            }
-            if (na != kEnd) dma_of(slot0, na);
-            if (nb != kEnd) dma_of(slot1, nb);
-            if (STREAM) {
-                uint32_t acc = ra ^ rb;
-#pragma unroll
-                for (int q = 0; q <= kChunkWords; q++) acc ^= da[q] ^ db[q];
-                if (acc == 0x9E3779B9u) p.out[0] = acc;   // keeps the reads live; practically never stores
-            } else {
-                uint32_t wa[kChunkWords], wb[kChunkWords];
-                realign(da, ra, wa);
-                realign(db, rb, wb);
-                constexpr int CL = kDmaChainWords;
-                uint32_t xa[kDmaChains], xb[kDmaChains];
-#pragma unroll
-                for (int hh = 0; hh < kDmaChains; hh++) {
-                    xa[hh] = wa[hh * CL] ^ (hh == 0 ? x0 : 0u);
-                    xb[hh] = wb[hh * CL] ^ (hh == 0 ? x0 : 0u);
-                }
-#pragma unroll
-                for (int i = 0; i < CL; i++)
-#pragma unroll
-                    for (int hh = 0; hh < kDmaChains; hh++) {
-                        xa[hh] = step4_l8(lds, xa[hh], i < CL - 1 ? wa[hh * CL + i + 1] : 0u, B, SEL);
-                        xb[hh] = step4_l8(lds, xb[hh], i < CL - 1 ? wb[hh * CL + i + 1] : 0u, B, SEL);
-                    }
-                uint32_t ma = xa[kDmaChains - 1], mb = xb[kDmaChains - 1];
-#pragma unroll
-                for (int hh = 0; hh < kDmaChains - 1; hh++) {
-                    ma = merge_shift_dma(lds, kDmaChains - 2 - hh, xa[hh], ma);
-                    mb = merge_shift_dma(lds, kDmaChains - 2 - hh, xb[hh], mb);
-                }
-                const uint32_t va = row_xor(lane_shift_dma(lds, ma, lanebase));
-                const uint32_t vb = row_xor(lane_shift_dma(lds, mb, lanebase));
-                emit<kDmaBad>(p, lds, c == kGroup - 1 && 4 * ia + g < p.n, 4 * ia + g, ~va);
-                emit<kDmaBad>(p, lds, hb && c == kGroup - 1 && 4 * ib + g < p.n, 4 * ib + g, ~vb);
-            }
-            ia = na;
-            ib = nb;
-        }
-        flush_bad<kDmaBad>(p, lds);
-        return;
-    }
 
     uint64_t it = D.first();
     if (it != kEnd) dma_of(slot0, it);
@@ -1230,265 +1094,6 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     flush_bad<kDmaBad>(p, lds);
 }
 
-#ifdef FCS_DMASEG
-// ---------------------------------------------------------------------------------------------
-// MEASUREMENT-ONLY (-DFCS_DMASEG -DFCS_NO_SEGIL; superseded by fcs_segil_kernel below, DESIGN.md
-// §3.2c). Fixed length over 1524 B (jumbo frames, e.g. 9000 B), staged through LDS by DMA
-// (fcs_dmaseg_kernel; selected by fixed_dmaseg(): packed frames, stride - len <= 8, and a
-// split into m = ceil(len / 1524) segments of Ls = floor(len / m) >= 1496 bytes, the front one
-// Lf = Ls + len mod m <= 1524 bytes).
-// Every segment is then shaped like a frame of fcs_dma_kernel: its 16 lane windows end e_c bytes
-// before the segment end, and only lane 15 masks the 1524 - Ls (front: 1524 - Lf) cover bytes
-// before the segment start (loop-invariant masks); the front segment's lane 15 injects INV. The
-// frame's register is XOR_s A_{Ls s}(v_s), s = 0 for the frame's last segment.
-// The segments of a unit of F frames (F m a multiple of 4, F = 1, 2 or 4) form a stream; a wave's
-// item is 4 consecutive stream segments, one per quarter-wave, in one 6 KiB slot DMA (consecutive
-// segments of packed frames are contiguous). Quarter q places its segment value in its frame with
-// one table shift, A_{Ls s} (the place tables for s = 1 .. m - 1: s <= 4 from the blob, the rest
-// composed at staging); a frame's register is then the plain XOR of its placed segments, summed
-// over the items by wave-uniform code on the four quarter values (the frame open at the item start
-// carries its partial XOR C). Units come from the dispenser, so a frame's segments are all
-// processed by one wave, in order.
-// An earlier form advanced each quarter only over the segments of its frame that follow in the
-// item (A_{Ls t}, t <= 3) and the carried register by A_{Ls k}: a second table shift per item,
-// 1.7 % slower at 9000 B.
-// A first version cut frames into 1524-B segments from the frame end (one short front segment,
-// lanes above its first byte zeroed, a partial lane masked per item): the per-item mask code
-// broke the chain block's scheduling and ran 2-12 % slower than the register-load kernel.
-// ---------------------------------------------------------------------------------------------
-constexpr uint32_t kDmaSegJumpHole = kDmaInvHole + 4;   // 4 holes per table: A_{Ls k}, k = 1 .. m - 1
-static_assert(kDmaSegJumpHole + 4 * (kDmaSegMaxSegs - 1) <= 256, "place tables overrun the table holes");
-static_assert(FCS_DMASEG_MAX_SEGS <= kDmaSegMaxSegs, "segment limit");
-
-// A_{Ls k}(s) for k = 1 .. m - 1; k = 0 returns s. Nibble table t of A_{Ls k} at hole
-// kDmaSegJumpHole + 4 (k - 1) + t / 2, +64 B for odd t.
-__device__ __forceinline__ uint32_t seg_jump(const uint8_t *lds, uint32_t k, uint32_t s) {
-    uint32_t r[8];
-    const uint32_t kk = k ? k - 1u : 0u;
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
-        const uint32_t base = dma_hole(kDmaSegJumpHole + 4u * kk + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1);
-        r[t] = lds_rd(lds, (sh & 0x3Cu) | base);
-    }
-    const uint32_t v = xor9(r, 0u);
-    return k ? v : s;
-}
-
-// MW: words lane 15's masks can touch (host-selected: 2 when 1524 - Lf <= 8, else kSingleMaskWords).
-template <int MW>
-__global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dmaseg_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaLdsBytes];
-    const int tid = threadIdx.x;
-    // ---- frame geometry (wave-uniform) ----
-    const uint32_t L = p.flen;
-    const uint32_t m = (L + kDmaCover - 1) / kDmaCover;                    // segments per frame, >= 2
-    const uint32_t F = (m & 3u) == 0 ? 1u : ((m & 1u) == 0 ? 2u : 4u);     // frames per unit
-    const uint32_t Ls = L / m, Lf = L - Ls * (m - 1);                        // segment, front segment
-
-    stage_dma_tables(p, lds, tid);
-    for (int i = tid; i < 4 * 128; i += kDmaWgThreads) {   // place tables A_{Ls k}, k = 1..4, from the blob
-        const int k = i >> 7, t = (i >> 4) & 7, e = i & 15;
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaSegJumpHole + 4u * (uint32_t)k + (uint32_t)(t >> 1)) +
-                                      64u * (uint32_t)(t & 1) + 4u * (uint32_t)e) =
-            p.blob[kBlobSegJump + (Ls - kDmaMinLen) * 512u + (uint32_t)i];
-    }
-    // A_{Ls k} for k = 5 .. m - 1: composed here as A_{Ls 4} o A_{Ls (k - 4)}, one k at a time
-    for (uint32_t k = 5; k < m; k++) {
-        __syncthreads();
-        if (tid < 128) {
-            const uint32_t t = (uint32_t)tid >> 4, e = (uint32_t)tid & 15u;
-            const uint32_t at = 64u * (t & 1u) + 4u * e;
-            const uint32_t prev = lds_rd(lds, dma_hole(kDmaSegJumpHole + 4u * (k - 5u) + (t >> 1)) + at);
-            const uint32_t v = seg_jump(lds, 4u, prev);
-            *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaSegJumpHole + 4u * (k - 1u) + (t >> 1)) + at) = v;
-        }
-    }
-    init_bad<kDmaBad>(lds);
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const int c = lane & (kGroup - 1);        // window index back from the segment end
-    const uint32_t q = (uint32_t)lane >> 4;   // quarter: stream segment 4 j + q of the item
-    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kDmaItemBytes;
-    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
-    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
-    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
-                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
-    const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
-    const uint32_t ec = dma_end_off(c);
-
-    // loop invariants: lane 15 masks the cover bytes before its segment (front and other
-    // segments), lanes 3/7/11 their overlap word; INV start of the front segment's lane 15
-    const int zn = (c == kGroup - 1) ? (int)(kDmaCover - Ls) : (dma_short_lane(c) ? 4 : 0);
-    const int zf = (c == kGroup - 1) ? (int)(kDmaCover - Lf) : (dma_short_lane(c) ? 4 : 0);
-    static_assert(MW >= 1 && MW <= kSingleMaskWords, "mask words");
-    uint32_t mn[MW], mf[MW];
-#pragma unroll
-    for (int i = 0; i < MW; i++) {
-        int t = zn - 4 * i, u = zf - 4 * i;
-        t = t < 0 ? 0 : (t > 4 ? 4 : t);
-        u = u < 0 ? 0 : (u > 4 ? 4 : u);
-        mn[i] = (uint32_t)(0xFFFFFFFFull << (8 * t));
-        mf[i] = (uint32_t)(0xFFFFFFFFull << (8 * u));
-    }
-    const uint32_t x0f = (c == kGroup - 1)
-                             ? lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zf / 32u) + (uint32_t)(zf % 32) * 4u)
-                             : 0u;
-
-    const uint64_t lo16 = p.lo4 & ~15ull;
-    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start inside the arena
-    auto slot_src = [&](uint64_t S) {
-        const uint64_t a = S & ~15ull;
-        return a < lo16 ? lo16 : (a > smax ? smax : a);
-    };
-    constexpr uint64_t kEnd = Dispenser::kEnd;
-    const uint64_t units = (p.n + F - 1) / F;
-    const uint32_t per_unit = F * m / 4;                                    // items of a full unit
-    const uint32_t cmax = per_unit >= 64 ? 1u : 64u / per_unit;
-    Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kDmaWaves, (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave,
-                lane, 100, 1, cmax);
-
-    // Item state, wave-uniform: unit u (frames u F ..), item j of J, and the stream position of
-    // quarter 0: frame fi0 of the unit, segment r0 counted from the frame's front (s = m - 1 - r).
-    struct It {
-        uint64_t u, fb0, src;   // fb0: start of quarter 0's frame; src: slot start
-        uint32_t j, J, Fu, fi0, r0, need;
-    };
-    auto seg_end = [&](uint32_t r) { return (uint64_t)Lf + (uint64_t)Ls * r; };   // from the frame start
-    auto place = [&](It &t) {
-        t.fb0 = p.base + (t.u * F + t.fi0) * p.stride;
-        t.src = slot_src(t.fb0 + (t.r0 ? seg_end(t.r0 - 1) : 0));
-        const uint32_t last = 4 * t.j + 3 < t.Fu * m ? 3u : t.Fu * m - 1u - 4 * t.j;   // last active quarter
-        uint32_t fi = 0, r = t.r0 + last;
-        while (r >= m) {
-            r -= m;
-            fi++;
-        }
-        const uint64_t nb = t.fb0 + fi * p.stride + seg_end(r) + 4 - t.src;
-        t.need = (uint32_t)(nb < (uint64_t)kDmaItemBytes ? nb : (uint64_t)kDmaItemBytes);
-    };
-    auto start_unit = [&](It &t, uint64_t u) {
-        t.u = u;
-        t.j = 0;
-        t.fi0 = 0;
-        t.r0 = 0;
-        const uint64_t left = p.n - u * F;
-        t.Fu = left < F ? (uint32_t)left : F;
-        t.J = (t.Fu * m + 3u) / 4u;
-        place(t);
-    };
-
-    It cur{};
-    bool live = false;
-    {
-        const uint64_t u0 = D.first();
-        if (u0 != kEnd) {
-            start_unit(cur, u0);
-            live = true;
-            dma_item<true>(slot, cur.src, lane, cur.need);
-        }
-    }
-    uint32_t C = 0;   // register of the frame open at the item start (wave-uniform)
-    while (live) {
-        // this lane's segment: quarter q = stream position (fi0, r0) + q
-        uint32_t dfi = 0, r = cur.r0 + q;
-        while (r >= m) {
-            r -= m;
-            dfi++;
-        }
-        const bool act = cur.fi0 + dfi < cur.Fu;
-        const uint32_t s = m - 1u - r;
-        const bool front = r == 0;
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot DMA has landed
-        const int64_t x = act ? (int64_t)(cur.fb0 + dfi * p.stride + seg_end(r) - cur.src) - (int64_t)ec - kChunkBytes : 0;
-        const uint32_t ra = (uint32_t)x & 3u;
-        const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
-        uint32_t d[kChunkWords + 1];
-#pragma unroll
-        for (int i = 0; i < kChunkWords; i++) d[i] = wp[i];
-        {
-            const uint64_t a24 = (uint64_t)(wp + kChunkWords), lim = (uint64_t)(slot + kDmaItemBytes - 4);
-            d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
-        }
-        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
-
-        // ---- the next item (same unit, or the dispenser's next unit): its DMA lands meanwhile ----
-        It nxt = cur;
-        bool nlive = true;
-        if (cur.j + 1 < cur.J) {
-            nxt.j++;
-            nxt.r0 += 4;
-            while (nxt.r0 >= m) {
-                nxt.r0 -= m;
-                nxt.fi0++;
-            }
-            place(nxt);
-        } else {
-            const uint64_t un = D.next(cur.u);
-            nlive = un != kEnd;
-            if (nlive) start_unit(nxt, un);
-        }
-        if (nlive) dma_item<true>(slot, nxt.src, lane, nxt.need);
-
-        // ---- this item's segment values ----
-        uint32_t w[kChunkWords];
-#pragma unroll
-        for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ra);
-#pragma unroll
-        for (int i = 0; i < MW; i++) w[i] &= front ? mf[i] : mn[i];
-        constexpr int CL = kDmaChainWords;
-        uint32_t xs[kDmaChains];
-#pragma unroll
-        for (int hh = 0; hh < kDmaChains; hh++) xs[hh] = w[hh * CL] ^ (hh == 0 && front ? x0f : 0u);
-#pragma unroll
-        for (int i = 0; i < CL; i++)
-#pragma unroll
-            for (int hh = 0; hh < kDmaChains; hh++)
-                xs[hh] = step4_l8(lds, xs[hh], i < CL - 1 ? w[hh * CL + i + 1] : 0u, B, SEL);
-        uint32_t mv = xs[kDmaChains - 1];
-#pragma unroll
-        for (int hh = 0; hh < kDmaChains - 1; hh++) mv = merge_shift_dma(lds, kDmaChains - 2 - hh, xs[hh], mv);
-        uint32_t v = lane_shift_dma(lds, mv, lanebase);
-        v = act ? v : 0u;
-        v = row_xor(v);
-        // placed in its frame: A_{Ls s}, s segments before the frame end
-#ifdef FCS_SEG_ABL_NOJUMP   // measurement-only: no placement shift (wrong FCS)
-        const uint32_t uq = v ^ s;
-#else
-        const uint32_t uq = seg_jump(lds, act ? s : 0u, v);
-#endif
-
-#ifdef FCS_SEG_ABL_NOCOMB   // measurement-only: each quarter's value stored as is (wrong FCS)
-        emit<kDmaBad>(p, lds, c == 0 && act, cur.u * F + cur.fi0 + dfi, ~uq);
-        cur = nxt;
-        live = nlive;
-        continue;
-#endif
-        // ---- per-frame accumulation (wave-uniform) ----
-        uint32_t acc = 0;
-        if (cur.r0 != 0) acc = C;   // the frame open at the item start: its placed segments so far
-        uint32_t rq = cur.r0, fq = cur.fi0;
-#pragma unroll
-        for (int qq = 0; qq < 4; qq++) {
-            if (fq >= cur.Fu) break;
-            const uint32_t vq = (uint32_t)__builtin_amdgcn_readlane((int)uq, 16 * qq);
-            acc = rq == 0 ? vq : (acc ^ vq);
-            if (rq == m - 1u) emit<kDmaBad>(p, lds, lane == 0, cur.u * F + fq, ~acc);
-            if (++rq == m) {
-                rq = 0;
-                fq++;
-            }
-        }
-        C = acc;
-
-        cur = nxt;
-        live = nlive;
-    }
-    flush_bad<kDmaBad>(p, lds);
-}
-#endif  // FCS_DMASEG
 
 // ---------------------------------------------------------------------------------------------
 // Fixed length over 1524 B, any stride: frame-interleaved segments staged through LDS by DMA
@@ -1665,17 +1270,8 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Variable-length frames (IMIX-shaped batches): windowed class scheduling. Superseded by
-// fcs_flat_kernel below (+16 % on IMIX); kept as the measurement baseline (-DFCS_VAR_HALFUNIT).
-// A wave owns windows of 64 consecutive frames (frame i of a window <-> lane i for metadata).
-// The window's frames are split by length into classes that use lanes differently:
-//   small  (len <= 96):  the owning lane alone processes the frame as one chunk (chunk 0, no
-//                        lane shift, no reduction);
-//   medium (len <= 768): 8 lanes per frame (chunk c <- lane & 7), 8 frames per item; lanes 8..15
-//                        of a row used the lane tables of chunks 8..15, fixed by one A_{-768};
-//   big    (len > 768):  16 lanes per frame (as the fixed kernels), 4 frames per item,
-//                        1536-B segments accumulated with A_1536.
-// All classes read the same ~64 frames of the arena close together in time (L2-local).
+// Variable-length frames: a lane's chunk loads and register value (fcs_flat_kernel below, and the
+// segment loop of its frames over 1536 B).
 // ---------------------------------------------------------------------------------------------
 template <bool TINY>
 __device__ __forceinline__ void issue_any(const KParams &p, int64_t cstart, bool need, Chunk &c) {
@@ -1764,135 +1360,6 @@ __device__ __forceinline__ int clamp_zr(int64_t z) {
     return z < -1 ? -1 : (z > kChunkBytes ? kChunkBytes : (int)z);
 }
 
-// One half-unit item of the windowed var kernel (fcs_var_kernel): 8 half-units of 8 lanes.
-// unit_issue resolves this lane's frame and chunk and issues its loads; unit_finish computes the
-// chunk, reduces each frame's lanes and stores.
-struct UnitItem {
-    Chunk ch;
-    uint32_t meta;   // zr + 1 (bits 0-7) | valid (8) | full row (9) | small lane (10) | empty frame (11) |
-                     // window lane of this lane's frame (16-21)
-};
-
-template <bool TINY>
-__device__ __forceinline__ void unit_issue(const KParams &p, const uint8_t *lists, uint32_t Ehi, uint32_t Elo,
-                                           uint32_t L, uint32_t nf, uint32_t nfm, uint32_t nu, uint32_t ns,
-                                           uint32_t t, int lane, int j, UnitItem &it) {
-    const uint32_t u = t + (uint32_t)(lane >> 3);
-    const bool isfull = u < 2 * nf;   // same for both halves of a row
-    const bool issmall = u >= nfm;
-    const uint32_t si = (u - nfm) * 8 + (uint32_t)(lane & 7);   // small frame rank
-    const bool valid = issmall ? (u < nu && si < ns) : u < nu;
-    const int src = valid ? (int)lists[isfull ? 64 + (u >> 1) : (issmall ? 192 + si : u - 2 * nf)] : 0;
-    const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
-    const uint32_t Lg = (uint32_t)__shfl((int)L, src);
-    const int c = isfull ? j : (issmall ? 0 : (lane & 7));   // chunk index back from the frame end
-    const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (c + 1);
-    const int zr = clamp_zr((int64_t)(Eg - Lg) - cstart);
-    issue_any<TINY>(p, cstart, valid && zr < kChunkBytes, it.ch);
-    it.meta = (uint32_t)((valid ? zr : kChunkBytes) + 1) | (valid ? 1u << 8 : 0u) | (isfull ? 1u << 9 : 0u) |
-              (issmall ? 1u << 10 : 0u) | (Lg == 0 ? 1u << 11 : 0u) | ((uint32_t)src << 16);
-}
-
-template <bool TINY>
-__device__ __forceinline__ void unit_finish(const KParams &p, const uint8_t *lds, const UnitItem &it, uint64_t w0,
-                                            int lane, int j, uint32_t base0, uint32_t base1, uint32_t lanebase) {
-    const bool valid = it.meta & (1u << 8), isfull = it.meta & (1u << 9), issmall = it.meta & (1u << 10);
-    const int zr = (int)(it.meta & 0xFFu) - 1;
-    const uint32_t own = chunk_value<TINY>(lds, it.ch, zr, zr, valid ? inv_start(lds, zr) : 0u, base0, base1);
-    uint32_t v = lane_shift(lds, own, lanebase);   // A_{96 j}
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
-    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // half_mirror
-    // full rows join their halves (row_mirror); medium upper halves used A_{96(c+8)}: undo A_768
-    const uint32_t joined = v ^ (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x140, 0xF, 0xF, false);
-    const uint32_t fixed = uniform_shift<kLdsM768>(lds, v, 0u);
-    v = isfull ? joined : (issmall ? own : (j >= 8 ? fixed : v));
-    emit(p, lds, valid && (isfull ? j == 15 : (issmall || (lane & 7) == 7)), w0 + ((it.meta >> 16) & 63u),
-         (it.meta & (1u << 11)) ? 0u : ~v);
-}
-
-template <bool TINY>
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_var_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
-    stage_tables<kWgThreads>(p, lds);
-    init_bad(lds);
-
-    const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-    const int j = lane & (kGroup - 1);
-    const uint32_t r4 = (uint32_t)(lane & 31) * 4u;
-    const uint32_t lanebase = kLdsLane | r4;
-    uint32_t base0, base1;
-    table_bases(lane, base0, base1);
-    uint8_t *lists = lds + kLdsWave + wave * kLdsWaveBytes;   // medium | full | multi | small, 64 each
-    const uint64_t GW = (uint64_t)gridDim.x * (kWgThreads / 64);
-
-    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kWgThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
-        // ---- window metadata: lane i <-> frame w0 + i ----
-        const uint64_t f = w0 + lane;
-        const bool act = f < p.n;
-        const uint32_t L = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
-        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;   // off == null: slots of p.stride
-        const bool small = act && L <= (uint32_t)kChunkBytes;
-        const bool med = act && !small && L <= 8u * kChunkBytes;
-        const bool full = act && L > 8u * kChunkBytes && L <= (uint32_t)kSegBytes;
-        const bool multi = act && L > (uint32_t)kSegBytes;
-        const uint64_t mmask = __ballot(med), fmask = __ballot(full), xmask = __ballot(multi);
-        const uint32_t nm = (uint32_t)__popcll(mmask), nf = (uint32_t)__popcll(fmask), nx = (uint32_t)__popcll(xmask);
-        const uint32_t rm = __builtin_amdgcn_mbcnt_hi((uint32_t)(mmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mmask, 0u));
-        const uint32_t rf = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
-        const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
-        if (med) lists[rm] = (uint8_t)lane;
-        if (full) lists[64 + rf] = (uint8_t)lane;
-        if (multi) lists[128 + rx] = (uint8_t)lane;
-        const uint64_t smask = __ballot(small);
-        const uint32_t ns = (uint32_t)__popcll(smask);
-        const uint32_t rs = __builtin_amdgcn_mbcnt_hi((uint32_t)(smask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smask, 0u));
-        if (small) lists[192 + rs] = (uint8_t)lane;
-        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
-
-        // ---- half-units (8 lanes each, 8 per item), in this order:
-        //      full frame (769..1536 B): two halves of one 16-lane row (chunk index = j);
-        //      medium frame (97..768 B): one half (chunk index = lane & 7);
-        //      small frames (<= 96 B): eight per half, one lane each, a single chunk.
-        //      Full frames come first, so their rows are aligned. ----
-        const uint32_t nfm = 2 * nf + nm;
-        const uint32_t nu = nfm + (ns + 7) / 8;
-        // one item at a time: a second item in flight measured 5-7 % slower here (the var loop is
-        // issue-bound, and the extra registers cost waits), unlike the fixed kernels
-        for (uint32_t t = 0; t < nu; t += 8) {
-            UnitItem A;
-            unit_issue<TINY>(p, lists, Ehi, Elo, L, nf, nfm, nu, ns, t, lane, j, A);
-            unit_finish<TINY>(p, lds, A, w0, lane, j, base0, base1, lanebase);
-        }
-
-        // ---- multi-segment frames (> 1536 B): 16 lanes each, 4 per item, segment by segment ----
-        for (uint32_t t = 0; t < nx; t += 4) {
-            const uint32_t rank = t + (uint32_t)(lane >> 4);
-            const bool valid = rank < nx;
-            const int src = valid ? (int)lists[128 + rank] : 0;
-            const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
-            const uint32_t Lq = (uint32_t)__shfl((int)L, src);
-            const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
-            uint32_t s = 0;
-            for (uint32_t k = 0; __any(k < m); k++) {
-                const bool on = k < m;
-                const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - k) -
-                                       (int64_t)kChunkBytes * (j + 1);
-                const int zr = (on && k == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
-                Chunk c;
-                issue_any<TINY>(p, cstart, on && zr < kChunkBytes, c);
-                const uint32_t r = chunk_value<TINY>(lds, c, zr, on ? zr : 0, (on && k == 0) ? inv_start(lds, zr) : 0u,
-                                                     base0, base1);
-                s = on ? (k == 0 ? r : uniform_shift<kLdsJump>(lds, s, r)) : s;
-            }
-            uint32_t v = lane_shift(lds, s, lanebase);
-            v = row_xor(v);
-            emit(p, lds, valid && j == 15, w0 + (uint32_t)src, Lq ? ~v : 0u);
-        }
-    }
-    flush_bad(p, lds);
-}
 
 // ---------------------------------------------------------------------------------------------
 // Variable-length frames, flat chunk stream (fcs_flat_kernel).
@@ -2020,47 +1487,11 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 #endif
             if (it.valid && v) atomicXor(&acc[it.src], v);
         };
-#ifdef FCS_FLAT_PIPE   // measurement-only build: the next item's loads in flight during this one
-        if (K) {
-            FlatItem A, B;
-            prep(0, 1, A);
-            uint32_t g0 = 64, tag = 2;
-            while (true) {
-                if (g0 >= K) { finish(A); break; }
-                prep(g0, tag, B);
-                finish(A);
-                g0 += 64; tag++;
-                if (g0 >= K) { finish(B); break; }
-                prep(g0, tag, A);
-                finish(B);
-                g0 += 64; tag++;
-            }
-        }
-#elif defined(FCS_FLAT_DEAL_AHEAD)   // measurement-only: the next item dealt while this item's loads fly
-        if (K) {
-            FlatItem it, nx;
-            deal(0, 1, it);
-            for (uint32_t g0 = 0, tag = 1; g0 < K; g0 += 64, tag++) {
-                issue(it);
-                const bool more = g0 + 64 < K;
-                if (more) deal(g0 + 64, tag + 1, nx);
-                finish(it);
-                if (more) {
-                    it.src = nx.src;
-                    it.zr = nx.zr;
-                    it.c = nx.c;
-                    it.valid = nx.valid;
-                    it.cstart = nx.cstart;
-                }
-            }
-        }
-#else
         for (uint32_t g0 = 0, tag = 1; g0 < K; g0 += 64, tag++) {
             FlatItem it;
             prep(g0, tag, it);
             finish(it);
         }
-#endif
 
         // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment ----
         const uint64_t xmask = __ballot(multi);
@@ -2104,780 +1535,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     flush_bad(p, lds);
 }
 
-// ---------------------------------------------------------------------------------------------
-// Shared by the LDS-DMA variable-length kernels (fcs_span_kernel, and the measurement-only
-// fcs_flatdma_kernel): the 32 KiB slice tables of fcs_dma_kernel and, in the row holes, the
-// c-indexed shift tables A_{96c} (nibble t of table c at hole 4c + t/2, +64 B for odd t), the A_48
-// merge table and INV of fcs_dma_kernel, A_1536 for frames over 1536 B, and each wave's window
-// scratch (accumulators, marks, frame lists).
-// ---------------------------------------------------------------------------------------------
-constexpr uint32_t kFdJumpHole = 152;                  // A_1536: 4 holes
-constexpr uint32_t kFdWaveHole = 160;                  // 4 holes per wave: acc[0..31], acc[32..63], marks | list, multi list
-static_assert(kDmaInvHole + 4 <= kFdJumpHole && kFdWaveHole + 4 * 16 <= 256, "holes");
 
-__device__ __forceinline__ uint32_t fd_acc_addr(uint32_t wave, uint32_t i) {
-    return dma_hole(kFdWaveHole + 4u * wave + (i >> 5)) + (i & 31u) * 4u;
-}
 
-// A_{96c}(s), c = 0..15, from the c-indexed hole tables.
-__device__ __forceinline__ uint32_t fd_chunk_shift(const uint8_t *lds, uint32_t s, uint32_t c) {
-    uint32_t r[8];
-    const uint32_t base = dma_hole(4u * c);
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
-        r[t] = lds_rd(lds, base + (sh & 0x3Cu) + 256u * (uint32_t)(t >> 1) + 64u * (uint32_t)(t & 1));
-    }
-    return xor9(r, 0u);
-}
 
-// A_1536(s) ^ extra from its hole table.
-__device__ __forceinline__ uint32_t fd_jump(const uint8_t *lds, uint32_t s, uint32_t extra) {
-    uint32_t r[8];
-#pragma unroll
-    for (int t = 0; t < 8; t++) {
-        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
-        r[t] = lds_rd(lds, dma_hole(kFdJumpHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) + (sh & 0x3Cu));
-    }
-    return xor9(r, extra);
-}
-
-__device__ __forceinline__ uint32_t fd_inv(const uint8_t *lds, int zr) {
-    const int zi = zr < 0 ? 0 : (zr > kChunkBytes - 1 ? kChunkBytes - 1 : zr);
-    const uint32_t iv = lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zi / 32u) + (uint32_t)(zi % 32) * 4u);
-    return (zr >= 0 && zr < kChunkBytes) ? iv : 0u;
-}
-
-// The words of a register-loaded chunk, realigned to its start (arena edge undone).
-__device__ __forceinline__ void fd_chunk_words(const Chunk &c, uint32_t (&w)[kChunkWords]) {
-    uint32_t d[kChunkWords + 1];
-#pragma unroll
-    for (int q = 0; q < 6; q++) {
-        d[4 * q] = c.x[q].x;
-        d[4 * q + 1] = c.x[q].y;
-        d[4 * q + 2] = c.x[q].z;
-        d[4 * q + 3] = c.x[q].w;
-    }
-    d[kChunkWords] = c.x6;
-    if (__any(c.dlead)) shift_up(d, c.dlead);
-#pragma unroll
-    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], c.r);
-}
-
-// A chunk's register before its shift: bytes before the frame start masked (groups of 4 words up
-// to the wave's largest claim zb, as chunk_value), x0 injected, two 12-word chains on the 32 KiB
-// tables, A_48 merge.
-__device__ __forceinline__ uint32_t fd_value(const uint8_t *lds, uint32_t (&w)[kChunkWords], int zr, int zb, uint32_t x0,
-                                             const uint32_t (&B)[4], const uint32_t (&SEL)[4]) {
-    const int zr8 = 8 * zr;
-#pragma unroll
-    for (int g = 0; g < kChunkWords / 4; g++) {
-        if (!__any(zb > 16 * g)) break;
-#pragma unroll
-        for (int i = 4 * g; i < 4 * g + 4; i++) {
-            w[i] = clear_low_bits(w[i], zr8 - 32 * i);
-        }
-    }
-    uint32_t xa = x0 ^ w[0], xb = w[12];
-#pragma unroll
-    for (int i = 0; i < 12; i++) {
-        xa = step4_l8(lds, xa, i < 11 ? w[i + 1] : 0u, B, SEL);
-        xb = step4_l8(lds, xb, i < 11 ? w[13 + i] : 0u, B, SEL);
-    }
-    return merge_shift_dma(lds, 0, xa, xb);
-}
-
-// Table image of the variable-length LDS-DMA kernels (layout above); zeroes every wave's scratch.
-template <int NT = kWgThreads>
-__device__ __forceinline__ void stage_fd_tables(const KParams &p, uint8_t *lds, int tid) {
-    for (int i = tid; i < 2048; i += NT) {   // slice tables as fcs_dma_kernel
-        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
-        u32x4 vv = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
-    }
-    for (int i = tid; i < 16 * 128; i += NT) {   // A_{96c}: table c, nibble t, entry e
-        const int c = i >> 7, t = (i >> 4) & 7, e = i & 15;
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * (uint32_t)c + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
-                                      4u * (uint32_t)e) = p.blob[kBlobFlat + c * (kFlatStride / 4) + t * 16 + e];
-    }
-    for (int i = tid; i < 128; i += NT) {   // A_48 (merge table 0 of fcs_dma_kernel) and A_1536
-        const int t = (i >> 4) & 7, e = i & 15;
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaMergeHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
-                                      4u * (uint32_t)e) = p.blob[kBlobMerge + (kDmaChainWords / 2 - 1) * 128 + i];
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdJumpHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
-                                      4u * (uint32_t)e) = p.blob[kBlobJump + i];
-    }
-    for (int i = tid; i < kChunkBytes; i += NT)
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kDmaInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
-            p.blob[kBlobInv + i];
-    for (int i = tid; i < 16 * 4 * 32; i += NT)   // window scratch of every wave: zero
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kFdWaveHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) = 0u;
-}
-
-#ifdef FCS_FLAT2
-// ---------------------------------------------------------------------------------------------
-// MEASUREMENT-ONLY (-DFCS_FLAT2; rejected, DESIGN.md §3.3: 2 x 8 waves IMIX +2 %, 576 B -2 %;
-// 2 x 10 and 2 x 12 waves slower or mixed).
-// The flat chunk stream at two workgroups per CU (fcs_flat2_kernel). fcs_flat_kernel runs slower
-// with fewer waves per CU (IMIX, one process: 12 waves 4828, 14 waves 5078, 16 waves 5286 GB/s),
-// and 16 is one workgroup's limit. This form
-// keeps the flat kernel's dealing and chunk work but takes the compact 64 KiB table image of the
-// LDS-DMA kernels (32 KiB of 8-replica slice tables; A_{96c}, A_48, A_1536, INV and each wave's
-// accumulators, marks and lists in the row holes: stage_fd_tables), so two workgroups of
-// kFlat2Threads fit one CU's LDS, and its registers are held to kFlat2Waves / 4 waves per SIMD.
-// ---------------------------------------------------------------------------------------------
-template <int NT>
-__global__ __launch_bounds__(NT, 2) void fcs_flat2_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing];
-    static_assert(NT / 64 <= 16, "wave scratch holds 16 waves");
-    const int tid = threadIdx.x;
-    stage_fd_tables<NT>(p, lds, tid);
-    init_bad<kDmaBad>(lds);
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & (kGroup - 1);
-    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
-    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
-    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
-                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
-    uint8_t *mark = lds + dma_hole(kFdWaveHole + 4u * wave + 2u);
-    uint8_t *list = mark + 64;
-    uint8_t *mlist = lds + dma_hole(kFdWaveHole + 4u * wave + 3u);
-    auto acc = [&](uint32_t i) { return reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, i)); };
-
-    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (NT / 64),
-                (uint64_t)blockIdx.x * (NT / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
-    for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
-        const uint64_t w0 = win * 64;
-        // ---- window metadata: lane i <-> frame w0 + i ----
-        const uint64_t f = w0 + lane;
-        const bool act = f < p.n;
-        const uint32_t L = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
-        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;
-        const bool multi = act && L > (uint32_t)kSegBytes;
-        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
-        uint32_t incl = k;   // inclusive prefix over the window
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += y;
-        }
-        const uint32_t P = incl - k;
-        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
-        const uint64_t fmask = __ballot(k != 0);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
-        mark[lane] = 0;
-        if (k) list[rank] = (uint8_t)lane;
-        wave_lds_sync();
-        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
-        // no frame over 1536 B: a chunk's frame rank is its frame's lane; frame ends in one 4 GiB page
-        const bool dense = __ballot(multi) == 0;
-        const uint32_t Ehi0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)Ehi);
-        const bool onehi = __ballot(Ehi != Ehi0) == 0;
-
-        // one item = 64 chunks: lane -> (frame, chunk), its loads, its chunk value into the frame
-        for (uint32_t g0 = 0, tag = 1; g0 < K; g0 += 64, tag++) {
-            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = (uint8_t)tag;
-            wave_lds_sync();
-            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
-            const uint64_t M = __ballot(mark[lane] == (uint8_t)tag);
-            const uint32_t g = g0 + (uint32_t)lane;
-            const bool valid = g < K;
-            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
-            const int src = valid ? (dense ? (int)(rk & 63u) : (int)list[rk & 63u]) : 0;
-            const uint32_t Eghi = onehi ? Ehi0 : (uint32_t)__shfl((int)Ehi, src);
-            const uint64_t Eg = ((uint64_t)Eghi << 32) | (uint32_t)__shfl((int)Elo, src);
-            const uint32_t Lg = (uint32_t)__shfl((int)L, src);
-            const uint32_t Pg = (uint32_t)__shfl((int)P, src);
-            const uint32_t c = valid ? g - Pg : 0u;   // chunk index back from the frame end
-            const int64_t cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(c + 1);
-            const int zr = valid ? clamp_zr((int64_t)(Eg - Lg) - cstart) : kChunkBytes;
-            Chunk ch;
-            issue_any<false>(p, cstart, valid && zr < kChunkBytes, ch);
-            uint32_t w[kChunkWords];
-            fd_chunk_words(ch, w);
-            // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
-            const uint32_t own = fd_value(lds, w, zr, zr < kChunkBytes ? zr : 0, valid ? fd_inv(lds, zr) : 0u, B, SEL);
-            const uint32_t v = fd_chunk_shift(lds, own, c & 15u);
-            if (valid && v) atomicXor(acc((uint32_t)src), v);
-        }
-
-        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment ----
-        const uint64_t xmask = __ballot(multi);
-        const uint32_t nx = (uint32_t)__popcll(xmask);
-        if (nx) {
-            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
-            if (multi) mlist[rx] = (uint8_t)lane;
-            wave_lds_sync();
-            for (uint32_t t = 0; t < nx; t += 4) {
-                const uint32_t rnk = t + (uint32_t)(lane >> 4);
-                const bool valid = rnk < nx;
-                const int src = valid ? (int)mlist[rnk] : 0;
-                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
-                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
-                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
-                uint32_t s = 0;
-                for (uint32_t q = 0; __any(q < m); q++) {
-                    const bool on = q < m;
-                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
-                                           (int64_t)kChunkBytes * (j + 1);
-                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
-                    Chunk cc;
-                    issue_any<false>(p, cstart, on && zr < kChunkBytes, cc);
-                    uint32_t w[kChunkWords];
-                    fd_chunk_words(cc, w);
-                    const uint32_t r = fd_value(lds, w, zr, on ? zr : 0, (on && q == 0) ? fd_inv(lds, zr) : 0u, B, SEL);
-                    s = on ? (q == 0 ? r : fd_jump(lds, s, r)) : s;
-                }
-                const uint32_t v = row_xor(fd_chunk_shift(lds, s, (uint32_t)j));
-                if (valid && j == 15) *acc((uint32_t)src) = v;
-            }
-        }
-
-        // ---- one coalesced store per window; clear the accumulators ----
-        wave_lds_sync();
-        const uint32_t a = *acc((uint32_t)lane);
-        emit<kDmaBad>(p, lds, act, f, L ? ~a : 0u);
-        *acc((uint32_t)lane) = 0u;
-    }
-    flush_bad<kDmaBad>(p, lds);
-}
-#endif  // FCS_FLAT2
-
-#ifdef FCS_FLATDMA
-constexpr uint32_t kFdSlotBytes = 6144;                // 64 lanes x 96 B, piece i of lane l at 1024 i + 16 l
-// ---------------------------------------------------------------------------------------------
-// MEASUREMENT-ONLY (-DFCS_FLATDMA; rejected: IMIX 4629 vs 5200 GB/s).
-// Variable-length frames, flat chunk stream, chunk windows staged through LDS by DMA
-// (fcs_flatdma_kernel; replaces fcs_flat_kernel<false> in -DFCS_FLATDMA builds).
-// The dealing of fcs_flat_kernel (64-frame windows, 64 chunks per item, frame-start marks), but
-// each lane copies its own 96-byte window into the wave's LDS slot with six
-// global_load_lds_dwordx4 at the window's exact byte address: gfx950's LDS-DMA honours any byte
-// alignment (tools/microbench/glds_align.hip), so no realignment is needed and no VGPR holds the
-// bytes in flight. Lane l's 16-byte piece i lands at slot + 1024 i + 16 l and comes back with one
-// ds_read_b128 per piece (16 lanes per 256-B bank row: 4 cycles, the minimum; random 16-B pieces
-// would cost 12, tools/microbench/lds_pat.hip). A wave deals its next item and issues that item's
-// DMA as soon as the current item's words are in registers, so the next item's bytes land while
-// the current item's CRC work runs (fcs_flat_kernel waits for each item's loads with nothing else
-// to do). An item whose windows reach before the arena start (the frames at the arena's first 96
-// bytes) is loaded into registers instead, with the arena-edge shift of the other kernels.
-// Tables: the 32 KiB slice tables of fcs_dma_kernel (step4_l8) and, in the row holes, the
-// c-indexed shift tables A_{96c} (nibble t of table c at hole 4c + t/2, +64 B for odd t), the A_48
-// merge table and INV of fcs_dma_kernel, A_1536 for frames over 1536 B, and each wave's window
-// scratch (accumulators, marks, frame lists).
-// ---------------------------------------------------------------------------------------------
-#ifndef FCS_FD_AUX   // cache policy of the window DMA (measurement-only override)
-#define FCS_FD_AUX 0
-#endif
-
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_flatdma_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing + 16 * kFdSlotBytes];
-    static_assert(kWgThreads / 64 <= 16, "slots");
-    const int tid = threadIdx.x;
-    stage_fd_tables(p, lds, tid);
-    init_bad<kDmaBad>(lds);
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & (kGroup - 1);
-    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
-    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
-    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
-                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
-    uint8_t *slot = lds + kDmaRing + wave * kFdSlotBytes;
-    uint8_t *mark = lds + dma_hole(kFdWaveHole + 4u * wave + 2u);
-    uint8_t *list = mark + 64;
-    uint8_t *mlist = lds + dma_hole(kFdWaveHole + 4u * wave + 3u);
-    const uint32_t acc_lane = fd_acc_addr(wave, (uint32_t)lane);
-
-    struct It {
-        int src, zr;
-        uint32_t c;
-        int64_t cstart;
-        uint64_t base;      // chunk-major DMA: lane 0's window start, and this lane's offset from it
-        int relv;
-        bool valid, rare;   // rare (wave-uniform): a window reaches before the arena start
-    };
-
-    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
-                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
-    uint32_t tagc = 0;   // mark tags: distinct within a window (reset with the marks)
-    for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
-        const uint64_t w0 = win * 64;
-        // ---- window metadata: lane i <-> frame w0 + i ----
-        const uint64_t f = w0 + lane;
-        const bool act = f < p.n;
-        const uint32_t L = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
-        const uint64_t E = act ? p.base + (p.off ? p.off[f] : f * p.stride) + L : p.lo4;
-        const bool multi = act && L > (uint32_t)kSegBytes;
-        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
-        uint32_t incl = k;   // inclusive prefix over the window
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += y;
-        }
-        const uint32_t P = incl - k;
-        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
-        const uint64_t fmask = __ballot(k != 0);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
-        mark[lane] = 0;
-        if (k) list[rank] = (uint8_t)lane;
-        wave_lds_sync();
-        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
-        tagc = 0;
-
-        // deal item g0: lane -> (frame, chunk), then issue its window DMA
-        auto prep = [&](uint32_t g0, It &it) {
-            const uint8_t tag = (uint8_t)++tagc;
-            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = tag;
-            wave_lds_sync();
-            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
-            const uint64_t M = __ballot(mark[lane] == tag);
-            const uint32_t g = g0 + (uint32_t)lane;
-            it.valid = g < K;
-            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
-            it.src = it.valid ? (int)list[rk & 63u] : 0;
-            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, it.src) << 32) | (uint32_t)__shfl((int)Elo, it.src);
-            const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
-            const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
-            it.c = it.valid ? g - Pg : 0u;   // chunk index back from the frame end
-            it.cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
-            it.zr = it.valid ? clamp_zr((int64_t)(Eg - Lg) - it.cstart) : kChunkBytes;
-            const bool need = it.valid && it.zr < kChunkBytes;
-            // chunk-major DMA: instruction i, lane l copies piece m of chunk q (6 q + m = 64 i + l)
-            // to slot + 96 q + 16 m, so the 6 lanes of a chunk read its 96 contiguous bytes and
-            // consecutive chunks of a frame are adjacent runs; chunk addresses travel as 32-bit
-            // offsets from lane 0's window
-            const uint64_t base = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((uint64_t)it.cstart >> 32)) << 32) |
-                                  (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uint64_t)it.cstart);
-            const int64_t rel = it.cstart - (int64_t)base;
-            const bool far = rel < -(int64_t)0x3FFFFFFF || rel > (int64_t)0x3FFFFFFF;
-            it.rare = __any(need && (it.cstart < (int64_t)p.lo4 || far));
-            it.base = base;
-            it.relv = need ? (int)rel : (int)0x80000000;
-        };
-        // the item's window DMA (after its dealing, once the slot is free)
-        auto dma = [&](const It &it) {
-            if (!it.rare) {
-                typedef __attribute__((address_space(3))) void lds_void;
-#pragma unroll
-                for (int i = 0; i < 6; i++) {
-                    const uint32_t t = 64u * (uint32_t)i + (uint32_t)lane, q = t / 6u, m = t - 6u * q;
-                    const int rq = __shfl(it.relv, (int)q);
-                    if (rq != (int)0x80000000)
-                        __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(it.base + (int64_t)rq + 16 * m),
-                                                         (lds_void *)(slot + 1024 * i), 16, 0, FCS_FD_AUX);
-                }
-            }
-        };
-        auto finish = [&](const It &it, uint32_t (&w)[kChunkWords]) {
-            // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
-            const uint32_t own = fd_value(lds, w, it.zr, it.zr < kChunkBytes ? it.zr : 0, it.valid ? fd_inv(lds, it.zr) : 0u,
-                                          B, SEL);
-            const uint32_t v = fd_chunk_shift(lds, own, it.c & 15u);
-            if (it.valid && v) atomicXor(reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)it.src)), v);
-        };
-
-        if (K) {
-            It cur;
-            prep(0, cur);
-            dma(cur);
-            for (uint32_t g0 = 0; g0 < K; g0 += 64) {
-                uint32_t w[kChunkWords];
-                // the next item's dealing first: its LDS round trips overlap this item's DMA wait
-                It nxt;
-                nxt.valid = false;
-                const bool more = g0 + 64 < K;
-                if (more) prep(g0 + 64, nxt);
-                if (!cur.rare) {
-                    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this item's window DMA has landed
-#pragma unroll
-                    for (int i = 0; i < 6; i++) {
-                        const u32x4 x = *reinterpret_cast<const u32x4 *>(slot + 96 * lane + 16 * i);
-                        w[4 * i] = x.x;
-                        w[4 * i + 1] = x.y;
-                        w[4 * i + 2] = x.z;
-                        w[4 * i + 3] = x.w;
-                    }
-                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
-                } else {   // the arena start: register loads with the edge shift
-                    Chunk ch;
-                    issue_any<false>(p, cur.cstart, cur.valid && cur.zr < kChunkBytes, ch);
-                    fd_chunk_words(ch, w);
-                }
-                if (more) dma(nxt);
-                finish(cur, w);
-                cur = nxt;
-            }
-        }
-
-        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment (register loads) ----
-        const uint64_t xmask = __ballot(multi);
-        const uint32_t nx = (uint32_t)__popcll(xmask);
-        if (nx) {
-            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
-            if (multi) mlist[rx] = (uint8_t)lane;
-            wave_lds_sync();
-            for (uint32_t t = 0; t < nx; t += 4) {
-                const uint32_t rnk = t + (uint32_t)(lane >> 4);
-                const bool valid = rnk < nx;
-                const int src = valid ? (int)mlist[rnk] : 0;
-                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
-                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
-                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
-                uint32_t s = 0;
-                for (uint32_t q = 0; __any(q < m); q++) {
-                    const bool on = q < m;
-                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
-                                           (int64_t)kChunkBytes * (j + 1);
-                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
-                    Chunk cc;
-                    issue_any<false>(p, cstart, on && zr < kChunkBytes, cc);
-                    uint32_t w[kChunkWords];
-                    fd_chunk_words(cc, w);
-                    const uint32_t r = fd_value(lds, w, zr, on ? zr : 0, (on && q == 0) ? fd_inv(lds, zr) : 0u, B, SEL);
-                    s = on ? (q == 0 ? r : fd_jump(lds, s, r)) : s;
-                }
-                const uint32_t v = row_xor(fd_chunk_shift(lds, s, (uint32_t)j));
-                if (valid && j == 15) *reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)src)) = v;
-            }
-        }
-
-        // ---- one coalesced store per window; clear the accumulators ----
-        wave_lds_sync();
-        uint32_t *accp = reinterpret_cast<uint32_t *>(lds + acc_lane);
-        const uint32_t a = *accp;
-        emit<kDmaBad>(p, lds, act, f, L ? ~a : 0u);
-        *accp = 0u;
-    }
-    flush_bad<kDmaBad>(p, lds);
-}
-#endif  // FCS_FLATDMA
-
-#ifdef FCS_SPAN
-// ---------------------------------------------------------------------------------------------
-// MEASUREMENT-ONLY (-DFCS_SPAN; rejected: IMIX 4408 vs 4977 GB/s for fcs_flat_kernel in one
-// process). Its loads alone run at 5734-6130 GB/s against the flat kernel's 5344,
-// but its CRC work is not hidden behind them: per item it adds the LDS-DMA writes, seven 16-B
-// window reads and a 16-B realignment to the chain's table lookups, and the CU's VALU and LDS
-// pipes then limit it.
-// Variable-length frames, flat chunk stream staged through LDS by span DMA (fcs_span_kernel;
-// replaces fcs_flat_kernel<false> for windowed batches in -DFCS_SPAN builds).
-// The dealing of fcs_flat_kernel (64-frame windows, 64 chunks per item, frame-start marks), with a
-// frame's chunks dealt front to back: window chunk g is chunk k - 1 - (g - P) back from its frame's
-// end (k chunks, P the frame's first chunk). An item's 64 chunks then lie in arena order, and for
-// packed frames inside one span of at most 64 x 96 bytes (frame-aligned chunks overlap at frame
-// fronts, they never leave gaps). That span is one LDS-DMA of up to six 1 KiB rows into the wave's
-// 6 KiB slot: the coalesced rows of fcs_dma_kernel instead of 64 scattered 96-B windows. Its start
-// and end are wave-uniform scalar work (the frames holding the item's first and last chunk: a
-// ballot over the prefix, readlanes), independent of the per-lane dealing, so the next item's DMA
-// is issued as soon as the current item's windows are in registers; the current item's CRC work
-// and the next item's dealing (marks, ballots, bpermutes) run while it flies. A lane reads its
-// 96-B window at its byte offset in the slot (25 dwords, realigned as in fcs_dma_kernel).
-// An item whose windows do not all lie in its slot (gaps between frames, offsets out of order, a
-// frame over 1536 B between two others) loads them into registers instead (issue_any, the
-// arena-edge path of the other kernels). Frames over 1536 B take the segment loop of
-// fcs_flat_kernel. The next window's offsets and lengths are loaded at the start of the current one.
-// ---------------------------------------------------------------------------------------------
-struct SpanDma {
-    uint64_t src;    // 16-B aligned address of the slot's first byte
-    uint32_t need;   // slot bytes up to the end of the item's last chunk
-    bool rare;       // wave-uniform: the item's chunks do not fit the slot (register loads, no DMA)
-};
-
-// The item's span: 1 KiB rows as far as its bytes reach. The first and the last row keep the
-// default cache policy (their 128-B lines are shared with the neighbouring items), the rows
-// between are non-temporal, as in dma_item.
-__device__ __forceinline__ void span_dma(const uint8_t *slot, const SpanDma &sd, int lane) {
-    typedef __attribute__((address_space(3))) void lds_void;
-    const uint64_t a = sd.src + 16 * (uint64_t)lane, b = a + 4096;
-    lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
-    const uint32_t o = 16u * (uint32_t)lane, need = sd.need;
-    const uint32_t last = (need - 1u) >> 10;   // wave-uniform
-    if (o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, FCS_DMA_EDGE_AUX);
-    if (1024u + o < need) {
-        if (last == 1) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_EDGE_AUX);
-        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, FCS_DMA_AUX);
-    }
-    if (2048u + o < need) {
-        if (last == 2) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_EDGE_AUX);
-        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
-    }
-    if (3072u + o < need) {
-        if (last == 3) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_EDGE_AUX);
-        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
-    }
-    if (4096u + o < need) {
-        if (last == 4) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_EDGE_AUX);
-        else __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
-    }
-    if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_EDGE_AUX);
-}
-
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_span_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaRing + 16 * kDmaItemBytes];
-    static_assert(kWgThreads / 64 <= 16, "slots");
-    const int tid = threadIdx.x;
-    stage_fd_tables(p, lds, tid);
-    init_bad<kDmaBad>(lds);
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
-    const int j = lane & (kGroup - 1);
-    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
-    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
-    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
-                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
-    const uint8_t *slot = lds + kDmaRing + wave * kDmaItemBytes;
-    uint8_t *mark = lds + dma_hole(kFdWaveHole + 4u * wave + 2u);
-    uint8_t *list = mark + 64;
-    uint8_t *mlist = lds + dma_hole(kFdWaveHole + 4u * wave + 3u);
-    const uint32_t acc_lane = fd_acc_addr(wave, (uint32_t)lane);
-    const uint64_t lo16 = p.lo4 & ~15ull;
-    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start (host: arena >= 2 slots)
-
-    struct It {
-        int src, zr;
-        uint32_t c;
-        int64_t cstart;
-        bool valid, rare;
-    };
-
-    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
-                (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
-    // window metadata, loaded one window ahead (raw: the loads stay in flight): lane i <-> frame 64 win + i
-    auto load_meta = [&](uint64_t win, uint32_t &Lr, uint64_t &Or) {
-        const uint64_t f = win * 64 + (uint64_t)lane;
-        const bool act = win != Dispenser::kEnd && f < p.n;
-        Lr = act ? (p.len ? p.len[f] : p.flen) : 0u;   // len == null: fixed length
-        Or = act ? (p.off ? p.off[f] : f * p.stride) : 0u;
-    };
-    uint64_t win = D.first();
-    uint32_t Ln;
-    uint64_t On;
-    load_meta(win, Ln, On);
-    uint32_t tagc = 0;   // mark tags: distinct within a window (reset with the marks)
-    while (win != Dispenser::kEnd) {
-        const uint64_t w0 = win * 64;
-        const uint64_t f = w0 + lane;
-        const bool act = f < p.n;
-        const uint32_t L = Ln;
-        const uint64_t E = act ? p.base + On + L : p.lo4;
-        const uint64_t nwin = D.next(win);
-        load_meta(nwin, Ln, On);
-        const bool multi = act && L > (uint32_t)kSegBytes;
-        const uint32_t k = (!act || multi) ? 0u : (L ? (L + kChunkBytes - 1) / kChunkBytes : 1u);
-        uint32_t incl = k;   // inclusive prefix over the window
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += y;
-        }
-        const uint32_t P = incl - k;
-        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
-        const uint64_t fmask = __ballot(k != 0);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
-        mark[lane] = 0;
-        if (k) list[rank] = (uint8_t)lane;
-        wave_lds_sync();
-        const uint32_t Elo = (uint32_t)E, Ehi = (uint32_t)(E >> 32);
-        // no frame over 1536 B: the frames with chunks are lanes 0, 1, ..., so a rank is a lane
-        const bool dense = __ballot(multi) == 0;
-        tagc = 0;
-
-        // wave-uniform: start address of window chunk g < K
-        auto chunk_at = [&](uint32_t g) -> int64_t {
-            const uint32_t rk = (uint32_t)__popcll(__ballot(k != 0 && P <= g)) - 1u;
-            const int fl = dense ? (int)rk : __builtin_amdgcn_readfirstlane((int)list[rk & 63u]);
-            const uint64_t Ef = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)Ehi, fl) << 32) |
-                                (uint32_t)__builtin_amdgcn_readlane((int)Elo, fl);
-            const uint32_t Lf = (uint32_t)__builtin_amdgcn_readlane((int)L, fl);
-            const uint32_t Pf = (uint32_t)__builtin_amdgcn_readlane((int)P, fl);
-            const uint32_t kf = Lf ? (Lf + kChunkBytes - 1) / kChunkBytes : 1u;
-            return (int64_t)Ef - (int64_t)kChunkBytes * (int64_t)(kf - (g - Pf));
-        };
-        // the slot of item g0: from its first chunk's 16-B line to its last chunk's end
-        auto span = [&](uint32_t g0) -> SpanDma {
-            const uint32_t g1 = (g0 + 64 < K ? g0 + 64 : K) - 1u;
-            const int64_t s0 = chunk_at(g0), e1 = chunk_at(g1) + kChunkBytes;
-            SpanDma sd;
-            const uint64_t a = (uint64_t)s0 & ~15ull;
-            sd.src = a < lo16 ? lo16 : (a > smax ? smax : a);
-            const int64_t need = e1 - (int64_t)sd.src;
-            sd.rare = need <= 0 || need > (int64_t)kDmaItemBytes;
-            sd.need = (uint32_t)__builtin_amdgcn_readfirstlane((int)(sd.rare ? 1u : (uint32_t)need));
-            sd.src = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(sd.src >> 32)) << 32) |
-                     (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)sd.src);
-            return sd;
-        };
-        // deal item g0: lane -> (frame, chunk); the item stays on the DMA path only if every lane's
-        // frame bytes lie in the slot
-        auto prep = [&](uint32_t g0, const SpanDma &sd, It &it) {
-            const uint8_t tag = (uint8_t)++tagc;
-            if (k && P >= g0 && P < g0 + 64) mark[P - g0] = tag;
-            wave_lds_sync();
-            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
-            const uint64_t M = __ballot(mark[lane] == tag);
-            const uint32_t g = g0 + (uint32_t)lane;
-            it.valid = g < K;
-            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
-            it.src = it.valid ? (dense ? (int)(rk & 63u) : (int)list[rk & 63u]) : 0;
-            const uint64_t Eg = ((uint64_t)(uint32_t)__shfl((int)Ehi, it.src) << 32) | (uint32_t)__shfl((int)Elo, it.src);
-            const uint32_t Lg = (uint32_t)__shfl((int)L, it.src);
-            const uint32_t Pg = (uint32_t)__shfl((int)P, it.src);
-            const uint32_t kg = Lg ? (Lg + kChunkBytes - 1) / kChunkBytes : 1u;
-            it.c = it.valid ? kg - 1u - (g - Pg) : 0u;   // chunk index back from the frame end
-            it.cstart = (int64_t)Eg - (int64_t)kChunkBytes * (int64_t)(it.c + 1);
-            const int64_t fs = (int64_t)(Eg - Lg);
-            it.zr = it.valid ? clamp_zr(fs - it.cstart) : kChunkBytes;
-            const int64_t lo = it.cstart > fs ? it.cstart : fs;
-            const bool in = !it.valid || it.zr >= kChunkBytes ||
-                            (lo >= (int64_t)sd.src && it.cstart + kChunkBytes <= (int64_t)sd.src + (int64_t)sd.need);
-            it.rare = sd.rare || __any(!in);
-        };
-
-        if (K) {
-            SpanDma sp = span(0);
-            if (!sp.rare) span_dma(slot, sp, lane);
-            It cur;
-            prep(0, sp, cur);
-            for (uint32_t g0 = 0; g0 < K; g0 += 64) {
-                const bool more = g0 + 64 < K;
-                SpanDma sn{0, 1u, true};
-                if (more) sn = span(g0 + 64);
-                uint32_t w[kChunkWords];
-#ifdef FCS_SPAN_B32   // measurement-only: 25 dword reads at the window's 4-B address (bank conflicts)
-                if (!cur.rare) {
-                    const int x = cur.valid ? (int)(cur.cstart - (int64_t)sp.src) : 0;
-                    const uint32_t r = (uint32_t)x & 3u;
-                    const uint8_t *wp = slot + (x & ~3);
-                    uint32_t d[kChunkWords + 1];
-                    __builtin_amdgcn_s_waitcnt(0x0F70);
-#pragma unroll
-                    for (int q = 0; q < kChunkWords; q++) d[q] = *reinterpret_cast<const uint32_t *>(wp + 4 * q);
-                    {
-                        const uint8_t *a24 = wp + 4 * kChunkWords, *lim = slot + kDmaItemBytes - 4;
-                        d[kChunkWords] = *reinterpret_cast<const uint32_t *>(a24 < lim ? a24 : lim);
-                    }
-                    __builtin_amdgcn_s_waitcnt(0xC07F);
-#pragma unroll
-                    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
-                } else
-#endif
-                if (!cur.rare) {
-                    // the window at its byte offset x in the slot (x >= -95: a front window reaching
-                    // before the arena start reads LDS below the slot, bytes that get masked), read
-                    // as seven 16-B pieces from x rounded down to 16 B: packed windows sit at 64..96-B
-                    // strides, where ds_read_b32 would put 16-32 lanes on one bank (25 reads), and
-                    // ds_read_b128 8-16 lanes on one 16-B group (7 reads; tools/microbench/lds_pat.hip)
-                    const int x = cur.valid ? (int)(cur.cstart - (int64_t)sp.src) : 0;
-                    const uint8_t *wp = slot + (x & ~15);
-                    u32x4 q[7];
-                    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the item's span has landed
-#pragma unroll
-                    for (int i = 0; i < 6; i++) q[i] = *reinterpret_cast<const u32x4 *>(wp + 16 * i);
-                    {   // the 7th piece matters only when x is not 16-B aligned, and then lies in the slot
-                        const uint8_t *a6 = wp + 96, *lim = slot + kDmaItemBytes - 16;
-                        q[6] = *reinterpret_cast<const u32x4 *>(a6 < lim ? a6 : lim);
-                    }
-                    __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next span
-                    uint32_t d[28];
-#pragma unroll
-                    for (int i = 0; i < 7; i++) {
-                        d[4 * i] = q[i].x;
-                        d[4 * i + 1] = q[i].y;
-                        d[4 * i + 2] = q[i].z;
-                        d[4 * i + 3] = q[i].w;
-                    }
-                    // realign: dword shift s = (x >> 2) & 3 in two select stages, then the byte shift.
-                    // The selects are v_perm (whole dword from either source): written as ?: the
-                    // compiler turns the stages into an indexed array in scratch memory.
-#ifdef FCS_SPAN_ABL_NOALIGN   // measurement-only: no realignment (wrong FCS unless x is 16-B aligned)
-#pragma unroll
-                    for (int i = 0; i < kChunkWords; i++) w[i] = d[i];
-#else
-                    const uint32_t p1 = (x & 4) ? 0x07060504u : 0x03020100u, p2 = (x & 8) ? 0x07060504u : 0x03020100u;
-#pragma unroll
-                    for (int i = 0; i < 26; i++) d[i] = __builtin_amdgcn_perm(d[i + 2], d[i], p2);
-#pragma unroll
-                    for (int i = 0; i < 25; i++) d[i] = __builtin_amdgcn_perm(d[i + 1], d[i], p1);
-                    const uint32_t r = (uint32_t)x & 3u;
-#pragma unroll
-                    for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
-#endif
-                } else {   // register loads (with the arena-edge shift)
-                    Chunk ch;
-                    issue_any<false>(p, cur.cstart, cur.valid && cur.zr < kChunkBytes, ch);
-                    fd_chunk_words(ch, w);
-                    __builtin_amdgcn_s_waitcnt(0x0F70);   // and a span DMA issued for this item, if any
-                }
-                if (more && !sn.rare) span_dma(slot, sn, lane);
-                {
-#ifdef FCS_SPAN_NOCRC   // measurement-only build: the span DMA, reads and dealing without the CRC work
-                    uint32_t v = cur.c;
-#pragma unroll
-                    for (int i = 0; i < kChunkWords; i++) v ^= w[i];
-#else
-                    // lanes past the window's chunks and the dummy chunk of an empty frame (zr = 96) are discarded
-                    const uint32_t own = fd_value(lds, w, cur.zr, cur.zr < kChunkBytes ? cur.zr : 0,
-                                                  cur.valid ? fd_inv(lds, cur.zr) : 0u, B, SEL);
-                    const uint32_t v = fd_chunk_shift(lds, own, cur.c & 15u);
-#endif
-                    if (cur.valid && v) atomicXor(reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)cur.src)), v);
-                }
-                if (more) prep(g0 + 64, sn, cur);
-                sp = sn;
-            }
-        }
-
-        // ---- frames over 1536 B: 16 lanes each, 4 per item, segment by segment (register loads) ----
-        const uint64_t xmask = __ballot(multi);
-        const uint32_t nx = (uint32_t)__popcll(xmask);
-        if (nx) {
-            const uint32_t rx = __builtin_amdgcn_mbcnt_hi((uint32_t)(xmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)xmask, 0u));
-            if (multi) mlist[rx] = (uint8_t)lane;
-            wave_lds_sync();
-            for (uint32_t t = 0; t < nx; t += 4) {
-                const uint32_t rnk = t + (uint32_t)(lane >> 4);
-                const bool valid = rnk < nx;
-                const int src = valid ? (int)mlist[rnk] : 0;
-                const uint64_t Eq = ((uint64_t)(uint32_t)__shfl((int)Ehi, src) << 32) | (uint32_t)__shfl((int)Elo, src);
-                const uint32_t Lq = (uint32_t)__shfl((int)L, src);
-                const uint32_t m = valid ? (Lq + (kSegBytes - 1)) / kSegBytes : 0u;
-                uint32_t s = 0;
-                for (uint32_t q = 0; __any(q < m); q++) {
-                    const bool on = q < m;
-                    const int64_t cstart = (int64_t)Eq - (int64_t)kSegBytes * (int64_t)(m - 1 - q) -
-                                           (int64_t)kChunkBytes * (j + 1);
-                    const int zr = (on && q == 0) ? clamp_zr((int64_t)(Eq - Lq) - cstart) : (on ? -1 : kChunkBytes);
-                    Chunk cc;
-                    issue_any<false>(p, cstart, on && zr < kChunkBytes, cc);
-                    uint32_t w[kChunkWords];
-                    fd_chunk_words(cc, w);
-                    const uint32_t r = fd_value(lds, w, zr, on ? zr : 0, (on && q == 0) ? fd_inv(lds, zr) : 0u, B, SEL);
-                    s = on ? (q == 0 ? r : fd_jump(lds, s, r)) : s;
-                }
-                const uint32_t v = row_xor(fd_chunk_shift(lds, s, (uint32_t)j));
-                if (valid && j == 15) *reinterpret_cast<uint32_t *>(lds + fd_acc_addr(wave, (uint32_t)src)) = v;
-            }
-        }
-
-        // ---- one coalesced store per window; clear the accumulators ----
-        wave_lds_sync();
-        uint32_t *accp = reinterpret_cast<uint32_t *>(lds + acc_lane);
-        const uint32_t a = *accp;
-        emit<kDmaBad>(p, lds, act, f, L ? ~a : 0u);
-        *accp = 0u;
-        win = nwin;
-    }
-    flush_bad<kDmaBad>(p, lds);
-}
-#endif  // FCS_SPAN
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -3163,35 +1823,12 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             if (tiny) FCS_LAUNCH(true, true, false);
             else FCS_LAUNCH(true, false, false);
         } else if (tiny) {
-#ifdef FCS_VAR_HALFUNIT   // measurement-only build: the half-unit windowed kernel it replaced
-            hipLaunchKernelGGL((fcs_var_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
-#else
             hipLaunchKernelGGL((fcs_flat_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
-#endif
         } else {
-#if defined(FCS_VAR_HALFUNIT)
-            hipLaunchKernelGGL((fcs_var_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
-#elif defined(FCS_FLATDMA)   // measurement-only build: per-lane window DMA (rejected)
-            hipLaunchKernelGGL(fcs_flatdma_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
-#else
-#ifdef FCS_FLAT2
-            if (var_flat2(p)) hipLaunchKernelGGL(fcs_flat2_kernel<kFlat2Threads>, dim3(2 * grid), dim3(kFlat2Threads), 0, st, p);
-            else
-#endif
-#ifdef FCS_SPAN   // measurement-only build: span DMA (rejected)
-            if (var_span(p)) hipLaunchKernelGGL(fcs_span_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
-            else
-#endif
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
-#endif
         }
     } else if (fixed_segil(p)) {
         hipLaunchKernelGGL(fcs_segil_kernel, dim3(grid), dim3(kSegilThreads), 0, st, p);
-#ifdef FCS_DMASEG
-    } else if (!tiny && fixed_dmaseg(p)) {
-        if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dmaseg_kernel<2>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
-        else hipLaunchKernelGGL((fcs_dmaseg_kernel<kSingleMaskWords>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
-#endif
     } else if (!tiny && fixed_dma(p)) {
         if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dma_kernel<2, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
         else hipLaunchKernelGGL((fcs_dma_kernel<kSingleMaskWords, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);

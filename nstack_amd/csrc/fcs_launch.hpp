@@ -107,35 +107,14 @@ inline bool fixed_single(const KParams &p) {
 #endif
 }
 // Windowed variable-length batches (and the short fixed-length route) take fcs_flat_kernel.
-// Measurement-only (-DFCS_SPAN): the span-DMA kernel (fcs_span_kernel) instead when the arena
-// holds two 6 KiB slots (its slots are clamped to the arena's last 6 KiB). DESIGN.md §3.3.
-inline bool var_span(const KParams &p) {
-#ifdef FCS_SPAN
-    return p.hi4 - p.lo4 >= 2 * 6144ull;
-#else
-    (void)p;
-    return false;
-#endif
-}
-// Measurement-only (-DFCS_FLAT2): windowed batches at two workgroups of kFlat2Threads per CU
-// (fcs_flat2_kernel; the host's grid counts CUs, the launcher doubles it) when the arena is not tiny.
-#ifndef FCS_FLAT2_THREADS
-#define FCS_FLAT2_THREADS 640
-#endif
-constexpr int kFlat2Threads = FCS_FLAT2_THREADS;
-inline bool var_flat2(const KParams &p) { return p.hi4 - p.lo4 >= 2 * (uint64_t)kChunkBytes; }
 // LDS-DMA kernel (fcs_dma_kernel): one-segment frames of kDmaMinLen..kDmaCover bytes whose four
 // consecutive frames (one wave item) fit one 6 KiB slot: the slot starts at floor16 of the first
 // frame's start and must reach ceil4 of the fourth frame's end (3 stride + len <= 6144 - 15 - 3),
 // and the arena must hold a whole slot (the last items' slots are clamped to its end).
-#ifndef FCS_DMA_PAIR   // 1: each wave works on two items at once, one 6 KiB slot each (8 waves per CU)
-#define FCS_DMA_PAIR 0
-#endif
-constexpr bool kDmaPair = FCS_DMA_PAIR != 0;
 #ifndef FCS_DMA_WG_THREADS   // measurement-only override
-#define FCS_DMA_WG_THREADS (FCS_DMA_PAIR ? 512 : 1024)
+#define FCS_DMA_WG_THREADS 1024
 #endif
-constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;  // one 6 KiB LDS slot per wave (two in pair mode)
+constexpr int kDmaWgThreads = FCS_DMA_WG_THREADS;  // one 6 KiB LDS slot per wave
 static_assert(kDmaWgThreads % 64 == 0 && kDmaWgThreads <= 1024, "LDS holds 16 slots next to the 64 KiB tables");
 // Batches of at least this many items (4 frames) per wave of the grid hand their tail out
 // dynamically (KParams::ctr): below it the static share alone balances well enough.
@@ -164,33 +143,9 @@ inline bool fixed_segil(const KParams &p) {
     return p.flen > kDmaCover && !fixed_tiny(p) && 4ull * p.flen >= 3ull * kDmaCover * m;
 #endif
 }
-// Segmented LDS-DMA kernel (fcs_dmaseg_kernel, MEASUREMENT-ONLY: -DFCS_DMASEG with -DFCS_NO_SEGIL;
-// superseded by fcs_segil_kernel, which matches it in its bands and has none): frames over
-// kDmaCover bytes that split into m = ceil(len / 1524) <= 27 segments of Ls = floor(len / m) >=
-// kDmaMinLen bytes with the remainder in the front one (<= kDmaCover), packed (gaps of at most 8
-// bytes) so four consecutive segments fit one slot; the arena holds two slots.
-#ifndef FCS_DMASEG_MAX_GAP   // measurement-only overrides (gap -1: never)
-#define FCS_DMASEG_MAX_GAP 8
-#endif
-constexpr uint32_t kDmaSegMaxSegs = 27;
-#ifndef FCS_DMASEG_MAX_SEGS
-#define FCS_DMASEG_MAX_SEGS 27
-#endif
-inline bool fixed_dmaseg(const KParams &p) {
-#ifndef FCS_DMASEG
-    (void)p;
-    return false;
-#else
-    if ((int64_t)FCS_DMASEG_MAX_GAP < 0 || p.flen <= kDmaCover || p.stride < p.flen ||
-        p.stride - p.flen > (uint64_t)FCS_DMASEG_MAX_GAP || p.hi4 - p.lo4 < 2 * kDmaItemBytes)
-        return false;
-    const uint32_t m = (p.flen + kDmaCover - 1) / kDmaCover, ls = p.flen / m;
-    return m <= FCS_DMASEG_MAX_SEGS && ls >= kDmaMinLen && p.flen - ls * (m - 1) <= kDmaCover;
-#endif
-}
 inline int fixed_threads(const KParams &p) {
     if (fixed_segil(p)) return kSegilWgThreads;
-    if (!fixed_tiny(p) && (fixed_dma(p) || fixed_dmaseg(p))) return kDmaWgThreads;
+    if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;
     return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;
 }
 

@@ -15,8 +15,9 @@
 //                                                     (A_24(c)^d))
 //   front init    INV[z] = A_z^{-1}(0xFFFFFFFF)      (register value that, after z leading
 //                                                     zero bytes, equals the all-ones init)
-//   half-row fix  M   = A_{-768}                     (8-lane groups in lanes 8..15 of a row
-//                                                     used the lane tables of lanes 8..15)
+//   M   = A_{-768}                                   (unused since round 3: the half-unit
+//                                                     kernel that needed it is gone; kept so the
+//                                                     blob and LDS offsets below stay put)
 //   chunk shifts  C_c = A_{96 c}         c = 0..15   (flat variable-length kernel: a lane's
 //                                                     chunk index is data-dependent, so the
 //                                                     table is indexed by c, not by lane)
@@ -89,9 +90,7 @@ constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
 constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][136] (C_c, LDS order)
 constexpr uint32_t kBlobLaneDma = kBlobFlat + kFlatBytes / 4;   // uint32 [8][16][32]: A_{e_c}
 constexpr uint32_t kBlobMerge = kBlobLaneDma + 8 * 16 * 32;     // uint32 [11][8][16]: A_{8k}, k = 1..11
-constexpr uint32_t kSegLens = kDmaCover - kDmaMinLen + 1;       // segment lengths 1496..1524
-constexpr uint32_t kBlobSegJump = kBlobMerge + 11 * 8 * 16;     // uint32 [Ls][4][8][16]: A_{Ls k}, k = 1..4
-constexpr uint32_t kBlobWords = kBlobSegJump + kSegLens * 4 * 8 * 16;
+constexpr uint32_t kBlobWords = kBlobMerge + 11 * 8 * 16;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -171,12 +170,6 @@ struct Tables {
             for (int t = 0; t < 8; t++)
                 for (int e = 0; e < 16; e++) b[kBlobMerge + (k - 1) * 128 + t * 16 + e] = nt[t][e];
         }
-        for (uint32_t ls = 0; ls < kSegLens; ls++)   // segment jumps of the segmented LDS-DMA kernel
-            for (int k = 1; k <= 4; k++) {
-                nibble_table((long)(kDmaMinLen + ls) * k, nt);
-                for (int t = 0; t < 8; t++)
-                    for (int e = 0; e < 16; e++) b[kBlobSegJump + ls * 512 + (k - 1) * 128 + t * 16 + e] = nt[t][e];
-            }
         return b;
     }
     // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.

@@ -134,7 +134,7 @@ def model_frame(lds, mem: bytes, S: int, L: int):
     return (~v & 0xFFFFFFFF) if L else 0
 
 
-# ---- LDS-DMA fixed kernel (fcs_dma_kernel): LDS16 tables, 6 KiB slots, windows at e_c ----
+# ---- LDS-DMA fixed kernel (fcs_dma_kernel): 32 KiB slice tables, 6 KiB slots, windows at e_c ----
 BLOB_M768 = BLOB_INV + CHUNK
 BLOB_FLAT = BLOB_M768 + 8 * 16
 BLOB_LANE_DMA = BLOB_FLAT + 16 * 544 // 4
@@ -258,109 +258,7 @@ def model_dma_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f
     return out
 
 
-# ---- fcs_dmaseg_kernel (measurement build): equal segments shaped like 1518-B frames ----
-BLOB_SEG_JUMP = BLOB_MERGE + 11 * 8 * 16     # fcs_tables.hpp kBlobSegJump: [Ls - 1496][k - 1][t][e]
-SEG_MIN = 1496
-
-
-def seg_jump(blob, ls, k, s):
-    """A_{ls k}(s), k = 1..4, from the blob's segment-jump nibble tables."""
-    base = BLOB_SEG_JUMP + (ls - SEG_MIN) * 512 + (k - 1) * 128
-    r = 0
-    for t in range(8):
-        r ^= int(blob[base + t * 16 + ((s >> (4 * t)) & 15)])
-    return r
-
-
-def model_segment_value(lds, cover: bytes, zc: int, front: bool, chains=DMA_CHAINS):
-    """The register value of one segment as fcs_dmaseg_kernel's quarter computes it: `cover` is the
-    1524 bytes ending at the segment end (its first zc bytes lie before the segment and are
-    masked by lane 15); the front segment's lane 15 injects INV[zc]."""
-    assert len(cover) == DMA_COVER
-    cl = 24 // chains
-    v = 0
-    for c in range(16):
-        lane = c
-        start = DMA_COVER - dma_end_off(c) - CHUNK
-        w = [int.from_bytes(cover[start + 4 * i:start + 4 * i + 4], "little") for i in range(24)]
-        z = zc if c == 15 else (4 if dma_short_lane(c) else 0)
-        for i in range(8):
-            t = max(0, min(4, z - 4 * i))
-            w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
-        x0 = int(lds[(hole(INV_HOLE + z // 32) + (z % 32) * 4) // 4]) if (c == 15 and front) else 0
-        xs = [w[h * cl] ^ (x0 if h == 0 else 0) for h in range(chains)]
-        for i in range(cl):
-            for h in range(chains):
-                xs[h] = step4_l8(lds, xs[h], lane) ^ (w[h * cl + i + 1] if i < cl - 1 else 0)
-        m = xs[chains - 1]
-        for h in range(chains - 1):
-            m = merge_shift(lds, chains - 2 - h, xs[h]) ^ m
-        lanebase = 128 + (lane & 31) * 4
-        s = 0
-        for t in range(8):
-            sh = (m >> (4 * t - 8)) if 4 * t >= 8 else ((m << (8 - 4 * t)) & 0xFFFFFFFF)
-            s ^= int(lds[(((sh & 0xF00) | lanebase) + t * 4096) // 4])
-        v ^= s
-    return v
-
-
-def model_dmaseg_frame(lds, blob, frame: bytes, garbage: bytes):
-    """FCS of one frame by fcs_dmaseg_kernel's decomposition: m = ceil(len / 1524) segments of
-    Ls = len // m bytes (the remainder in the front one), each a 1524-B cover ending at its
-    segment end, the frame register XOR_s A_{Ls s}(v_s) folded front to back with A_{Ls}."""
-    L = len(frame)
-    m = -(-L // DMA_COVER)
-    ls = L // m
-    lf = L - ls * (m - 1)
-    padded = bytes(garbage[:DMA_COVER]) + frame
-    acc = 0
-    for r in range(m):
-        end = DMA_COVER + lf + ls * r                  # segment end within `padded`
-        seg_len = lf if r == 0 else ls
-        cover = padded[end - DMA_COVER:end]
-        v = model_segment_value(lds, cover, DMA_COVER - seg_len, r == 0)
-        acc = (seg_jump(blob, ls, 1, acc) if r else 0) ^ v
-    return ~acc & 0xFFFFFFFF
-
-
-def seg_place_tables(blob, ls, m):
-    """The kernel's place tables A_{Ls k}, k = 1 .. m - 1, as 8 x 16 nibble tables: k <= 4 from the
-    blob, k >= 5 composed at staging as A_{Ls 4} o A_{Ls (k - 4)}, entry by entry."""
-    tabs = {}
-    for k in range(1, min(m, 5)):
-        base = BLOB_SEG_JUMP + (ls - SEG_MIN) * 512 + (k - 1) * 128
-        tabs[k] = [int(x) for x in blob[base:base + 128]]
-    for k in range(5, m):
-        tabs[k] = [seg_jump(blob, ls, 4, e) for e in tabs[k - 4]]
-    return tabs
-
-
-def apply_nibbles(tab, s):
-    r = 0
-    for t in range(8):
-        r ^= tab[t * 16 + ((s >> (4 * t)) & 15)]
-    return r
-
-
-def model_dmaseg_frame_abs(lds, blob, frame: bytes, garbage: bytes):
-    """FCS of one frame with every segment placed directly: XOR_s A_{Ls s}(v_s), s counted from the
-    frame's last segment, with the place tables of seg_place_tables (no carry to advance)."""
-    L = len(frame)
-    m = -(-L // DMA_COVER)
-    ls = L // m
-    lf = L - ls * (m - 1)
-    tabs = seg_place_tables(blob, ls, m)
-    padded = bytes(garbage[:DMA_COVER]) + frame
-    acc = 0
-    for r in range(m):
-        end = DMA_COVER + lf + ls * r
-        seg_len = lf if r == 0 else ls
-        v = model_segment_value(lds, padded[end - DMA_COVER:end], DMA_COVER - seg_len, r == 0)
-        s_ = m - 1 - r
-        acc ^= apply_nibbles(tabs[s_], v) if s_ else v
-    return ~acc & 0xFFFFFFFF
-
-
+# ---- fcs_segil_kernel: frame-interleaved segments ----
 def model_segil_window_value(lds, win: bytes, lane: int, z: int, x0: int, chains=DMA_CHAINS):
     """One lane window of fcs_segil_kernel (as fcs_dma_kernel's): 96 bytes, the first z masked,
     x0 XORed into chain 0's start; two chains merged, shifted by the lane table A_{e_c}."""

@@ -1,9 +1,9 @@
 """GPU parity of the windowed variable-length path on packed and unpacked arenas.
 
 Windowed batches (more than 16384 frames, and short fixed lengths) take fcs_flat_kernel. The
-measurement-only span-DMA variant (-DFCS_SPAN, fcs_span_kernel) stages each item's
-64 chunks through LDS as one contiguous span when the item's frames are packed and falls back to
-register loads per item when they are not (gaps, offsets out of order, a frame over 1536 B between
+span-DMA variant measured in round 2 (removed) staged each item's 64 chunks
+through LDS as one contiguous span when the item's frames were packed and fell back to register
+loads per item when they were not (gaps, offsets out of order, a frame over 1536 B between
 two others); these tests aim at both sides of that choice and at the span's edges (first frame at
 the arena start, last frame at the arena end, empty and 1-byte frames, frames of exactly k x 96
 bytes, which make the longest spans) and run against either build (NSTACK_FCS_LIB selects the

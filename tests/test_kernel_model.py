@@ -161,44 +161,6 @@ def test_dma_table_lookups_bank_distinct():
             assert len({km.l8_banks(l, xs[l], k) for l in range(32)}) == 32
 
 
-@pytest.mark.parametrize("L", [2992, 3000, 3048, 4488, 4500, 4572, 6000, 7500, 7620])
-def test_dmaseg_decomposition_model(lds_dma, L):
-    """fcs_dmaseg_kernel's (measurement build, superseded by fcs_segil_kernel) split into equal
-    segments shaped like 1518-B frames, with the blob's
-    segment-jump tables A_{Ls k}, reproduces the CRC (zlib = src/ether_fcs.c:4-19); the cover
-    bytes before each segment are random garbage that the masks must remove."""
-    blob = na.tables_blob()
-    rng = np.random.default_rng(L)
-    frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
-    garbage = rng.integers(0, 256, 1524, dtype=np.uint8).tobytes()
-    assert km.model_dmaseg_frame(lds_dma[2], blob, frame, garbage) == zlib.crc32(frame)
-
-
-def test_dmaseg_jump_tables_compose():
-    """A_{Ls k} = A_{Ls}^k for every segment length of the blob (k = 2..4)."""
-    blob = na.tables_blob()
-    rng = np.random.default_rng(9)
-    for ls in (1496, 1500, 1510, 1524):
-        for s in rng.integers(0, 1 << 32, 4, dtype=np.uint64):
-            s = int(s)
-            one = s
-            for k in range(1, 5):
-                one = km.seg_jump(blob, ls, 1, one)
-                assert km.seg_jump(blob, ls, k, s) == one, (ls, k)
-
-
-@pytest.mark.parametrize("L", [3000, 9000, 16500, 41148])
-def test_dmaseg_place_model(lds_dma, L):
-    """The segmented kernel's (measurement build) placement form: each segment shifted by A_{Ls s} for its place s from
-    the frame end (tables for s >= 5 composed from the blob's A_{Ls 4}), the frame the XOR of its
-    placed segments, reproduces the CRC (zlib = src/ether_fcs.c:4-19) up to 27 segments."""
-    blob = na.tables_blob()
-    rng = np.random.default_rng(L + 1)
-    frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
-    garbage = rng.integers(0, 256, 1524, dtype=np.uint8).tobytes()
-    assert km.model_dmaseg_frame_abs(lds_dma[2], blob, frame, garbage) == zlib.crc32(frame)
-
-
 @pytest.mark.parametrize("L", [1525, 1530, 2000, 3048, 3049, 4573, 9000, 10000])
 def test_segil_decomposition_model(lds_dma, L):
     """fcs_segil_kernel's decomposition: a front segment of L - 1524 (m - 1) bytes with per-lane
