@@ -94,6 +94,27 @@ def _load_pmc_traffic(frames: int, L, kernel: str = None):
     return best
 
 
+def _load_kernel_profile(kernel: str, nbytes: int):
+    """The committed rocprofv3 kernel statistics of this command (profiles/rNN_bench_kernel_stats_split.csv,
+    newest round; tools/kernel_stats_split.py): the `kernel` row carrying the most time (the headline
+    launches; the host-inclusive pipeline launches the same kernel on small chunks). Returns the
+    traced average ms per launch and the roofline fraction it gives, beside the in-run HIP-event one."""
+    import csv
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_kernel_stats_split.csv")))
+    if not files:
+        return None
+    best = None
+    for r in csv.DictReader(open(files[-1])):
+        if r["Name"].startswith(kernel) and (best is None or int(r["TotalDurationNs"]) > int(best["TotalDurationNs"])):
+            best = r
+    if best is None:
+        return None
+    ms = float(best["AverageNs"]) / 1e6
+    return {"profile_kernel_ms": round(ms, 4), "profile_median_ms": round(float(best["MedianNs"]) / 1e6, 4),
+            "profile_calls": int(best["Calls"]), "profile_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            "profile_source": os.path.relpath(files[-1], ROOT)}
+
+
 def _time_launches(fn, reps, stream, torch):
     """Average ms per launch from HIP events on the launch stream, after one untimed launch."""
     fn()
@@ -121,9 +142,7 @@ def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
     res = {}
     # ---- configs[2]: 128 M IMIX frames, 7:4:1 of 64/576/1518 in exact counts, shuffled, packed ----
     n = 128 << 20
-    counts = [78293676, 44739242, 11184810]
-    ln_np = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), counts)
-    np.random.default_rng(7).shuffle(ln_np)
+    ln_np = imix_lengths(n)   # 78293676 / 44739242 / 11184810 frames of 64 / 576 / 1518 B
     ln = torch.from_numpy(ln_np.view(np.int32)).to(dev)
     off = torch.zeros(n, dtype=torch.int64, device=dev)
     off[1:] = torch.cumsum(ln[:-1].to(torch.int64), 0)
@@ -214,7 +233,154 @@ def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
                                       "spot_checked": len(idx), "spot_bad": bad}
         del pinned, hout
         lib.fcs_host_free(p)
+    # ---- host-inclusive IMIX: the same 7:4:1 mix in pinned host memory, offsets and lengths in
+    #      pageable host arrays, through ether_fcs_batch_host (north_star: "the rate including the
+    #      copies to and from the GPU") ----
+    res["host_inclusive_imix"] = host_inclusive_imix(torch, na, dev, stream, rng, host_gib)
     return res
+
+
+def imix_lengths(n: int, seed: int = 7):
+    """BASELINE configs[2]: n frames of 64/576/1518 B in exact 7:4:1 proportions, shuffled."""
+    import numpy as np
+    c1518 = n // 12
+    c576 = (n * 4) // 12
+    c64 = n - c576 - c1518
+    ln = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), [c64, c576, c1518])
+    np.random.default_rng(seed).shuffle(ln)
+    return ln
+
+
+def host_inclusive_imix(torch, na, dev, stream, rng, host_gib=4.0):
+    """IMIX frames packed in a pinned host arena (fcs_host_alloc) -> ether_fcs_batch_host (chunked H2D
+    of frames + offsets + lengths -> flat kernel -> D2H of the CRCs). Ceiling: plain async H2D copies
+    of the same pinned arena plus the 12 B of metadata per frame, same process."""
+    import numpy as np
+    n = int(host_gib * GIB / 355.83)   # frames whose mean length is 4270 / 12 B
+    ln = imix_lengths(n, seed=11)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1], dtype=np.uint64, out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    lib = na.load()
+    p = lib.fcs_host_alloc(total)
+    if not p:
+        return None
+    try:
+        pinned = np.ctypeslib.as_array((ctypes.c_uint8 * total).from_address(p))
+        d = torch.empty(total, dtype=torch.uint8, device=dev)
+        na.fill_splitmix_dev(d, total, SEED + 5, 0, stream)
+        torch.cuda.synchronize()
+        pinned[:] = d.cpu().numpy()
+        del d
+        torch.cuda.empty_cache()
+        out = np.zeros(n, dtype=np.uint32)
+        m = min(n, 1 << 16)
+        na.batch_host(p, int(off[m - 1]) + int(ln[m - 1]), off[:m], ln[:m], out[:m], m)   # pipeline buffers, untimed
+        t0 = time.perf_counter()
+        na.batch_host(p, total, off, ln, out, n)
+        secs = time.perf_counter() - t0
+        idx = rng.integers(0, n, 128)
+        bad = _spot(out, lambda i: pinned[int(off[i]):int(off[i]) + int(ln[i])].tobytes(), idx)
+        src = torch.from_numpy(pinned)
+        meta = torch.from_numpy(np.concatenate([off.view(np.uint8), ln.view(np.uint8)])).pin_memory()
+        chunk = min(total, int(GIB))
+        dbuf = torch.empty(chunk, dtype=torch.uint8, device=dev)
+        dmeta = torch.empty(meta.numel(), dtype=torch.uint8, device=dev)
+        dbuf.copy_(src[:chunk], non_blocking=True)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for o in range(0, total, chunk):
+            k = min(chunk, total - o)
+            dbuf[:k].copy_(src[o:o + k], non_blocking=True)
+        dmeta.copy_(meta, non_blocking=True)
+        torch.cuda.synchronize()
+        copy_secs = time.perf_counter() - t0
+        del dbuf, dmeta, src, meta
+        torch.cuda.empty_cache()
+        gbs = total / secs / 1e9
+        return {"what": "IMIX frames in pinned host memory + offsets/lengths in pageable host arrays -> "
+                        "ether_fcs_batch_host (chunked H2D -> flat kernel -> D2H of CRCs); PCIe bound, never `value`",
+                "frames": n, "bytes": total, "metadata_bytes": n * 12, "ms": round(secs * 1e3, 3),
+                "GB_s": round(gbs, 2), "Mframes_s": round(n / secs / 1e6, 1),
+                "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": 63.0, "unit": "GB/s",
+                             "frac": round(gbs / 63.0, 4),
+                             "h2d_copy_s": round(copy_secs, 4),
+                             "frac_of_h2d_copy": round(copy_secs / secs, 4),
+                             "h2d_copy_what": "plain async copies of the pinned arena (1 GiB pieces) plus the "
+                                              "pinned offsets and lengths, same process"},
+                "spot_checked": len(idx), "spot_bad": bad}
+    finally:
+        lib.fcs_host_free(p)
+
+
+def imix_shard(world: int, rank: int, n_blk: int):
+    """Host side of imix_sharded: rank's contiguous frame range [lo, hi) of the global IMIX stream
+    (`world` blocks of n_blk frames) from fcs_shard_plan over the global lengths, the shard's lengths
+    and offsets (packed, from 0), the global byte position of its first byte, and its byte count."""
+    import numpy as np
+    blk = imix_lengths(n_blk)
+    blk_bytes = int(blk.sum(dtype=np.uint64))
+    glob_len = np.tile(blk, world)
+    lo, hi = shard_range(len(glob_len), world, rank, glob_len)
+    del glob_len
+    idx = np.arange(lo, hi, dtype=np.int64) % n_blk
+    ln_np = blk[idx]
+    del idx
+    q, r = divmod(lo, n_blk)
+    byte0 = q * blk_bytes + int(blk[:r].sum(dtype=np.uint64))
+    off_np = np.zeros(hi - lo, dtype=np.uint64)
+    if hi - lo > 1:
+        np.cumsum(ln_np[:-1], dtype=np.uint64, out=off_np[1:])
+    total = int(off_np[-1]) + int(ln_np[-1]) if hi > lo else 0
+    return lo, hi, ln_np, off_np, byte0, total
+
+
+def imix_sharded(torch, na, dev, stream, world: int, rank: int, dist, n_blk: int = 128 << 20, reps: int = 5):
+    """BASELINE configs[2] per GPU at N > 1 (weak scaling): the global stream is `world` blocks of n_blk
+    IMIX frames (64/576/1518 B, 7:4:1, shuffled), packed. Each rank takes its byte-balanced contiguous
+    shard from the engine's planner (fcs_shard_plan over the global lengths), fills it with its slice
+    of one global byte stream, and times `reps` launches of ether_fcs_batch_dev with HIP events on its
+    stream; rank 0 reports the aggregate (all ranks' bytes / the slowest rank's time). Only the
+    barrier, the max and two integer sums cross ranks (gloo)."""
+    import numpy as np
+    lo, hi, ln_np, off_np, byte0, total = imix_shard(world, rank, n_blk)
+    n = hi - lo
+    arena = torch.empty(total, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, total, SEED + 2, byte0, stream)
+    off = torch.from_numpy(off_np.view(np.int64)).to(dev)
+    ln = torch.from_numpy(ln_np.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    na.batch_dev(arena, total, off, ln, out, n, stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    t0 = time.perf_counter()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        na.batch_dev(arena, total, off, ln, out, n, stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    dist.barrier()
+    wall = time.perf_counter() - t0
+    kms = e0.elapsed_time(e1) / reps
+    rng = np.random.default_rng(100 + rank)
+    pick = rng.integers(0, n, 64)
+    crcs = out.cpu().numpy().view(np.uint32)
+    bad = _spot(crcs, lambda i: splitmix_bytes(SEED + 2, byte0 + int(off_np[i]), int(ln_np[i])).tobytes(), pick)
+    agg = torch.tensor([total, n, bad], dtype=torch.int64)
+    dist.all_reduce(agg)
+    tmax = torch.tensor([wall], dtype=torch.float64)
+    dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    del arena, off, ln, out
+    torch.cuda.empty_cache()
+    all_bytes, all_frames, all_bad = (int(x) for x in agg.tolist())
+    t = float(tmax.item()) / reps
+    return {"config": "BASELINE configs[2] per GPU, weak scaling", "frames_per_block": n_blk, "blocks": world,
+            "global_frames": all_frames, "global_bytes": all_bytes, "ms_per_step_max_rank": round(t * 1e3, 4),
+            "GB_s_aggregate": round(all_bytes / t / 1e9, 1), "rank0_kernel_ms": round(kms, 4),
+            "rank0_frames": n, "rank0_bytes": total,
+            "sharding": "fcs_shard_plan byte-balanced over the global lengths (contiguous ranges)",
+            "spot_checked": 64 * world, "spot_bad": all_bad}
 
 
 def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
@@ -298,7 +464,9 @@ def main():
     ap.add_argument("--len", type=int, default=1518)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--no-verify", action="store_true")
-    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs (N = 1 only)")
+    ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs")
+    ap.add_argument("--imix-frames-per-gpu", type=int, default=128 << 20,
+                    help="N > 1: IMIX frames per GPU of the sharded configs[2] run (0 = skip)")
     args = ap.parse_args()
 
     import numpy as np
@@ -420,6 +588,9 @@ def main():
                 "frac_of_read_stream": round(achieved_gbs / read_gbs, 4),
                 "dma_stream_gbs": round(dma_gbs, 1),
                 "frac_of_dma_stream": round(achieved_gbs / dma_gbs, 4)}
+    prof = _load_kernel_profile("void fcs::fcs_dma_kernel<2, false>", nbytes) if L == 1518 and F == 64 << 20 else None
+    if prof:   # the committed trace of this command (another box, under the tracer): box spread in DESIGN §4.2
+        roofline.update(prof)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu:
@@ -435,6 +606,11 @@ def main():
                 rf["frac_of_read_stream"] = round(rf["achieved"] / read_gbs, 4)
                 rf["frac_of_dma_stream"] = round(rf["achieved"] / dma_gbs, 4)
 
+    if dist and not args.no_configs and args.imix_frames_per_gpu > 0:
+        del arena, out
+        torch.cuda.empty_cache()
+        configs = {"imix_sharded": imix_sharded(torch, na, dev, stream, world, rank, dist,
+                                                n_blk=args.imix_frames_per_gpu)}
     if dist:
         dist.barrier()
     if rank == 0:

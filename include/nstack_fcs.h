@@ -23,12 +23,14 @@
  *
  * Errors: the batch/device entry points return 0 on success or a negative errno
  * (-EINVAL bad arguments, -ENODEV no usable GPU / HIP code object missing, -ENOMEM,
- * -EIO a HIP runtime error; fcs_last_error() has the text). There is NO CPU fallback:
- * without a GPU the engine fails loudly. ether_fcs() has no error channel in the
- * reference (it cannot fail there): a failed attempt (HIP error, lost completion, timeout)
- * drops that lane's stream and result word and is retried once on a fresh lane; only if the
- * retry fails too does it print the reason to stderr and abort rather than return a wrong FCS
- * (fcs_engine_stats counts calls, retries and recoveries).
+ * -EIO a HIP runtime error; fcs_last_error() has the text). These entry points have NO CPU
+ * fallback: without a GPU they fail loudly. ether_fcs() has no error channel in the reference
+ * (it cannot fail there): a failed attempt (HIP error, lost completion, timeout)
+ * quarantines that lane's stream and result word and is retried once on a fresh lane; if the
+ * retry fails too, or bsize >= 4 GiB (the kernels take 32-bit lengths), the call is answered by
+ * the library's own host CRC instead of aborting, so the result never differs from the
+ * reference. Each such call is counted (fcs_engine_host_fallbacks) and the first one is reported
+ * on stderr; fcs_engine_stats counts calls, retries and recoveries.
  *
  * Threading: every entry point is thread-safe and may be called concurrently (the reference
  * calls ether_fcs from the main, ingress, egress and TCP-timer threads: SURVEY.md §8b).
@@ -65,6 +67,9 @@ uint64_t fcs_engine_set_var_threshold(uint64_t frames);
  * succeeded, and lanes (stream + result word) dropped after a failure. Any pointer may be NULL. */
 void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t *dropin_recovered,
                       uint64_t *lane_resets);
+/* Drop-in calls answered by the host CRC because the GPU path failed twice or bsize >= 4 GiB
+ * (0 on a healthy GPU: the GPU test suite asserts it). */
+uint64_t fcs_engine_host_fallbacks(void);
 /* Host batch paths: calls that were split over more than one engine device, and the shard jobs
  * those calls ran (one host thread and pipeline each). Any pointer may be NULL. */
 void fcs_engine_host_stats(uint64_t *sharded_calls, uint64_t *shard_jobs);

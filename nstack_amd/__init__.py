@@ -22,7 +22,7 @@ __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fi
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
@@ -88,6 +88,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_timed_fixed_dev": (i32, [vp, u64, u32, u64, vp, vp, i32, c.POINTER(c.c_float)]),
         "fcs_tables_blob": (i32, [vp, u64]),
         "fcs_engine_stats": (None, [c.POINTER(u64)] * 4),
+        "fcs_engine_host_fallbacks": (u64, []),
         "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
@@ -270,8 +271,11 @@ def engine_stats() -> dict:
     """Drop-in ether_fcs health counters (fcs_engine_stats)."""
     import ctypes as c
     v = [c.c_uint64(0) for _ in range(4)]
-    load().fcs_engine_stats(*[c.byref(x) for x in v])
-    return dict(zip(("dropin_calls", "dropin_retries", "dropin_recovered", "lane_resets"), (x.value for x in v)))
+    L = load()
+    L.fcs_engine_stats(*[c.byref(x) for x in v])
+    d = dict(zip(("dropin_calls", "dropin_retries", "dropin_recovered", "lane_resets"), (x.value for x in v)))
+    d["host_fallbacks"] = int(L.fcs_engine_host_fallbacks())   # drop-in calls the host CRC answered
+    return d
 
 
 def engine_host_stats() -> dict:

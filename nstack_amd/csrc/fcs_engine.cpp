@@ -3,9 +3,11 @@
 // Replaces ether_fcs() (/root/reference/src/ether_fcs.c:4-19, prototype src/nstack_ether.h:80)
 // and provides the batched forms its TX call site (src/linux/ether.c:262-263) needs.
 // Per-device state (constant tables in HBM, staging buffers, streams) is created lazily and is
-// safe to use from many threads. There is deliberately no CPU CRC path in this library: every
-// FCS is computed by the HIP kernel, and a missing GPU or code object is reported as an error
-// (or, for the error-less drop-in ether_fcs, an abort with the reason on stderr).
+// safe to use from many threads. Every batch and device entry point computes on the GPU only: a
+// missing GPU or code object is reported as -errno. The one exception is the error-less drop-in
+// ether_fcs, whose reference cannot fail: after the GPU attempt and its retry on a
+// fresh lane have both failed, it returns the host CRC of fcs_host_crc.cpp (counted, announced on
+// stderr) instead of aborting.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -22,10 +24,12 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <initializer_list>
 
 #include "../../include/nstack_fcs.h"
 #include "fcs_device.hpp"
 #include "fcs_error.hpp"
+#include "fcs_host_crc.hpp"
 #include "fcs_launch.hpp"
 #include "fcs_tables.hpp"
 
@@ -77,6 +81,7 @@ struct DeviceGuard {
 
 // Drop-in ether_fcs health counters (fcs_engine_stats).
 std::atomic<uint64_t> g_dropin_calls{0}, g_dropin_retries{0}, g_dropin_recovered{0}, g_lane_resets{0};
+std::atomic<uint64_t> g_host_fallbacks{0};   // drop-in calls answered by the host CRC (fcs_host_crc.cpp)
 
 #ifdef FCS_FAULT_HOOK
 // Test-only build (libnstack_fcs_faults.so): the calling thread's next N drop-in attempts fail as
@@ -87,8 +92,17 @@ bool injected_fault() {
     g_inject_faults--;
     return true;
 }
+// ... and the next N single-frame attempts give up right after the launch, as if the 10 s wait had
+// run out, while their kernel is still in flight (the quarantine path).
+thread_local int g_inject_timeouts = 0;
+bool injected_timeout() {
+    if (g_inject_timeouts <= 0) return false;
+    g_inject_timeouts--;
+    return true;
+}
 #else
 inline bool injected_fault() { return false; }
+inline bool injected_timeout() { return false; }
 #endif
 
 // Double-buffered host pipeline resources of one device.
@@ -115,9 +129,20 @@ struct DevState {
     uint32_t *d_kinit = nullptr;      // kinit_table() in device memory (mapped-list kernel)
     // Dynamic-tail counters of the LDS-DMA kernel: a ring of kCtrSlots, one 64-B line each; a
     // large fixed launch takes the next slot and zeroes it on its own stream before the kernel.
+    // A slot is reused only after the kernel that last used it has finished: the reuser's stream
+    // waits for that kernel's completion event before zeroing the slot (ctr_mu[slot] is held from
+    // taking the slot until the event is recorded behind the new launch).
     static constexpr uint32_t kCtrSlots = 256;
     unsigned long long *d_ctr = nullptr;
     std::atomic<uint32_t> ctr_seq{0};
+    std::mutex ctr_mu[kCtrSlots];
+    hipEvent_t ctr_done[kCtrSlots] = {};
+    // Streams and mapped result words of drop-in lanes given up while a kernel may still be in
+    // flight on them (timeout, lost completion, device error): never reused or freed before
+    // fcs_engine_fini, so a late kernel cannot write into memory that serves another call.
+    std::mutex q_mu;
+    std::vector<hipStream_t> q_streams;
+    std::vector<void *> q_host;
     std::mutex pipe_mu;      // one host pipeline at a time per device
     Pipe pipe;
     std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
@@ -294,9 +319,34 @@ std::atomic<uint64_t> g_var_threshold{16384};
 constexpr uint32_t kFixedFlatMaxLen = FCS_FIXED_FLAT_MAX;
 
 // A zeroed work counter for one launch (Dispenser in fcs_kernel.hip): the next slot of the
-// device's ring, cleared on the launch's own stream just before the kernel.
-int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p) {
+// device's ring, cleared on the launch's own stream just before the kernel, after the slot's
+// previous kernel (on any stream) has finished. The lease holds the slot until the new launch's
+// completion event is recorded (CounterLease::~CounterLease, after the launch).
+struct CounterLease {
+    DevState *ds = nullptr;
+    hipStream_t st = nullptr;
+    int slot = -1;
+    CounterLease() = default;
+    CounterLease(const CounterLease &) = delete;
+    CounterLease &operator=(const CounterLease &) = delete;
+    ~CounterLease() {
+        if (slot < 0) return;
+        (void)hipEventRecord(ds->ctr_done[slot], st);
+        ds->ctr_mu[slot].unlock();
+    }
+};
+
+int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p, CounterLease &lease) {
     const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
+    ds->ctr_mu[slot].lock();
+    lease.ds = ds;
+    lease.st = st;
+    lease.slot = (int)slot;
+    if (!ds->ctr_done[slot]) {
+        HIPTRY(hipEventCreateWithFlags(&ds->ctr_done[slot], hipEventDisableTiming), "hipEventCreate(counter)");
+    } else {
+        HIPTRY(hipStreamWaitEvent(st, ds->ctr_done[slot], 0), "waiting for the counter slot's last kernel");
+    }
     p.ctr = ds->d_ctr + 8 * slot;
     HIPTRY(hipMemsetAsync(p.ctr, 0, 8, st), "zeroing the work counter");
     return 0;
@@ -318,6 +368,7 @@ constexpr uint64_t kFixedDynMinUnitsPerWave = FCS_FIXED_DYN_MIN;
 
 int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
                  uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
+    CounterLease lease;   // declared first: released (event recorded) after the launch below
     fcs::KParams p{};
     p.ok = ok;
     p.bad = bad;
@@ -338,7 +389,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         p.zmax = fcs::kChunkBytes;
         const int fgrid = grid_for(ds, n, fcs::kWgThreads);
         if ((n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)fgrid * (fcs::kWgThreads / 64)) {
-            const int rc = take_counter(ds, st, p);
+            const int rc = take_counter(ds, st, p, lease);
             if (rc) return rc;
         }
         HIPTRY(fcs::launch_fcs(true, true, p, fgrid, st), "launching fcs_flat_kernel<fixed>");
@@ -349,20 +400,20 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
         const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
         if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic schedule
-            const int rc = take_counter(ds, st, p);
+            const int rc = take_counter(ds, st, p, lease);
             if (rc) return rc;
         }
     } else if (fcs::fixed_segil(p)) {   // frame-interleaved segments: units of 4 frames
         const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kSegilWgThreads / 64);
         if (units >= kFixedDynMinUnitsPerWave * waves) {
-            const int rc = take_counter(ds, st, p);
+            const int rc = take_counter(ds, st, p, lease);
             if (rc) return rc;
         }
     } else if (!fcs::fixed_tiny(p) && !fcs::fixed_single(p)) {
         // generic kernel: units of 4 frames (one per quarter-wave), dynamic for large batches
         const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);
         if (units >= kFixedDynMinUnitsPerWave * waves) {
-            const int rc = take_counter(ds, st, p);
+            const int rc = take_counter(ds, st, p, lease);
             if (rc) return rc;
         }
     }
@@ -374,6 +425,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
 int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint64_t *off,
                const uint32_t *len, uint32_t *out, uint64_t n, hipStream_t st, uint8_t *ok = nullptr,
                unsigned long long *bad = nullptr, uint64_t stride = 0) {
+    CounterLease lease;
     fcs::KParams p{};
     p.ok = ok;
     p.bad = bad;
@@ -390,7 +442,7 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     const bool windowed = n > g_var_threshold.load(std::memory_order_relaxed);
     const int grid = grid_for(ds, n, fcs::kWgThreads);
     if (windowed && (n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)grid * (fcs::kWgThreads / 64)) {
-        const int rc = take_counter(ds, st, p);
+        const int rc = take_counter(ds, st, p, lease);
         if (rc) return rc;
     }
     HIPTRY(fcs::launch_fcs(true, windowed, p, grid, st), "launching fcs_kernel<var>");
@@ -738,12 +790,20 @@ uint32_t my_lane() {
     return me % DevState::kOneLanes;
 }
 
+// Set aside a stream and pinned words that a kernel may still use: neither destroyed nor freed
+// (hipHostFree could block behind a hung kernel, and a late kernel must not write into a word that
+// serves another call by then) until fcs_engine_fini.
+void quarantine(DevState *ds, hipStream_t st, std::initializer_list<void *> host) {
+    std::lock_guard<std::mutex> lk(ds->q_mu);
+    if (st) ds->q_streams.push_back(st);
+    for (void *h : host)
+        if (h) ds->q_host.push_back(h);
+}
+
 // Drop a lane whose last call failed: its stream and result word are recreated on next use, so a
 // stream left in an error state or a result word a stuck kernel may still write is never reused.
 void reset_lane(DevState *ds, DevState::OneLane &L) {
-    DeviceGuard dg(ds->dev);
-    if (L.st) (void)hipStreamDestroy(L.st);
-    if (L.flag) (void)hipHostFree(L.flag);
+    quarantine(ds, L.st, {L.flag});
     L.st = nullptr;
     L.flag = L.dflag = nullptr;
     L.seq = 0;
@@ -786,6 +846,10 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc, uint32_
         if ((uint32_t)(v >> 32) == a.seq) {
             *crc = (uint32_t)v;
             return 0;
+        }
+        if (i == 1 && injected_timeout()) {   // FCS_FAULT_HOOK builds only: give up with the kernel in flight
+            reset_lane(ds, L);
+            return fail(ETIMEDOUT, "single-frame kernel: injected timeout (FCS_FAULT_HOOK build)");
         }
         __builtin_ia32_pause();
         if ((i & 4095) == 0) {
@@ -967,10 +1031,8 @@ int run_staged(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
     std::lock_guard<std::mutex> lk(ds->one_mu);
     DeviceGuard dg(ds->dev);
     HIPTRY(dg.err, "hipSetDevice");
-    auto reset = [ds] {
-        if (ds->one_stream) (void)hipStreamDestroy(ds->one_stream);
-        if (ds->one_hout) (void)hipHostFree(ds->one_hout);
-        if (ds->one_flag) (void)hipHostFree(ds->one_flag);
+    auto reset = [ds] {   // the staging buffer one_h is kept: no kernel writes it
+        quarantine(ds, ds->one_stream, {ds->one_hout, ds->one_flag});
         ds->one_stream = nullptr;
         ds->one_hout = ds->one_dout = nullptr;
         ds->one_flag = ds->one_dflag = nullptr;
@@ -1145,6 +1207,52 @@ int fcs::set_error(int err, const char *fmt, ...) {
     return -err;
 }
 
+// Release everything a device state holds (engine shutdown, or an alias state that is no longer an
+// engine device). Caller holds g_mu.
+static void destroy_state(DevState *ds) {
+    hipSetDevice(ds->dev);
+    Pipe &pp = ds->pipe;
+    for (int b = 0; b < Pipe::kDepth; b++) {
+        if (pp.done[b]) hipEventDestroy(pp.done[b]);
+        if (pp.d_in[b]) hipFree(pp.d_in[b]);
+        if (pp.h_in[b]) hipHostFree(pp.h_in[b]);
+        if (pp.d_off[b]) hipFree(pp.d_off[b]);
+        if (pp.d_len[b]) hipFree(pp.d_len[b]);
+        if (pp.d_out[b]) hipFree(pp.d_out[b]);
+        if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
+        if (pp.h_len[b]) hipHostFree(pp.h_len[b]);
+        if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
+    }
+    if (pp.stream) hipStreamDestroy(pp.stream);
+    if (ds->tx_stream) hipStreamDestroy(ds->tx_stream);
+    if (ds->tx_len) hipHostFree(ds->tx_len);
+    if (ds->tx_out) hipHostFree(ds->tx_out);
+    if (ds->tx_off) hipHostFree(ds->tx_off);
+    if (ds->tx_flag) hipHostFree(ds->tx_flag);
+    if (ds->tx_dcount) hipFree(ds->tx_dcount);
+    if (ds->vz_off) hipHostFree(ds->vz_off);
+    if (ds->vz_len) hipHostFree(ds->vz_len);
+    if (ds->vz_ok) hipHostFree(ds->vz_ok);
+    if (ds->vz_dbad) hipFree(ds->vz_dbad);
+    if (ds->one_stream) hipStreamDestroy(ds->one_stream);
+    if (ds->one_h) hipHostFree(ds->one_h);
+    if (ds->one_hout) hipHostFree(ds->one_hout);
+    if (ds->one_flag) hipHostFree(ds->one_flag);
+    for (DevState::OneLane &L : ds->one_lane) {
+        if (L.st) hipStreamDestroy(L.st);
+        if (L.flag) hipHostFree(L.flag);
+    }
+    if (!ds->q_streams.empty() || !ds->q_host.empty()) (void)hipDeviceSynchronize();
+    for (hipStream_t q : ds->q_streams) hipStreamDestroy(q);
+    for (void *h : ds->q_host) hipHostFree(h);
+    for (hipEvent_t ev : ds->ctr_done)
+        if (ev) hipEventDestroy(ev);
+    if (ds->d_blob) hipFree(ds->d_blob);
+    if (ds->d_one_blob) hipFree(ds->d_one_blob);
+    if (ds->d_kinit) hipFree(ds->d_kinit);
+    if (ds->d_ctr) hipFree(ds->d_ctr);
+}
+
 extern "C" {
 
 const char *fcs_last_error(void) { return g_last_error.c_str(); }
@@ -1164,6 +1272,16 @@ int fcs_engine_init(int ndev) {
         std::lock_guard<std::mutex> lk(g_mu);
         g_engine_devs.clear();
         for (int d = 0; d < use; d++) g_engine_devs.push_back(d);
+        // alias states (NSTACK_FCS_ALIAS_DEVICES test hook) of ids that are no longer engine
+        // devices are released now, not at fcs_engine_fini
+        for (auto it = g_alias.begin(); it != g_alias.end();) {
+            if (it->first >= use) {
+                destroy_state(it->second.get());
+                it = g_alias.erase(it);
+            } else {
+                ++it;
+            }
+        }
     }
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
@@ -1175,49 +1293,10 @@ void fcs_engine_fini(void) {
     std::lock_guard<std::mutex> lk(g_mu);
     int cur = 0;
     (void)hipGetDevice(&cur);
-    std::vector<DevState *> all;
     for (auto &up : g_dev)
-        if (up) all.push_back(up.get());
+        if (up) destroy_state(up.get());
     for (auto &kv : g_alias)
-        if (kv.second) all.push_back(kv.second.get());
-    for (DevState *ds : all) {
-        hipSetDevice(ds->dev);
-        Pipe &pp = ds->pipe;
-        for (int b = 0; b < Pipe::kDepth; b++) {
-            if (pp.done[b]) hipEventDestroy(pp.done[b]);
-            if (pp.d_in[b]) hipFree(pp.d_in[b]);
-            if (pp.h_in[b]) hipHostFree(pp.h_in[b]);
-            if (pp.d_off[b]) hipFree(pp.d_off[b]);
-            if (pp.d_len[b]) hipFree(pp.d_len[b]);
-            if (pp.d_out[b]) hipFree(pp.d_out[b]);
-            if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
-            if (pp.h_len[b]) hipHostFree(pp.h_len[b]);
-            if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
-        }
-        if (pp.stream) hipStreamDestroy(pp.stream);
-        if (ds->tx_stream) hipStreamDestroy(ds->tx_stream);
-        if (ds->tx_len) hipHostFree(ds->tx_len);
-        if (ds->tx_out) hipHostFree(ds->tx_out);
-        if (ds->tx_off) hipHostFree(ds->tx_off);
-        if (ds->tx_flag) hipHostFree(ds->tx_flag);
-        if (ds->tx_dcount) hipFree(ds->tx_dcount);
-        if (ds->vz_off) hipHostFree(ds->vz_off);
-        if (ds->vz_len) hipHostFree(ds->vz_len);
-        if (ds->vz_ok) hipHostFree(ds->vz_ok);
-        if (ds->vz_dbad) hipFree(ds->vz_dbad);
-        if (ds->one_stream) hipStreamDestroy(ds->one_stream);
-        if (ds->one_h) hipHostFree(ds->one_h);
-        if (ds->one_hout) hipHostFree(ds->one_hout);
-        if (ds->one_flag) hipHostFree(ds->one_flag);
-        for (DevState::OneLane &L : ds->one_lane) {
-            if (L.st) hipStreamDestroy(L.st);
-            if (L.flag) hipHostFree(L.flag);
-        }
-        if (ds->d_blob) hipFree(ds->d_blob);
-        if (ds->d_one_blob) hipFree(ds->d_one_blob);
-        if (ds->d_kinit) hipFree(ds->d_kinit);
-        if (ds->d_ctr) hipFree(ds->d_ctr);
-    }
+        if (kv.second) destroy_state(kv.second.get());
     g_dev.clear();
     g_alias.clear();
     g_engine_devs.clear();
@@ -1371,17 +1450,23 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
 
 // Drop-in for src/ether_fcs.c:4. Synchronous, reentrant. The reference cannot fail and has no
 // error channel (SURVEY.md §8b Errors), so an attempt that fails (HIP error, lost completion,
-// 10 s timeout) is retried once: the failed lane's stream and result word are dropped and the
-// frame goes through the next lane, freshly created. Only when the retry fails too (no GPU, a
-// sticky device error) does the call print the reason and abort — never return a wrong FCS.
-// There is no CPU CRC path to fall back to. Counters: fcs_engine_stats.
+// 10 s timeout) is retried once: the failed lane's stream and result word are quarantined and the
+// frame goes through the next lane, freshly created. When the retry fails too (no GPU, a sticky
+// device error), or the buffer is too long for the kernels' 32-bit frame lengths, the call is
+// answered by the host CRC (fcs_host_crc.cpp): counted in fcs_engine_host_fallbacks and reported
+// on stderr the first time, never a wrong FCS and never an abort. Counters: fcs_engine_stats.
 uint32_t ether_fcs(const void *data, size_t bsize) {
     if (bsize == 0) return 0;   // src/ether_fcs.c: the loop does not run, crc stays 0
     g_dropin_calls.fetch_add(1, std::memory_order_relaxed);
-    if (bsize > 0xFFFFFFFFull) {   // the kernels take 32-bit frame lengths; never truncate
-        std::fprintf(stderr, "nstack_fcs: ether_fcs: %zu-byte buffer exceeds the 4 GiB frame limit\n", bsize);
-        std::abort();
-    }
+    auto host = [&](const char *why) {
+        static std::atomic<bool> told{false};
+        if (!told.exchange(true))
+            std::fprintf(stderr, "nstack_fcs: ether_fcs: %s; answering from the host CRC (counted in "
+                                 "fcs_engine_host_fallbacks; reported once)\n", why);
+        g_host_fallbacks.fetch_add(1, std::memory_order_relaxed);
+        return fcs::host_crc32(data, bsize);
+    };
+    if (bsize > 0xFFFFFFFFull) return host("buffer of 4 GiB or more (the kernels take 32-bit frame lengths)");
     const uint32_t lane = my_lane();
     uint32_t c = 0;
     if (dropin_attempt(data, bsize, lane, &c) == 0) return c;
@@ -1392,10 +1477,12 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
         g_last_error = "ether_fcs recovered after: " + first;
         return c;
     }
-    std::fprintf(stderr, "nstack_fcs: ether_fcs: %s (first attempt: %s); no usable GPU engine, aborting\n",
-                 g_last_error.c_str(), first.c_str());
-    std::abort();
+    const std::string why = "no usable GPU engine (" + g_last_error + "; first attempt: " + first + ")";
+    g_last_error = "ether_fcs answered by the host CRC after: " + why;
+    return host(why.c_str());
 }
+
+uint64_t fcs_engine_host_fallbacks(void) { return g_host_fallbacks.load(std::memory_order_relaxed); }
 
 void fcs_engine_host_stats(uint64_t *sharded_calls, uint64_t *shard_jobs) {
     if (sharded_calls) *sharded_calls = g_sharded_calls.load(std::memory_order_relaxed);
@@ -1412,6 +1499,7 @@ void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t
 
 #ifdef FCS_FAULT_HOOK
 void fcs_debug_fail_next(int attempts) { g_inject_faults = attempts; }
+void fcs_debug_timeout_next(int attempts) { g_inject_timeouts = attempts; }
 #endif
 
 int fcs_shard_plan(const uint32_t *len, uint64_t n, uint32_t parts, uint64_t *cut) {
@@ -1492,7 +1580,8 @@ int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stre
     k.out = sink;
     const hipStream_t st = (hipStream_t)stream;
     const int grid = grid_for(ds, k.n, fcs::kDmaWgThreads);
-    if ((rc = take_counter(ds, st, k))) return rc;
+    CounterLease lease;
+    if ((rc = take_counter(ds, st, k, lease))) return rc;
     HIPTRY(fcs::launch_dma_stream(k, grid, st), "launching the LDS-DMA read stream");
     return 0;
 }

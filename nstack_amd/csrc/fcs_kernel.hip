@@ -164,7 +164,8 @@ __device__ __forceinline__ Item frame_item(const KParams &p, uint64_t f) {
 }
 
 // Raw loads of one lane chunk (issued one item ahead of their use) and what is needed to
-// interpret them. Loads are unconditional and stay inside [lo4, hi4): lanes with nothing to load
+// interpret them. The register-load kernels' loads are unconditional and stay inside [lo4, hi4)
+// (the LDS-DMA kernels read whole 16-B pieces instead: fcs_dma_kernel): lanes with nothing to load
 // read lo4; a window that starts before lo4 (front lane of a frame at the very start of the
 // arena) is moved up to lo4 in a wave-uniform branch and shifted back after the data has landed
 // (process()).
@@ -303,6 +304,7 @@ struct Dispenser {
     uint64_t U, W, wid, Is, Ks;
     uint64_t k = 0, ce = 0, pend = 0, psize = 0, seen = 0;
     uint32_t cmin, cmax;
+    uint32_t align = 1;   // chunks of at least `align` units are cut to multiples of it (aligned result runs)
     int lane;
     bool dyn = false;
 
@@ -316,6 +318,7 @@ struct Dispenser {
         const uint64_t left = U - Is > seen ? U - Is - seen : 0;
         uint64_t sz = left / (2 * W);
         sz = sz < cmin ? cmin : (sz > cmax ? cmax : sz);
+        if (sz >= align) sz -= sz % align;
         uint64_t v = 0;
         if (lane == 0) v = atomicAdd(ctr, (unsigned long long)sz);
         pend = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(v >> 32)) << 32) |
@@ -968,6 +971,9 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     const uint32_t x0 = (c == kGroup - 1) ? lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zc / 32u) + (uint32_t)(zc % 32) * 4u)
                                           : 0u;
 
+    // Slots are whole 16-B pieces: reads stay inside [floor16(lo4), ceil16(hi4)), i.e. up to 12 bytes
+    // before the arena's first and after its last dword (never across a page: pages are 4 KiB
+    // aligned). Those bytes land in the slot but lie outside every window's frame bytes.
     const uint64_t lo16 = p.lo4 & ~15ull;
     const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kDmaItemBytes;   // last slot start inside the arena
     auto slot_src = [&](uint64_t S) {
@@ -978,6 +984,7 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
     constexpr uint64_t kEnd = Dispenser::kEnd;
     Dispenser D(p.ctr, (p.n + 3) >> 2, (uint64_t)gridDim.x * kDmaWaves,
                 (uint64_t)blockIdx.x * kDmaWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
+    D.align = 16;   // chunks start on 16-item groups: whole 256-B result runs
     auto item_start = [&](uint64_t i) { return p.base + 4 * i * p.stride; };   // first frame of item i
     // slot bytes an item's windows read: up to its last frame's end plus the realignment dword
     auto item_need = [&](uint64_t S, uint64_t src) {
@@ -994,6 +1001,8 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
 
     uint64_t it = D.first();
     if (it != kEnd) dma_of(slot0, it);
+    uint32_t cbuf = 0;    // FCSs of the current run of items, lane 4 (item & 15) + frame
+    uint64_t cmask = 0;   // lanes of cbuf that hold one (wave-uniform)
 
 #ifdef FCS_STAMPS   // measurement-only: per-wave cycles waiting for the slot vs. the whole item
     uint64_t st_wait = 0, st_all = 0, st_items = 0;
@@ -1068,7 +1077,21 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
         for (int hh = 0; hh < kDmaChains - 1; hh++) mv = merge_shift_dma(lds, kDmaChains - 2 - hh, xs[hh], mv);
         uint32_t v = lane_shift_dma(lds, mv, lanebase);
         v = row_xor(v);
-        emit<kDmaBad>(p, lds, c == kGroup - 1 && f + g < p.n, f + g, ~v);
+        // Results of a run of consecutive items collect in one register (lane 4 k + g: frame g of
+        // item k of a 16-item group) and leave as one coalesced store of up to 256 B: a 16-B store
+        // per item, whose 128-B line the L2 evicted half-written before the next items filled it,
+        // cost 2x the CRC bytes in HBM writes (WRITE_SIZE).
+        {
+            const uint32_t k = (uint32_t)(it & 15u);
+            const uint32_t vq = (uint32_t)__shfl((int)~v, (lane & 3) * kGroup);   // frame (lane & 3)'s FCS
+            if ((uint32_t)(lane >> 2) == k) cbuf = vq;
+            const uint64_t live = f + 4 <= p.n ? 0xFull : ((1ull << (p.n - f)) - 1ull);
+            cmask |= live << (4 * k);
+            if (k == 15 || nxt != it + 1) {
+                emit<kDmaBad>(p, lds, (cmask >> lane) & 1ull, 4 * (it & ~15ull) + (uint64_t)lane, cbuf);
+                cmask = 0;
+            }
+        }
         it = nxt;
 #ifdef FCS_STAMPS
         __builtin_amdgcn_sched_barrier(0);
@@ -1176,9 +1199,11 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     const int zb = fdead ? 0 : zf;   // the wave masks word groups up to its largest live claim
 
     const uint64_t n = p.n, units = (n + 3) >> 2;
-    const uint32_t cmax = m >= 64 ? 1u : 64u / m;
+    // chunks of about 64 items, and at least 16 units so that result runs fill 256-B groups
+    const uint32_t cmax = m >= 4 ? 16u : 64u / m;
     Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kSegilWaves, (uint64_t)blockIdx.x * kSegilWaves + (uint64_t)wave,
                 lane, 100, 1, cmax);
+    D.align = 16;
     constexpr uint64_t kEnd = Dispenser::kEnd;
     // segment r of frame f: [start, start + len); the run starts at the 16-B boundary below it
     auto seg_start = [&](uint64_t f, uint32_t r) {
@@ -1201,6 +1226,8 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     uint32_t r = 0;
     if (u != kEnd) issue(u, 0);
     uint32_t acc = 0;   // this quarter's frame: CRC state after its segments so far
+    uint32_t cbuf = 0;    // FCSs of the current run of units, lane 4 (unit & 15) + frame
+    uint64_t cmask = 0;   // lanes of cbuf that hold one (wave-uniform)
     while (u != kEnd) {   // wave-uniform
         const uint64_t f = 4 * u + q;
         const bool act = f < n;
@@ -1262,7 +1289,17 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
         uint32_t v = lane_shift_dma(lds, mv, lanebase);
         if (r == 0 && fdead) v = 0u;
         acc = row_xor(v);
-        if (r == m - 1) emit<kDmaBad>(p, lds, c == kGroup - 1 && act, f, ~acc);
+        if (r == m - 1) {   // results of consecutive units leave as one coalesced store (as fcs_dma_kernel)
+            const uint32_t k = (uint32_t)(u & 15u);
+            const uint32_t vq = (uint32_t)__shfl((int)~acc, (lane & 3) * kGroup);
+            if ((uint32_t)(lane >> 2) == k) cbuf = vq;
+            const uint64_t f0 = 4 * u;
+            cmask |= (f0 + 4 <= n ? 0xFull : ((1ull << (n - f0)) - 1ull)) << (4 * k);
+            if (k == 15 || un != u + 1) {
+                emit<kDmaBad>(p, lds, (cmask >> lane) & 1ull, 4 * (u & ~15ull) + (uint64_t)lane, cbuf);
+                cmask = 0;
+            }
+        }
         u = un;
         r = rn;
     }

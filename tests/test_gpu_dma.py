@@ -126,3 +126,24 @@ def test_dma_dynamic_tail_concurrent_streams(dev, oracle):
     torch.cuda.synchronize()
     assert np.array_equal(o1.cpu().numpy().view(np.uint32), exp)
     assert np.array_equal(o2.cpu().numpy().view(np.uint32), exp)
+
+
+def test_counter_ring_reuse_across_streams(dev, oracle):
+    """more dynamic launches in flight than the 256-slot counter ring, spread over two
+    streams. A slot's new user must wait for its previous kernel before zeroing it; otherwise two
+    kernels share one counter and skip each other's items (entries never written). 600 launches of
+    262144 x 1518 B (the smallest batch that takes the dynamic schedule on 256 CUs), each into its
+    own output, all checked against the oracle's CRCs."""
+    L, n, launches = 1518, 1 << 18, 600
+    host = np.random.default_rng(12).integers(0, 256, n * L, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    exp = oracle_fixed(oracle, host, L, L, n)
+    outs = torch.full((launches, n), -1, dtype=torch.int32, device=dev)
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    torch.cuda.synchronize()
+    for k in range(launches):
+        na.fixed_dev(d, L, L, n, outs[k], streams[k & 1])
+    torch.cuda.synchronize()
+    got = outs.cpu().numpy().view(np.uint32)
+    bad = np.nonzero((got != exp[None, :]).any(axis=1))[0]
+    assert bad.size == 0, f"{bad.size} launches with wrong or unwritten entries, first {int(bad[0])}"

@@ -1,0 +1,19 @@
+"""Runs last in the GPU suite (file order): the product library answered every drop-in ether_fcs
+call of this session on the GPU. fcs_engine_host_fallbacks counts the calls its host CRC answered
+(only after the GPU attempt and its retry both failed, or for buffers >= 4 GiB); on a
+healthy MI355X it must be 0, which shows the HIP path served every drop-in call of the suite."""
+import pytest
+
+import nstack_amd as na
+
+pytestmark = pytest.mark.gpu
+
+
+def test_product_library_never_used_its_host_crc():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    assert na.ether_fcs(b"123456789") == 0xCBF43926
+    st = na.engine_stats()
+    assert st["dropin_calls"] > 0
+    assert st["host_fallbacks"] == 0, st

@@ -27,6 +27,7 @@ sys.path.insert(0, ROOT)
 import bench  # noqa: E402
 
 TOTAL, L, SEED = 3001, 1518, 77
+IMIX_BLK = 1200   # frames per GPU of the sharded IMIX bench config in these tests
 
 
 def _oracle():
@@ -69,6 +70,19 @@ def _worker(rank, world, port, q, mode="fixed"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     o = _oracle()
+    if mode == "imix_bench":   # bench.py's configs[2] shard at N > 1 (imix_shard -> imix_sharded)
+        lo, hi, ln, off, byte0, total = bench.imix_shard(world, rank, IMIX_BLK)
+        buf = np.empty(total + 8, dtype=np.uint8)
+        o.oracle_splitmix_fill(buf.ctypes.data, total, SEED, byte0)
+        crc = np.zeros(hi - lo, dtype=np.uint32)
+        o.oracle_fcs_batch.argtypes = [ctypes.c_void_p] * 4 + [ctypes.c_size_t, ctypes.c_int]
+        o.oracle_fcs_batch(buf.ctypes.data, off.ctypes.data, ln.ctypes.data, crc.ctypes.data, hi - lo, 1)
+        sizes = [None] * world
+        dist.all_gather_object(sizes, (lo, hi, crc.tolist(), byte0, total))
+        if rank == 0:
+            q.put((sizes, 0.0))
+        dist.destroy_process_group()
+        return
     if mode == "imix":
         ln = _imix(TOTAL)
         lo, hi = bench.shard_range(TOTAL, world, rank, ln)
@@ -142,3 +156,26 @@ def test_shard_ranges_cover_eight_gpus():
     r = [bench.shard_range(total, 8, k) for k in range(8)]
     assert r[0][0] == 0 and r[-1][1] == total
     assert all(hi - lo == 64 << 20 for lo, hi in r)
+
+
+def test_two_rank_imix_bench_path_shards_match_single_pass():
+    """bench.py's N > 1 IMIX config (imix_shard): the global stream is `world` blocks of IMIX frames;
+    the ranks' fcs_shard_plan ranges partition it, each rank's bytes start at its global byte
+    position, and the gathered CRCs equal one pass over the whole stream."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "imix_bench")) for r in range(world)]
+    for p in procs:
+        p.start()
+    sizes, _ = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    glob = np.tile(bench.imix_lengths(IMIX_BLK), world)
+    assert sizes[0][0] == 0 and sizes[-1][1] == len(glob) and sizes[0][1] == sizes[1][0]
+    assert sizes[0][3] == 0 and sizes[1][3] == int(glob[:sizes[1][0]].sum())   # global byte positions
+    assert sizes[0][4] + sizes[1][4] == int(glob.sum())
+    gathered = np.concatenate([np.array(s[2], dtype=np.uint32) for s in sizes])
+    assert np.array_equal(gathered, _crcs_var(_oracle(), glob, 0, len(glob)))
