@@ -310,7 +310,12 @@ struct Dispenser {
 
     __device__ Dispenser(unsigned long long *ctr_, uint64_t U_, uint64_t W_, uint64_t wid_, int lane_,
                          uint32_t dyn_pct, uint32_t cmin_, uint32_t cmax_)
-        : ctr(ctr_), U(U_), W(W_), wid(wid_), cmin(cmin_), cmax(cmax_), lane(lane_) {
+        : ctr(ctr_), U(U_), W(W_), cmin(cmin_), cmax(cmax_), lane(lane_) {
+        // wave-uniform by construction; said so, the compiler keeps the whole schedule in SGPRs
+        // (from threadIdx.x >> 6 it kept it in VGPRs: 64-bit VALU division, and a VGPR spill in
+        // the flat kernel)
+        wid = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(wid_ >> 32)) << 32) |
+              (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)wid_);
         Is = ctr ? (U * (100 - dyn_pct) / 100) / W * W : U;   // statically assigned units in all
         Ks = wid < Is ? (Is - wid + W - 1) / W : 0;             // ... of this wave
     }
@@ -1429,7 +1434,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     init_bad(lds);
 
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int j = lane & (kGroup - 1);
     uint32_t base0, base1;
     table_bases(lane, base0, base1);
