@@ -137,6 +137,10 @@ struct DevState {
     std::atomic<uint32_t> ctr_seq{0};
     std::mutex ctr_mu[kCtrSlots];
     hipEvent_t ctr_done[kCtrSlots] = {};
+    // Per-slot device scratch for launches that need some besides the counter (the arena-stream
+    // kernel's list of units for fcs_flat_kernel), guarded by the same slot lease.
+    uint32_t *ctr_scr[kCtrSlots] = {};
+    uint64_t ctr_scr_words[kCtrSlots] = {};
     // Streams and mapped result words of drop-in lanes given up while a kernel may still be in
     // flight on them (timeout, lost completion, device error): never reused or freed before
     // fcs_engine_fini, so a late kernel cannot write into memory that serves another call.
@@ -309,6 +313,9 @@ uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
 // 16384 = 4 frames x 16 waves x 256 CUs: one item per quarter-wave on a full chip.
 std::atomic<uint64_t> g_var_threshold{16384};
 
+// Device word holding the unit-list length of the last arena-stream launch (fcs_debug_stream_listed).
+std::atomic<uint32_t *> g_last_stream_count{nullptr};
+
 // Fixed-length batches of frames up to this length (and more than g_var_threshold frames) take the
 // flat variable-length kernel: a 64-B frame then costs one lane instead of a quarter-wave. Measured
 // against the quarter-wave kernel (tools/ab.py): 64 B 11x, 576 B 2.1x, 1300 B
@@ -335,6 +342,26 @@ struct CounterLease {
         ds->ctr_mu[slot].unlock();
     }
 };
+
+// Device scratch of `words` u32 that belongs to a held slot lease (grown on the host once the
+// slot's last kernel has finished).
+int lease_scratch(CounterLease &lease, uint64_t words, uint32_t **out) {
+    DevState *ds = lease.ds;
+    const int s = lease.slot;
+    if (ds->ctr_scr_words[s] < words) {
+        if (ds->ctr_scr[s]) {
+            HIPTRY(hipEventSynchronize(ds->ctr_done[s]), "waiting for the counter slot's last kernel");
+            HIPTRY(hipFree(ds->ctr_scr[s]), "hipFree(slot scratch)");
+            ds->ctr_scr[s] = nullptr;
+            ds->ctr_scr_words[s] = 0;
+        }
+        const uint64_t w = std::max<uint64_t>(words, 1u << 16);
+        HIPTRY(hipMalloc(&ds->ctr_scr[s], w * 4), "hipMalloc(slot scratch)");
+        ds->ctr_scr_words[s] = w;
+    }
+    *out = ds->ctr_scr[s];
+    return 0;
+}
 
 int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p, CounterLease &lease) {
     const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
@@ -441,6 +468,27 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     p.blob = ds->d_blob;
     const bool windowed = n > g_var_threshold.load(std::memory_order_relaxed);
     const int grid = grid_for(ds, n, fcs::kWgThreads);
+#ifndef FCS_NO_STREAM   // measurement-only: every windowed batch through fcs_flat_kernel alone
+    if (windowed && off != nullptr && p.hi4 - p.lo4 >= 2 * (uint64_t)fcs::kChunkBytes) {
+        // arena stream for units of packed 64..1536-B frames, then fcs_flat_kernel for the units it
+        // listed (it returns at once when there are none)
+        int rc = take_counter(ds, st, p, lease);
+        if (rc) return rc;
+        const uint64_t units = (n + fcs::kStUnitFrames - 1) / fcs::kStUnitFrames;
+        uint32_t *scr = nullptr;
+        if ((rc = lease_scratch(lease, units + 1, &scr))) return rc;
+        p.ucount = scr;
+        p.ulist = scr + 1;
+        g_last_stream_count.store(scr, std::memory_order_relaxed);
+        HIPTRY(hipMemsetAsync(p.ucount, 0, 4, st), "zeroing the unit list");
+        HIPTRY(fcs::launch_stream(p, (int)std::min<uint64_t>((uint64_t)ds->cus, units), st), "launching fcs_stream_kernel");
+        fcs::KParams q = p;
+        CounterLease lease2;
+        if ((rc = take_counter(ds, st, q, lease2))) return rc;
+        HIPTRY(fcs::launch_fcs(true, true, q, grid, st), "launching fcs_flat_kernel<listed units>");
+        return 0;
+    }
+#endif
     if (windowed && (n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)grid * (fcs::kWgThreads / 64)) {
         const int rc = take_counter(ds, st, p, lease);
         if (rc) return rc;
@@ -1251,6 +1299,8 @@ static void destroy_state(DevState *ds) {
     if (ds->d_one_blob) hipFree(ds->d_one_blob);
     if (ds->d_kinit) hipFree(ds->d_kinit);
     if (ds->d_ctr) hipFree(ds->d_ctr);
+    for (uint32_t *scr : ds->ctr_scr)
+        if (scr) hipFree(scr);
 }
 
 extern "C" {
@@ -1483,6 +1533,15 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
 }
 
 uint64_t fcs_engine_host_fallbacks(void) { return g_host_fallbacks.load(std::memory_order_relaxed); }
+
+int64_t fcs_debug_stream_listed(void) {
+    uint32_t *d = g_last_stream_count.load(std::memory_order_relaxed);
+    if (!d) return -1;
+    HIPTRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    uint32_t v = 0;
+    HIPTRY(hipMemcpy(&v, d, 4, hipMemcpyDeviceToHost), "reading the unit-list length");
+    return (int64_t)v;
+}
 
 void fcs_engine_host_stats(uint64_t *sharded_calls, uint64_t *shard_jobs) {
     if (sharded_calls) *sharded_calls = g_sharded_calls.load(std::memory_order_relaxed);

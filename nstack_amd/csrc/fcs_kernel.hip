@@ -1430,6 +1430,12 @@ __device__ __forceinline__ uint32_t chunk_shift(const uint8_t *lds, uint32_t s, 
 template <bool TINY>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsBytes];
+    // After fcs_stream_kernel (p.ulist set): only the units it listed, 8 windows each; none -> done.
+    uint64_t nwin = (p.n + 63) >> 6;
+    if (p.ulist != nullptr) {
+        nwin = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)*p.ucount) * (kStUnitFrames / 64);
+        if (nwin == 0) return;
+    }
     stage_tables_flat(p, lds);
     init_bad(lds);
 
@@ -1444,9 +1450,11 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     acc[lane] = 0u;
     mark[lane] = 0;
     // windows of 64 frames from the dispenser (dynamic chunks of up to 16 windows when p.ctr is set)
-    Dispenser D(p.ctr, (p.n + 63) >> 6, (uint64_t)gridDim.x * (kWgThreads / 64),
+    Dispenser D(p.ctr, nwin, (uint64_t)gridDim.x * (kWgThreads / 64),
                 (uint64_t)blockIdx.x * (kWgThreads / 64) + (uint64_t)wave, lane, 100, 1, FCS_FLAT_CHUNK_MAX);
-    for (uint64_t win = D.first(); win != Dispenser::kEnd; win = D.next(win)) {
+    for (uint64_t wi = D.first(); wi != Dispenser::kEnd; wi = D.next(wi)) {
+        constexpr uint32_t kUw = kStUnitFrames / 64;   // windows per listed unit
+        const uint64_t win = p.ulist ? (uint64_t)p.ulist[wi / kUw] * kUw + wi % kUw : wi;
         const uint64_t w0 = win * 64;
         // ---- window metadata: lane i <-> frame w0 + i ----
         const uint64_t f = w0 + lane;
@@ -1580,6 +1588,302 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 
 
 
+
+// ---------------------------------------------------------------------------------------------
+// Variable-length frames, arena stream (fcs_stream_kernel): batches with offsets, windowed size.
+// CPU model of the decomposition: tests/stream_model.py.
+// The dispenser hands out units of kStUnitFrames frames. A unit whose frames are packed
+// (off[i + 1] == off[i] + len[i]) and 64..1536 B long is taken here; any other unit is listed
+// in p.ulist for fcs_flat_kernel, launched right after on the same stream.
+// A unit's bytes are walked in 4 KiB items at fixed arena positions (the first item at the 16-B
+// boundary below the unit's first frame): one coalesced LDS-DMA per item, issued while the
+// previous item is computed, no dealing. Lane l's chunk is the item's bytes [64 l, 64 l + 64)
+// (LDS at 80 l: conflict-free ds_read_b128); its chain L runs over all 16 words from register 0.
+// A frame starts or ends in at most one place of a chunk (frames >= 64 B); there the lane takes a
+// tap of its chain, T' = A_4(s_k ^ (w_k & the k-th word's bytes before the boundary)), s_k the
+// chain after k = sigma / 4 words. Every chunk goes to the frame holding its last byte, shifted
+// by whole chunks to the chunk holding that frame's end: acc_B ^= A_{64 j}(V), j = le - l - 1;
+// V = L, or where B starts, L ^ A_{4 (15 - k)}(T') ^ A_{64 - sigma}(~0) (the previous frame's
+// bytes out, the all-ones start in). Where a frame ends, the lane closes it:
+// R(~0, frame) = A_{r - 4}(T' ^ A_{4 (k + 1)}(acc)), sigma = 4 k + r. Results collect in an LDS
+// ring and leave as 256-B stores.
+// LDS (160 KiB): the 32 KiB slice tables of fcs_dma_kernel with, in the row holes, A_{64 j}
+// (j = 0..23), A_{4 i} (i = 0..16), A_{-d} (d = 1..4), K1[sigma] = A_{64 - sigma}(~0), the
+// chunk marks of every wave and the verify counters; 16 slots of 5 KiB; per wave accumulators
+// and results for 128 frames.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kStChunk = 64;
+constexpr uint32_t kStItem = 64 * kStChunk;
+constexpr uint32_t kStSlotBytes = 5120;
+constexpr int kStWaves = kWgThreads / 64;
+constexpr uint32_t kStHoleChunk = 0;                                   // A_{64 j}: 4 holes each
+constexpr uint32_t kStHoleWord = kStHoleChunk + 4 * kStChunkTabs;     // A_{4 i}
+constexpr uint32_t kStHoleInv = kStHoleWord + 4 * kStWordTabs;        // A_{-d}
+constexpr uint32_t kStHoleK1 = kStHoleInv + 4 * kStInvTabs;           // 2 holes
+constexpr uint32_t kStHoleMark = kStHoleK1 + 2;                       // 2 holes per wave
+constexpr uint32_t kStBad = dma_hole(kStHoleMark + 2 * 16);           // 16 x 8 B
+static_assert(kStHoleMark + 2 * 16 + 1 <= 256, "holes");
+static_assert(kStWaves <= 16, "marks and counters for 16 waves");
+constexpr uint32_t kStSlots = 65536;
+constexpr uint32_t kStRings = kStSlots + 16 * kStSlotBytes;           // per wave: acc[128], results[128]
+constexpr uint32_t kStLdsBytes = kStRings + 16 * 1024;
+static_assert(kStLdsBytes <= 163840, "LDS per CU");
+constexpr uint32_t kMarkStart = 1u << 31, kMarkEnd = 1u << 30;
+#ifndef FCS_ST_AUX   // cache policy of the item DMA's middle rows (measurement-only override)
+#define FCS_ST_AUX 2
+#endif
+
+// A_n(s) ^ extra from the nibble table at holes h .. h + 3 (nibble t at hole h + t / 2, +64 B for
+// odd t); h may differ per lane.
+__device__ __forceinline__ uint32_t hole_shift(const uint8_t *lds, uint32_t s, uint32_t h, uint32_t extra) {
+    uint32_t r[8];
+    const uint32_t base = h * 256u + kDmaHole;
+#pragma unroll
+    for (int t = 0; t < 8; t++) {
+        const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
+        r[t] = lds_rd(lds, base + 256u * (uint32_t)(t >> 1) + 64u * (uint32_t)(t & 1) + (sh & 0x3Cu));
+    }
+    return xor9(r, extra);
+}
+
+__device__ __forceinline__ void stage_stream_tables(const KParams &p, uint8_t *lds, int tid) {
+    for (int i = tid; i < 2048; i += kWgThreads) {   // slice tables as fcs_dma_kernel
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
+    }
+    for (int i = tid; i < (kStChunkTabs + kStWordTabs + kStInvTabs) * 128; i += kWgThreads) {
+        const uint32_t q = (uint32_t)i >> 7, t = ((uint32_t)i >> 4) & 7u, e = (uint32_t)i & 15u;
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * q + (t >> 1)) + 64u * (t & 1u) + 4u * e) = p.blob[kBlobStream + i];
+    }
+    for (int i = tid; i < 64; i += kWgThreads)
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kStHoleK1 + (uint32_t)i / 32u) + ((uint32_t)i % 32u) * 4u) =
+            p.blob[kBlobStreamK1 + i];
+    for (int i = tid; i < 2 * 16 * 32; i += kWgThreads)   // marks: empty
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kStHoleMark + (uint32_t)i / 32u) + ((uint32_t)i % 32u) * 4u) = 0u;
+    for (int i = tid; i < 16 * 256; i += kWgThreads) reinterpret_cast<uint32_t *>(lds + kStRings)[i] = 0u;
+}
+
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kStLdsBytes];
+    const int tid = threadIdx.x;
+    stage_stream_tables(p, lds, tid);
+    init_bad<kStBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    uint8_t *slot = lds + kStSlots + wave * kStSlotBytes;
+    uint32_t *acc = reinterpret_cast<uint32_t *>(lds + kStRings + wave * 1024u);
+    uint32_t *res = acc + 128;
+    const uint32_t mark_lane = dma_hole(kStHoleMark + 2u * wave + ((uint32_t)lane >> 5)) + ((uint32_t)lane & 31u) * 4u;
+    auto mark_at = [&](uint32_t c) {
+        return reinterpret_cast<uint32_t *>(lds + dma_hole(kStHoleMark + 2u * wave + (c >> 5)) + (c & 31u) * 4u);
+    };
+    // item DMA: instruction q, lane i moves LDS piece 64 q + i = 5 l + m (chunk l at 80 l; m = 4
+    // is the pad) from arena byte X + 64 l + 16 m
+    uint32_t goff[5];
+    bool gon[5];
+#pragma unroll
+    for (int q = 0; q < 5; q++) {
+        const uint32_t pj = 64u * (uint32_t)q + (uint32_t)lane, l = pj / 5u, m = pj - 5u * l;
+        goff[q] = 64u * l + 16u * m;
+        gon[q] = m < 4u;
+    }
+    const uint64_t hi16 = (p.hi4 + 15) & ~15ull;
+    auto dma_item = [&](uint64_t X) {
+        typedef __attribute__((address_space(3))) void lds_void;
+#pragma unroll
+        for (int q = 0; q < 5; q++) {
+            const uint64_t a = X + goff[q];
+            if (gon[q] && a < hi16) {   // first and last rows at the default policy (lines shared with neighbours)
+                if (q == 0 || q == 4)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), (lds_void *)(slot + 1024 * q), 16, 0, 0);
+                else
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), (lds_void *)(slot + 1024 * q), 16, 0,
+                                                     FCS_ST_AUX);
+            }
+        }
+    };
+    const u32x4 *chunk = reinterpret_cast<const u32x4 *>(slot + 80u * (uint32_t)lane);
+
+    constexpr uint64_t kEnd = Dispenser::kEnd;
+    const uint64_t units = (p.n + kStUnitFrames - 1) / kStUnitFrames;
+    Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kStWaves, (uint64_t)blockIdx.x * kStWaves + wave, lane, 100, 1, 8);
+    for (uint64_t u = D.first(); u != kEnd; u = D.next(u)) {
+        const uint64_t f0 = u * kStUnitFrames;
+        const uint32_t nf = (uint32_t)((p.n - f0) < kStUnitFrames ? (p.n - f0) : kStUnitFrames);
+        // ---- take the unit only if its frames are packed and 64..1536 B ----
+        uint64_t S[kStUnitFrames / 64];
+        uint32_t Ln[kStUnitFrames / 64];
+#pragma unroll
+        for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
+            const uint32_t g = 64u * (uint32_t)q + (uint32_t)lane;
+            S[q] = g < nf ? p.off[f0 + g] : 0ull;
+            Ln[q] = g < nf ? p.len[f0 + g] : kStMinLen;
+        }
+        bool bad = false;
+#pragma unroll
+        for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
+            const uint32_t g = 64u * (uint32_t)q + (uint32_t)lane;
+            bad |= Ln[q] < kStMinLen || Ln[q] > kStMaxLen;
+            // the next frame's start: lane + 1 of this batch, or lane 0 of the next one
+            uint32_t nlo = (uint32_t)__shfl_down((int)(uint32_t)S[q], 1), nhi = (uint32_t)__shfl_down((int)(uint32_t)(S[q] >> 32), 1);
+            if (q + 1 < (int)(kStUnitFrames / 64)) {
+                const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[q + 1]);
+                const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[q + 1] >> 32));
+                if (lane == 63) { nlo = blo; nhi = bhi; }
+            }
+            const uint64_t ns = ((uint64_t)nhi << 32) | nlo;
+            bad |= g + 1 < nf && ns != S[q] + Ln[q];
+        }
+        if (__any(bad)) {
+            if (lane == 0) p.ulist[atomicAdd(p.ucount, 1u)] = (uint32_t)u;
+            continue;
+        }
+        // ---- geometry, relative to X0 (the first item's start) ----
+        const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
+                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
+        const uint64_t X0 = s0 & ~15ull;
+        const uint32_t rel0 = (uint32_t)(s0 - X0);
+        // frame ends relative to X0 (packed: frame g ends where frame g + 1 starts)
+        uint32_t erel[kStUnitFrames / 64];
+        {
+            uint32_t run = rel0, pre = 0;
+#pragma unroll
+            for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
+                uint32_t incl = Ln[q];   // inclusive prefix of the lengths over the batch
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+                    if (lane >= d) incl += y;
+                }
+                erel[q] = run + incl;
+                run += (uint32_t)__shfl((int)incl, 63);
+                (void)pre;
+            }
+        }
+        const uint32_t last = nf - 1;
+        uint32_t E = 0;   // the unit's end, relative to X0
+#pragma unroll
+        for (int q = 0; q < (int)(kStUnitFrames / 64); q++)
+            if ((last >> 6) == (uint32_t)q) E = (uint32_t)__builtin_amdgcn_readlane((int)erel[q], (int)(last & 63u));
+        const uint32_t nitems = (E + kStItem - 1) / kStItem;
+        auto end_of = [&](uint32_t g) -> uint32_t {   // frame g's end (wave-uniform g)
+            uint32_t e = 0;
+#pragma unroll
+            for (int q = 0; q < (int)(kStUnitFrames / 64); q++)
+                if ((g >> 6) == (uint32_t)q) e = (uint32_t)__builtin_amdgcn_readlane((int)erel[q], (int)(g & 63u));
+            return e;
+        };
+
+        uint32_t nsf = 0, base_cnt = 0, fin = 0;
+        auto flush = [&](uint32_t b, uint32_t cnt) {   // results of frames 64 b .. 64 b + cnt - 1
+            wave_lds_sync();
+            const uint32_t v = res[(64u * b + (uint32_t)lane) & 127u];
+            emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + 64u * b + (uint32_t)lane, v);
+        };
+        auto closed_up_to = [&](uint32_t fin_new) {   // frames < fin_new have results: whole batches leave
+            while ((fin >> 6) < (fin_new >> 6)) {
+                flush(fin >> 6, 64u);
+                fin = ((fin >> 6) + 1u) << 6;
+            }
+            fin = fin_new > fin ? fin_new : fin;
+        };
+        dma_item(X0);
+        for (uint32_t t = 0; t < nitems; t++) {
+            const uint32_t Xr = kStItem * t;
+            // ---- marks: frames starting in this item, and the unit's end ----
+            uint32_t cnt = 0;
+#pragma unroll
+            for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
+                // frames >= 64 B: an item's starts lie in batches nsf / 64 and the one after
+                if ((uint32_t)q < (nsf >> 6) || (uint32_t)q > (nsf >> 6) + 1u) continue;
+                const uint32_t g = 64u * (uint32_t)q + (uint32_t)lane;
+                const uint32_t st = erel[q] - Ln[q];
+                const bool in = g >= nsf && g < nf && st < Xr + kStItem;
+                if (in) *mark_at((st - Xr) >> 6) = kMarkStart | (g << 6) | ((st - Xr) & 63u);
+                cnt += (uint32_t)__popcll(__ballot(in));
+            }
+            if (E < Xr + kStItem && lane == 0) *mark_at((E - Xr) >> 6) = kMarkEnd | ((E - Xr) & 63u);
+            nsf += cnt;
+            const uint32_t le_far = ((nsf ? end_of(nsf - 1) : E) - Xr) >> 6;   // chunk of the next boundary past this item
+            wave_lds_sync();
+            const uint32_t mk = lds_rd(lds, mark_lane);
+            *reinterpret_cast<uint32_t *>(lds + mark_lane) = 0u;
+            const bool isst = (mk & kMarkStart) != 0, isend = (mk & kMarkEnd) != 0;
+            const uint32_t sig = mk & 63u, k = sig >> 2, r = sig & 3u, bf = (mk >> 6) & 1023u;
+            const uint64_t Mst = __ballot(isst), Mb = __ballot(isst || isend);
+            const uint32_t rank = (uint32_t)__popcll(Mst & ((2ull << lane) - 1ull));
+            const int o = (int)(base_cnt + rank) - 1;                       // frame holding the chunk's last byte
+            const bool contrib = o >= 0 && Xr + 64u * (uint32_t)lane + 63u < E;
+            const uint64_t after = lane == 63 ? 0ull : (Mb & (~0ull << (lane + 1)));
+            const uint32_t le = after ? (uint32_t)__builtin_ctzll(after) : le_far;
+            const uint32_t j = contrib ? le - (uint32_t)lane - 1u : 0u;
+
+            // ---- this item's bytes; the next item's DMA ----
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's item has landed
+            uint32_t w[16];
+#pragma unroll
+            for (int i = 0; i < 4; i++) {
+                const u32x4 x = chunk[i];
+                w[4 * i] = x.x;
+                w[4 * i + 1] = x.y;
+                w[4 * i + 2] = x.z;
+                w[4 * i + 3] = x.w;
+            }
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+            if (t + 1 < nitems) dma_item(X0 + Xr + kStItem);
+
+            // ---- the chain over 16 words, with the tap at word k ----
+            const uint32_t keep = 0xFFFFFFFFu << (8u * r);   // word k's bytes at and after the boundary
+            uint32_t x = w[0], cap = 0;
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                if ((uint32_t)i == k) cap = x ^ (w[i] & keep);
+                x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
+            }
+            const uint32_t Tp = step4_l8(lds, cap, 0u, B, SEL);
+            const uint32_t k1 = lds_rd(lds, dma_hole(kStHoleK1 + sig / 32u) + (sig % 32u) * 4u);
+            const uint32_t U = hole_shift(lds, Tp, kStHoleWord + 4u * (15u - k), k1);
+            const uint32_t V = isst ? (x ^ U) : x;
+            const uint32_t W = hole_shift(lds, V, kStHoleChunk + 4u * j, 0u);
+            if (contrib && W) atomicXor(&acc[(uint32_t)o & 127u], W);
+            wave_lds_sync();
+
+            // ---- frames closing here: the previous frame where one starts, the unit's last at its end ----
+            const int A = isst ? (int)bf - 1 : (isend ? (int)last : -1);
+            const bool closes = A >= 0;
+            uint32_t a = 0;
+            if (closes) {
+                a = acc[(uint32_t)A & 127u];
+                acc[(uint32_t)A & 127u] = 0u;
+            }
+            const uint32_t inner = hole_shift(lds, a, kStHoleWord + 4u * (k + 1u), Tp);
+            const uint32_t reg = hole_shift(lds, inner, kStHoleInv + 4u * (3u - r), 0u);
+            if (closes) res[(uint32_t)A & 127u] = ~reg;
+            base_cnt += (uint32_t)__popcll(Mst);
+            const uint64_t Mc = __ballot(closes);
+            if (Mc) closed_up_to((uint32_t)__builtin_amdgcn_readlane(A, 63 - __builtin_clzll(Mc)) + 1u);
+        }
+        // the unit's end at the very end of its last item: no item holds its mark; T' = 0 there
+        if (E == kStItem * nitems) {
+            wave_lds_sync();
+            if (lane == 0) {
+                res[last & 127u] = ~acc[last & 127u];
+                acc[last & 127u] = 0u;
+            }
+            closed_up_to(nf);
+        }
+        if ((fin >> 6) * 64u < nf) flush(fin >> 6, nf - (fin >> 6) * 64u);
+        wave_lds_sync();
+    }
+    flush_bad<kStBad>(p, lds);
+}
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
@@ -1917,6 +2221,12 @@ hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hip
 hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
     hipLaunchKernelGGL((fcs_dma_kernel<2, true>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream(const KParams &p, int grid, hipStream_t st) {
+    (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    hipLaunchKernelGGL(fcs_stream_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
     return hipGetLastError();
 }
 

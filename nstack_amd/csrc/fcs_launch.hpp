@@ -23,7 +23,17 @@ struct KParams {
     uint8_t *ok;            // verify mode: ok[i] = 1 iff frame i (FCS trailer included) checks
     unsigned long long *bad;//   ... and *bad += number of frames that do not (else both null)
     unsigned long long *ctr;// zeroed device work counter for a dynamic schedule (null: static interleave)
+    // Arena-stream kernel (fcs_stream_kernel) and its follow-up: units of kStUnitFrames frames the
+    // stream kernel did not take (not packed, or a length outside 64..1536) are appended to ulist
+    // (count in *ucount, zeroed before the launch); fcs_flat_kernel with ulist set processes exactly
+    // those units (and returns at once when there are none).
+    uint32_t *ulist;
+    uint32_t *ucount;
 };
+// Arena-stream kernel geometry: units of frames handed out by the dispenser; 64-B lane chunks at
+// fixed arena positions, 64 per 4 KiB item; frames of 64..1536 B, packed within a unit.
+constexpr uint32_t kStUnitFrames = 512;
+constexpr uint32_t kStMinLen = 64, kStMaxLen = 1536;
 
 // Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). The 1504..1536-B
 // single-segment kernel and frames of kWideSegs (3) or more segments run 8 waves per CU: 2 per SIMD
@@ -157,6 +167,7 @@ hipError_t launch_small_list(const ListArgs &a, hipStream_t st);
 hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hipStream_t st);
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st);
 hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st);
+hipError_t launch_stream(const KParams &p, int grid, hipStream_t st);
 hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,
                            uint64_t n, hipStream_t st);
 

@@ -90,7 +90,13 @@ constexpr uint32_t kBlobM768 = kBlobInv + kChunkBytes;  // uint32 [8][16]
 constexpr uint32_t kBlobFlat = kBlobM768 + 8 * 16;      // uint32 [16][136] (C_c, LDS order)
 constexpr uint32_t kBlobLaneDma = kBlobFlat + kFlatBytes / 4;   // uint32 [8][16][32]: A_{e_c}
 constexpr uint32_t kBlobMerge = kBlobLaneDma + 8 * 16 * 32;     // uint32 [11][8][16]: A_{8k}, k = 1..11
-constexpr uint32_t kBlobWords = kBlobMerge + 11 * 8 * 16;
+// Arena-stream variable-length kernel (fcs_stream_kernel): chunk shifts A_{64 j} (j = 0..23),
+// word shifts A_{4 i} (i = 0..16), inverse byte shifts A_{-d} (d = 1..4), each a nibble table
+// [8][16], and K1[sigma] = A_{64 - sigma}(0xFFFFFFFF) (sigma = 0..63).
+constexpr int kStChunkTabs = 24, kStWordTabs = 17, kStInvTabs = 4;
+constexpr uint32_t kBlobStream = kBlobMerge + 11 * 8 * 16;
+constexpr uint32_t kBlobStreamK1 = kBlobStream + (kStChunkTabs + kStWordTabs + kStInvTabs) * 128;
+constexpr uint32_t kBlobWords = kBlobStreamK1 + 64;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -170,6 +176,18 @@ struct Tables {
             for (int t = 0; t < 8; t++)
                 for (int e = 0; e < 16; e++) b[kBlobMerge + (k - 1) * 128 + t * 16 + e] = nt[t][e];
         }
+        // arena-stream kernel: A_{64 j}, A_{4 i}, A_{-d}, K1
+        int q = 0;
+        auto put = [&](long n) {
+            nibble_table(n, nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobStream + q * 128 + t * 16 + e] = nt[t][e];
+            q++;
+        };
+        for (int j = 0; j < kStChunkTabs; j++) put(64L * j);
+        for (int i = 0; i < kStWordTabs; i++) put(4L * i);
+        for (int d = 1; d <= kStInvTabs; d++) put(-(long)d);
+        for (int sg = 0; sg < 64; sg++) b[kBlobStreamK1 + sg] = shift(0xFFFFFFFFu, 64 - sg);
         return b;
     }
     // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.
