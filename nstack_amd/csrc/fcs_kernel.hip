@@ -1599,18 +1599,20 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 // boundary below the unit's first frame): one coalesced LDS-DMA per item, issued while the
 // previous item is computed, no dealing. Lane l's chunk is the item's bytes [64 l, 64 l + 64)
 // (LDS at 80 l: conflict-free ds_read_b128); its chain L runs over all 16 words from register 0.
-// A frame starts or ends in at most one place of a chunk (frames >= 64 B); there the lane takes a
-// tap of its chain, T' = A_4(s_k ^ (w_k & the k-th word's bytes before the boundary)), s_k the
-// chain after k = sigma / 4 words. Every chunk goes to the frame holding its last byte, shifted
-// by whole chunks to the chunk holding that frame's end: acc_B ^= A_{64 j}(V), j = le - l - 1;
-// V = L, or where B starts, L ^ A_{4 (15 - k)}(T') ^ A_{64 - sigma}(~0) (the previous frame's
-// bytes out, the all-ones start in). Where a frame ends, the lane closes it:
-// R(~0, frame) = A_{r - 4}(T' ^ A_{4 (k + 1)}(acc)), sigma = 4 k + r. Results collect in an LDS
-// ring and leave as 256-B stores.
+// A frame starts in at most one place of a chunk (frames >= 64 B); there the lane takes a tap of
+// its chain, T' = A_4(s_k ^ (w_k & the k-th word's bytes before the boundary)), s_k the chain
+// after k = sigma / 4 words, and records it for the frame starting there (it is also the end tap
+// of the frame before). Every chunk goes to the frame holding its last byte, shifted by whole
+// chunks to the chunk holding that frame's end, A_{64 j}(L) with j = le - l - 1; the lanes of one
+// frame are summed by a wave-wide XOR scan and reach its LDS accumulator with one xor at each
+// segment edge. Once 64 frames have ended, one pass closes them, a frame per lane:
+//   acc ^= A_{64 (le - ls - 1)}(A_{4 (15 - k_s)}(T'_s) ^ A_{64 - sigma_s}(~0))   (its start)
+//   R(~0, frame) = A_{r_e - 4}(T'_e ^ A_{4 (k_e + 1)}(acc)),  sigma_e = 4 k_e + r_e   (its end)
+// and stores the 64 FCSs as one 256-B row.
 // LDS (160 KiB): the 32 KiB slice tables of fcs_dma_kernel with, in the row holes, A_{64 j}
 // (j = 0..23), A_{4 i} (i = 0..16), A_{-d} (d = 1..4), K1[sigma] = A_{64 - sigma}(~0), the
 // chunk marks of every wave and the verify counters; 16 slots of 5 KiB; per wave accumulators
-// and results for 128 frames.
+// and start taps of 128 frames.
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kStChunk = 64;
 constexpr uint32_t kStItem = 64 * kStChunk;
@@ -1625,7 +1627,7 @@ constexpr uint32_t kStBad = dma_hole(kStHoleMark + 2 * 16);           // 16 x 8 
 static_assert(kStHoleMark + 2 * 16 + 1 <= 256, "holes");
 static_assert(kStWaves <= 16, "marks and counters for 16 waves");
 constexpr uint32_t kStSlots = 65536;
-constexpr uint32_t kStRings = kStSlots + 16 * kStSlotBytes;           // per wave: acc[128], results[128]
+constexpr uint32_t kStRings = kStSlots + 16 * kStSlotBytes;           // per wave: acc[128], tap[128]
 constexpr uint32_t kStLdsBytes = kStRings + 16 * 1024;
 static_assert(kStLdsBytes <= 163840, "LDS per CU");
 constexpr uint32_t kMarkStart = 1u << 31, kMarkEnd = 1u << 30;
@@ -1644,6 +1646,18 @@ __device__ __forceinline__ uint32_t hole_shift(const uint8_t *lds, uint32_t s, u
         r[t] = lds_rd(lds, base + 256u * (uint32_t)(t >> 1) + 64u * (uint32_t)(t & 1) + (sh & 0x3Cu));
     }
     return xor9(r, extra);
+}
+
+// Inclusive XOR scan over the 64 lanes (row shifts within each 16-lane row, then the row
+// broadcasts of gfx9 DPP).
+__device__ __forceinline__ uint32_t wave_xor_scan(uint32_t v) {
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, true);   // row_shr:1
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, true);   // row_shr:2
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, true);   // row_shr:4
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, true);   // row_shr:8
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
 }
 
 __device__ __forceinline__ void stage_stream_tables(const KParams &p, uint8_t *lds, int tid) {
@@ -1678,12 +1692,13 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
     const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
                              0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
     uint8_t *slot = lds + kStSlots + wave * kStSlotBytes;
-    uint32_t *acc = reinterpret_cast<uint32_t *>(lds + kStRings + wave * 1024u);
-    uint32_t *res = acc + 128;
+    uint32_t *acc = reinterpret_cast<uint32_t *>(lds + kStRings + wave * 1024u);   // per frame (mod 128)
+    uint32_t *tap = acc + 128;                                                      // start tap per frame
     const uint32_t mark_lane = dma_hole(kStHoleMark + 2u * wave + ((uint32_t)lane >> 5)) + ((uint32_t)lane & 31u) * 4u;
     auto mark_at = [&](uint32_t c) {
         return reinterpret_cast<uint32_t *>(lds + dma_hole(kStHoleMark + 2u * wave + (c >> 5)) + (c & 31u) * 4u);
     };
+    auto k1_of = [&](uint32_t sg) { return lds_rd(lds, dma_hole(kStHoleK1 + sg / 32u) + (sg % 32u) * 4u); };
     // item DMA: instruction q, lane i moves LDS piece 64 q + i = 5 l + m (chunk l at 80 l; m = 4
     // is the pad) from arena byte X + 64 l + 16 m
     uint32_t goff[5];
@@ -1710,6 +1725,21 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         }
     };
     const u32x4 *chunk = reinterpret_cast<const u32x4 *>(slot + 80u * (uint32_t)lane);
+    // measurement build (FCS_ST_REGLOAD): the lane loads its own 64-B chunk into registers, the next
+    // item's loads in flight while the current one is computed (no slot)
+    auto load_item = [&](uint64_t X, uint32_t (&wv)[16]) {
+        const uint64_t a = X + 64u * (uint32_t)lane;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const u32x4 v = a + 16u * (uint32_t)i < hi16 ? gload<u32x4>(a + 16u * (uint32_t)i) : u32x4{0u, 0u, 0u, 0u};
+            wv[4 * i] = v.x;
+            wv[4 * i + 1] = v.y;
+            wv[4 * i + 2] = v.z;
+            wv[4 * i + 3] = v.w;
+        }
+    };
+    (void)load_item;
+    constexpr int kQ = (int)(kStUnitFrames / 64);
 
     constexpr uint64_t kEnd = Dispenser::kEnd;
     const uint64_t units = (p.n + kStUnitFrames - 1) / kStUnitFrames;
@@ -1718,25 +1748,28 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         const uint64_t f0 = u * kStUnitFrames;
         const uint32_t nf = (uint32_t)((p.n - f0) < kStUnitFrames ? (p.n - f0) : kStUnitFrames);
         // ---- take the unit only if its frames are packed and 64..1536 B ----
-        uint64_t S[kStUnitFrames / 64];
-        uint32_t Ln[kStUnitFrames / 64];
+        uint64_t S[kQ];
+        uint32_t Ln[kQ];
 #pragma unroll
-        for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
+        for (int q = 0; q < kQ; q++) {
             const uint32_t g = 64u * (uint32_t)q + (uint32_t)lane;
             S[q] = g < nf ? p.off[f0 + g] : 0ull;
             Ln[q] = g < nf ? p.len[f0 + g] : kStMinLen;
         }
         bool bad = false;
 #pragma unroll
-        for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
+        for (int q = 0; q < kQ; q++) {
             const uint32_t g = 64u * (uint32_t)q + (uint32_t)lane;
             bad |= Ln[q] < kStMinLen || Ln[q] > kStMaxLen;
             // the next frame's start: lane + 1 of this batch, or lane 0 of the next one
             uint32_t nlo = (uint32_t)__shfl_down((int)(uint32_t)S[q], 1), nhi = (uint32_t)__shfl_down((int)(uint32_t)(S[q] >> 32), 1);
-            if (q + 1 < (int)(kStUnitFrames / 64)) {
+            if (q + 1 < kQ) {
                 const uint32_t blo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[q + 1]);
                 const uint32_t bhi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[q + 1] >> 32));
-                if (lane == 63) { nlo = blo; nhi = bhi; }
+                if (lane == 63) {
+                    nlo = blo;
+                    nhi = bhi;
+                }
             }
             const uint64_t ns = ((uint64_t)nhi << 32) | nlo;
             bad |= g + 1 < nf && ns != S[q] + Ln[q];
@@ -1749,75 +1782,68 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
         const uint64_t X0 = s0 & ~15ull;
-        const uint32_t rel0 = (uint32_t)(s0 - X0);
-        // frame ends relative to X0 (packed: frame g ends where frame g + 1 starts)
-        uint32_t erel[kStUnitFrames / 64];
-        {
-            uint32_t run = rel0, pre = 0;
-#pragma unroll
-            for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
-                uint32_t incl = Ln[q];   // inclusive prefix of the lengths over the batch
-#pragma unroll
-                for (int d = 1; d < 64; d <<= 1) {
-                    const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-                    if (lane >= d) incl += y;
-                }
-                erel[q] = run + incl;
-                run += (uint32_t)__shfl((int)incl, 63);
-                (void)pre;
-            }
-        }
-        const uint32_t last = nf - 1;
-        uint32_t E = 0;   // the unit's end, relative to X0
-#pragma unroll
-        for (int q = 0; q < (int)(kStUnitFrames / 64); q++)
-            if ((last >> 6) == (uint32_t)q) E = (uint32_t)__builtin_amdgcn_readlane((int)erel[q], (int)(last & 63u));
-        const uint32_t nitems = (E + kStItem - 1) / kStItem;
-        auto end_of = [&](uint32_t g) -> uint32_t {   // frame g's end (wave-uniform g)
-            uint32_t e = 0;
-#pragma unroll
-            for (int q = 0; q < (int)(kStUnitFrames / 64); q++)
-                if ((g >> 6) == (uint32_t)q) e = (uint32_t)__builtin_amdgcn_readlane((int)erel[q], (int)(g & 63u));
-            return e;
-        };
-
-        uint32_t nsf = 0, base_cnt = 0, fin = 0;
-        auto flush = [&](uint32_t b, uint32_t cnt) {   // results of frames 64 b .. 64 b + cnt - 1
-            wave_lds_sync();
-            const uint32_t v = res[(64u * b + (uint32_t)lane) & 127u];
-            emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + 64u * b + (uint32_t)lane, v);
-        };
-        auto closed_up_to = [&](uint32_t fin_new) {   // frames < fin_new have results: whole batches leave
-            while ((fin >> 6) < (fin_new >> 6)) {
-                flush(fin >> 6, 64u);
-                fin = ((fin >> 6) + 1u) << 6;
-            }
-            fin = fin_new > fin ? fin_new : fin;
-        };
+#ifndef FCS_ST_REGLOAD
         dma_item(X0);
-        for (uint32_t t = 0; t < nitems; t++) {
-            const uint32_t Xr = kStItem * t;
-            // ---- marks: frames starting in this item, and the unit's end ----
-            uint32_t cnt = 0;
+#endif
+        const uint64_t o0 = X0 - p.base;   // arena offset of X0
+        const uint32_t last = nf - 1;
+        // The cursor: frames 64 cb + lane (batch A) and 64 (cb + 1) + lane (batch B): end (relative
+        // to X0) and length. An item's starts lie in these two batches (frames >= 64 B).
+        uint32_t cb = 0;
+        uint32_t eA = (uint32_t)(S[0] + Ln[0] - o0), lA = Ln[0];
+        uint32_t eB = (uint32_t)(S[1] + Ln[1] - o0), lB = Ln[1];
+        uint32_t E = 0;   // the unit's end
 #pragma unroll
-            for (int q = 0; q < (int)(kStUnitFrames / 64); q++) {
-                // frames >= 64 B: an item's starts lie in batches nsf / 64 and the one after
-                if ((uint32_t)q < (nsf >> 6) || (uint32_t)q > (nsf >> 6) + 1u) continue;
-                const uint32_t g = 64u * (uint32_t)q + (uint32_t)lane;
-                const uint32_t st = erel[q] - Ln[q];
-                const bool in = g >= nsf && g < nf && st < Xr + kStItem;
-                if (in) *mark_at((st - Xr) >> 6) = kMarkStart | (g << 6) | ((st - Xr) & 63u);
-                cnt += (uint32_t)__popcll(__ballot(in));
-            }
+        for (int q = 0; q < kQ; q++)
+            if ((last >> 6) == (uint32_t)q) E = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(S[q] + Ln[q] - o0), (int)(last & 63u));
+        const uint32_t nitems = (E + kStItem - 1) / kStItem;
+        uint32_t nsf = 0, base_cnt = 0, closed = 0;
+        uint32_t tend = 0;   // end tap of the unit's last frame (0 when it ends on an item edge)
+        // close frames 64 b .. 64 b + cnt - 1 (all ended; e, L: their ends and lengths): start term,
+        // end tap, one 256-B store
+        auto close_pass = [&](uint32_t b, uint32_t cnt, uint32_t e, uint32_t L) {
+            wave_lds_sync();
+            const uint32_t g = 64u * b + (uint32_t)lane;
+            const uint32_t st = e - L, ss = st & 63u, se = e & 63u;
+            const uint32_t Ts = tap[g & 127u];
+            const uint32_t Te = g < last ? tap[(g + 1u) & 127u] : tend;
+            const uint32_t a0 = acc[g & 127u];
+            wave_lds_sync();
+            acc[g & 127u] = 0u;
+            const uint32_t U = hole_shift(lds, Ts, kStHoleWord + 4u * (15u - (ss >> 2)), k1_of(ss));
+            const uint32_t js = (uint32_t)lane < cnt ? (e >> 6) - (st >> 6) - 1u : 0u;
+            const uint32_t a = hole_shift(lds, U, kStHoleChunk + 4u * js, a0);
+            const uint32_t inner = hole_shift(lds, a, kStHoleWord + 4u * ((se >> 2) + 1u), Te);
+            const uint32_t reg = hole_shift(lds, inner, kStHoleInv + 4u * (3u - (se & 3u)), 0u);
+            emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + g, ~reg);
+        };
+        auto item = [&](uint32_t t, uint32_t (&wc)[16], uint32_t (&wn)[16]) {
+            const uint32_t Xr = kStItem * t;
+#ifdef FCS_ST_REGLOAD
+            if (t + 1 < nitems) load_item(X0 + Xr + kStItem, wn);   // the next item's bytes, into registers
+#else
+            (void)wn;
+#endif
+            // ---- marks: frames starting in this item, and the unit's end ----
+            const uint32_t gA = 64u * cb + (uint32_t)lane, gB = gA + 64u;
+            const uint32_t sA = eA - lA, sB = eB - lB;
+            const bool inA = gA >= nsf && gA < nf && sA < Xr + kStItem;
+            const bool inB = gB >= nsf && gB < nf && sB < Xr + kStItem;
+            if (inA) *mark_at((sA - Xr) >> 6) = kMarkStart | (gA << 6) | ((sA - Xr) & 63u);
+            if (inB) *mark_at((sB - Xr) >> 6) = kMarkStart | (gB << 6) | ((sB - Xr) & 63u);
             if (E < Xr + kStItem && lane == 0) *mark_at((E - Xr) >> 6) = kMarkEnd | ((E - Xr) & 63u);
-            nsf += cnt;
-            const uint32_t le_far = ((nsf ? end_of(nsf - 1) : E) - Xr) >> 6;   // chunk of the next boundary past this item
+            nsf += (uint32_t)__popcll(__ballot(inA)) + (uint32_t)__popcll(__ballot(inB));
+            // chunk of the next boundary past this item: the end of the last frame started so far
+            const uint32_t gl = nsf - 1u;
+            const uint32_t el = (gl >> 6) == cb ? (uint32_t)__builtin_amdgcn_readlane((int)eA, (int)(gl & 63u))
+                                                : (uint32_t)__builtin_amdgcn_readlane((int)eB, (int)(gl & 63u));
+            const uint32_t le_far = (el - Xr) >> 6;
             wave_lds_sync();
             const uint32_t mk = lds_rd(lds, mark_lane);
             *reinterpret_cast<uint32_t *>(lds + mark_lane) = 0u;
             const bool isst = (mk & kMarkStart) != 0, isend = (mk & kMarkEnd) != 0;
             const uint32_t sig = mk & 63u, k = sig >> 2, r = sig & 3u, bf = (mk >> 6) & 1023u;
-            const uint64_t Mst = __ballot(isst), Mb = __ballot(isst || isend);
+            const uint64_t Mst = __ballot(isst), Mend = __ballot(isend), Mb = Mst | Mend;
             const uint32_t rank = (uint32_t)__popcll(Mst & ((2ull << lane) - 1ull));
             const int o = (int)(base_cnt + rank) - 1;                       // frame holding the chunk's last byte
             const bool contrib = o >= 0 && Xr + 64u * (uint32_t)lane + 63u < E;
@@ -1825,9 +1851,13 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             const uint32_t le = after ? (uint32_t)__builtin_ctzll(after) : le_far;
             const uint32_t j = contrib ? le - (uint32_t)lane - 1u : 0u;
 
+#ifdef FCS_ST_REGLOAD
+            uint32_t (&w)[16] = wc;
+            uint32_t wk = 0;
+#else
             // ---- this item's bytes; the next item's DMA ----
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's item has landed
-            uint32_t w[16];
+            uint32_t (&w)[16] = wc;
 #pragma unroll
             for (int i = 0; i < 4; i++) {
                 const u32x4 x = chunk[i];
@@ -1836,50 +1866,73 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
                 w[4 * i + 2] = x.z;
                 w[4 * i + 3] = x.w;
             }
+            const uint32_t wk = lds_rd(slot, 80u * (uint32_t)lane + 4u * k);   // the tap word
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
             if (t + 1 < nitems) dma_item(X0 + Xr + kStItem);
+#endif
 
-            // ---- the chain over 16 words, with the tap at word k ----
-            const uint32_t keep = 0xFFFFFFFFu << (8u * r);   // word k's bytes at and after the boundary
-            uint32_t x = w[0], cap = 0;
+            // ---- the chain over 16 words; its state before word k ----
+            uint32_t x = w[0], xk = 0;
+#ifdef FCS_ST_NOCRC   // measurement-only: the words XORed instead of the chain (wrong FCS)
+#pragma unroll
+            for (int i = 1; i < 16; i++) x ^= w[i];
+            xk = x ^ k;
+#else
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                if ((uint32_t)i == k) cap = x ^ (w[i] & keep);
+                if ((uint32_t)i == k) {
+                    xk = x;
+#ifdef FCS_ST_REGLOAD
+                    wk = w[i];
+#endif
+                }
                 x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
             }
-            const uint32_t Tp = step4_l8(lds, cap, 0u, B, SEL);
-            const uint32_t k1 = lds_rd(lds, dma_hole(kStHoleK1 + sig / 32u) + (sig % 32u) * 4u);
-            const uint32_t U = hole_shift(lds, Tp, kStHoleWord + 4u * (15u - k), k1);
-            const uint32_t V = isst ? (x ^ U) : x;
-            const uint32_t W = hole_shift(lds, V, kStHoleChunk + 4u * j, 0u);
-            if (contrib && W) atomicXor(&acc[(uint32_t)o & 127u], W);
-            wave_lds_sync();
+#endif
+            // the tap: word k's bytes before the boundary finish the prefix (x_k ^ w_k = s_k)
+            const uint32_t Tp = step4_l8(lds, xk ^ (wk & (0xFFFFFFFFu << (8u * r))), 0u, B, SEL);
+            if (isst) tap[bf & 127u] = Tp;
+            if (Mend) tend = (uint32_t)__builtin_amdgcn_readlane((int)Tp, (int)__builtin_ctzll(Mend));
 
-            // ---- frames closing here: the previous frame where one starts, the unit's last at its end ----
-            const int A = isst ? (int)bf - 1 : (isend ? (int)last : -1);
-            const bool closes = A >= 0;
-            uint32_t a = 0;
-            if (closes) {
-                a = acc[(uint32_t)A & 127u];
-                acc[(uint32_t)A & 127u] = 0u;
-            }
-            const uint32_t inner = hole_shift(lds, a, kStHoleWord + 4u * (k + 1u), Tp);
-            const uint32_t reg = hole_shift(lds, inner, kStHoleInv + 4u * (3u - r), 0u);
-            if (closes) res[(uint32_t)A & 127u] = ~reg;
+            // ---- chunk contributions: one XOR per segment edge of each frame's lanes ----
+            const uint32_t Wc = hole_shift(lds, x, kStHoleChunk + 4u * j, 0u);
+            const uint32_t P = wave_xor_scan(contrib ? Wc : 0u);
+            const uint32_t Pp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0x138, 0xF, 0xF, true);   // wave_shr:1
+            const bool seg_end = lane == 63 || ((Mst >> (lane + 1)) & 1ull);
+            const uint32_t v = (seg_end ? P : 0u) ^ ((isst && lane > 0) ? Pp : 0u);
+            if (o >= 0 && v) atomicXor(&acc[(uint32_t)o & 127u], v);
             base_cnt += (uint32_t)__popcll(Mst);
-            const uint64_t Mc = __ballot(closes);
-            if (Mc) closed_up_to((uint32_t)__builtin_amdgcn_readlane(A, 63 - __builtin_clzll(Mc)) + 1u);
-        }
-        // the unit's end at the very end of its last item: no item holds its mark; T' = 0 there
-        if (E == kStItem * nitems) {
-            wave_lds_sync();
-            if (lane == 0) {
-                res[last & 127u] = ~acc[last & 127u];
-                acc[last & 127u] = 0u;
+            // frames before the last one starting here have ended (all of them at the unit's end);
+            // a cursor batch all of whose frames have ended closes, and the cursor moves on
+            uint32_t ended = closed;
+            if (Mst) ended = (uint32_t)__builtin_amdgcn_readlane((int)bf, 63 - __builtin_clzll(Mst));
+            if (Mend) ended = nf;
+            if (ended >= 64u * (cb + 1u) && 64u * (cb + 1u) <= last) {
+                close_pass(cb, 64u, eA, lA);
+                closed = 64u * (cb + 1u);
+                cb++;
+                eA = eB;
+                lA = lB;
+                const uint32_t g = 64u * (cb + 1u) + (uint32_t)lane;
+                const bool act = g < nf;
+                lB = act ? p.len[f0 + g] : kStMinLen;
+                eB = act ? (uint32_t)(p.off[f0 + g] - o0) + lB : 0u;
             }
-            closed_up_to(nf);
+        };
+        uint32_t W0[16], W1[16];
+#ifdef FCS_ST_REGLOAD
+        load_item(X0, W0);
+#endif
+        for (uint32_t t = 0; t < nitems; t += 2) {
+            item(t, W0, W1);
+            if (t + 1 < nitems) item(t + 1, W1, W0);
         }
-        if ((fin >> 6) * 64u < nf) flush(fin >> 6, nf - (fin >> 6) * 64u);
+        // the last batch (A, or B when A closed in the last item) closes at the unit's end
+        if (closed < nf) {
+            if ((closed >> 6) == cb) close_pass(cb, nf - closed, eA, lA);
+            else close_pass(cb + 1u, nf - closed, eB, lB);
+            closed = nf;
+        }
         wave_lds_sync();
     }
     flush_bad<kStBad>(p, lds);
