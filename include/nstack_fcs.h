@@ -143,10 +143,12 @@ int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stre
 int fcs_timed_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_t n,
                         uint32_t *out, void *stream, int reps, float *ms_per_launch);
 
-/* Test introspection: the number of 512-frame units the last arena-stream launch (windowed
- * variable-length batches) left to fcs_flat_kernel because their frames are not packed or not
- * 64..1536 B long; -1 before any. Synchronises the device. */
+/* Test introspection: the number of units (fcs_debug_stream_unit_frames() frames each) the last
+ * arena-stream launch (windowed variable-length batches) left to fcs_flat_kernel because their
+ * frames are not packed or not 64..1536 B long; -1 before any. Synchronises
+ * the device. */
 int64_t fcs_debug_stream_listed(void);
+uint32_t fcs_debug_stream_unit_frames(void);
 /* Test introspection: copy the constant tables the kernel stages into LDS (GF(2) operators of
  * the CRC, built on the host once; no frame data involved). Returns words written or -errno. */
 int fcs_tables_blob(uint32_t *out, uint64_t words);

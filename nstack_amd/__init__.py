@@ -22,7 +22,7 @@ __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fi
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_debug_stream_listed", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
@@ -90,6 +90,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_engine_stats": (None, [c.POINTER(u64)] * 4),
         "fcs_engine_host_fallbacks": (u64, []),
         "fcs_debug_stream_listed": (c.c_int64, []),
+        "fcs_debug_stream_unit_frames": (u32, []),
         "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
@@ -282,6 +283,11 @@ def engine_stats() -> dict:
 def stream_listed() -> int:
     """Units of the last arena-stream launch left to fcs_flat_kernel (fcs_debug_stream_listed)."""
     return int(load().fcs_debug_stream_listed())
+
+
+def stream_unit_frames() -> int:
+    """Frames per unit of the arena-stream kernel's dispenser (fcs_debug_stream_unit_frames)."""
+    return int(load().fcs_debug_stream_unit_frames())
 
 
 def engine_host_stats() -> dict:

@@ -466,6 +466,9 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     p.hi4 = ceil4((uint64_t)arena + arena_bytes);
     p.zmax = fcs::kChunkBytes;
     p.blob = ds->d_blob;
+#ifdef FCS_STAMPS
+    p.dbg = g_dbg;
+#endif
     const bool windowed = n > g_var_threshold.load(std::memory_order_relaxed);
     const int grid = grid_for(ds, n, fcs::kWgThreads);
 #ifndef FCS_NO_STREAM   // measurement-only: every windowed batch through fcs_flat_kernel alone
@@ -1533,6 +1536,8 @@ uint32_t ether_fcs(const void *data, size_t bsize) {
 }
 
 uint64_t fcs_engine_host_fallbacks(void) { return g_host_fallbacks.load(std::memory_order_relaxed); }
+
+uint32_t fcs_debug_stream_unit_frames(void) { return fcs::kStUnitFrames; }
 
 int64_t fcs_debug_stream_listed(void) {
     uint32_t *d = g_last_stream_count.load(std::memory_order_relaxed);

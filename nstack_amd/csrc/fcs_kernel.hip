@@ -1596,27 +1596,32 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 // (off[i + 1] == off[i] + len[i]) and 64..1536 B long is taken here; any other unit is listed
 // in p.ulist for fcs_flat_kernel, launched right after on the same stream.
 // A unit's bytes are walked in 4 KiB items at fixed arena positions (the first item at the 16-B
-// boundary below the unit's first frame): one coalesced LDS-DMA per item, issued while the
-// previous item is computed, no dealing. Lane l's chunk is the item's bytes [64 l, 64 l + 64)
-// (LDS at 80 l: conflict-free ds_read_b128); its chain L runs over all 16 words from register 0.
+// boundary below the unit's first frame): one coalesced LDS-DMA per item (four 1 KiB rows from one
+// address register), issued while the previous item is computed, no dealing. Lane l's chunk is the
+// item's bytes [64 l, 64 l + 64); its 16-B pieces sit in LDS swizzled (piece m of chunk l at
+// 64 l + 16 ((m + l / 4) mod 4)), so the four ds_read_b128 of a chunk are conflict-free without
+// padding. Its chain L runs over all 16 words from register 0.
 // A frame starts in at most one place of a chunk (frames >= 64 B); there the lane takes a tap of
 // its chain, T' = A_4(s_k ^ (w_k & the k-th word's bytes before the boundary)), s_k the chain
 // after k = sigma / 4 words, and records it for the frame starting there (it is also the end tap
 // of the frame before). Every chunk goes to the frame holding its last byte, shifted by whole
 // chunks to the chunk holding that frame's end, A_{64 j}(L) with j = le - l - 1; the lanes of one
-// frame are summed by a wave-wide XOR scan and reach its LDS accumulator with one xor at each
-// segment edge. Once 64 frames have ended, one pass closes them, a frame per lane:
+// frame are summed by a wave-wide XOR scan, and the lane ending the frame's run of lanes adds the
+// run's sum to the frame's LDS accumulator (one plain read-modify-write per frame and item: an LDS
+// atomic here made the compiler wait for the next item's DMA, vmcnt(0), before it). Once 64
+// frames have ended, one pass closes them, a frame per lane:
 //   acc ^= A_{64 (le - ls - 1)}(A_{4 (15 - k_s)}(T'_s) ^ A_{64 - sigma_s}(~0))   (its start)
 //   R(~0, frame) = A_{r_e - 4}(T'_e ^ A_{4 (k_e + 1)}(acc)),  sigma_e = 4 k_e + r_e   (its end)
-// and stores the 64 FCSs as one 256-B row.
-// LDS (160 KiB): the 32 KiB slice tables of fcs_dma_kernel with, in the row holes, A_{64 j}
+// and stores the 64 FCSs as one 256-B row. The frames' ends and lengths stay in registers from
+// the unit's packed check (one word per frame), so no global load waits inside the item loop.
+// LDS (144 KiB): the 32 KiB slice tables of fcs_dma_kernel with, in the row holes, A_{64 j}
 // (j = 0..23), A_{4 i} (i = 0..16), A_{-d} (d = 1..4), K1[sigma] = A_{64 - sigma}(~0), the
-// chunk marks of every wave and the verify counters; 16 slots of 5 KiB; per wave accumulators
+// chunk marks of every wave and the verify counters; 16 slots of 4 KiB; per wave accumulators
 // and start taps of 128 frames.
 // ---------------------------------------------------------------------------------------------
 constexpr uint32_t kStChunk = 64;
 constexpr uint32_t kStItem = 64 * kStChunk;
-constexpr uint32_t kStSlotBytes = 5120;
+constexpr uint32_t kStSlotBytes = kStItem;
 constexpr int kStWaves = kWgThreads / 64;
 constexpr uint32_t kStHoleChunk = 0;                                   // A_{64 j}: 4 holes each
 constexpr uint32_t kStHoleWord = kStHoleChunk + 4 * kStChunkTabs;     // A_{4 i}
@@ -1631,19 +1636,40 @@ constexpr uint32_t kStRings = kStSlots + 16 * kStSlotBytes;           // per wav
 constexpr uint32_t kStLdsBytes = kStRings + 16 * 1024;
 static_assert(kStLdsBytes <= 163840, "LDS per CU");
 constexpr uint32_t kMarkStart = 1u << 31, kMarkEnd = 1u << 30;
+// A frame's end (relative to the unit's first item) and length in one word: end << 11 | len
+// (ends < 2^20: 512 frames of at most 1536 B; lengths < 2^11).
+constexpr uint32_t kStLenBits = 11;
+static_assert(kStUnitFrames * kStMaxLen + 16 < (1u << (32 - kStLenBits)) && kStMaxLen < (1u << kStLenBits), "packing");
+// FCS_STAMPS (measurement-only): per-wave s_memtime sums of the item's phases (tools/stamps_stream.py)
+#ifdef FCS_STAMPS
+#define ST_T(v)                              \
+    __builtin_amdgcn_sched_barrier(0);       \
+    const uint64_t v = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0);
+#else
+#define ST_T(v)
+#endif
 #ifndef FCS_ST_AUX   // cache policy of the item DMA's middle rows (measurement-only override)
 #define FCS_ST_AUX 2
 #endif
 
-// A_n(s) ^ extra from the nibble table at holes h .. h + 3 (nibble t at hole h + t / 2, +64 B for
-// odd t); h may differ per lane.
+// A_n(s) ^ extra from the nibble table at holes h .. h + 3 (h = 4 q for table q; h may differ per
+// lane). Nibble t sits in hole h + t / 2, in the half (t + q) & 1 of its 32 banks: lanes shifting by
+// tables of both parities in one lookup spread over all 32 banks instead of 16 (the chunk shifts'
+// table index is data-dependent, so a lookup mixes tables; same-address reads broadcast).
+#ifndef FCS_ST_NOSKEW
+constexpr uint32_t kStSkew = 1;
+#else   // measurement-only: every table's even nibbles in the low half (round-3 first layout)
+constexpr uint32_t kStSkew = 0;
+#endif
 __device__ __forceinline__ uint32_t hole_shift(const uint8_t *lds, uint32_t s, uint32_t h, uint32_t extra) {
     uint32_t r[8];
     const uint32_t base = h * 256u + kDmaHole;
+    const uint32_t ev = 64u * ((h >> 2) & kStSkew), od = 64u - ev;   // byte offset of the even / odd nibbles' half
 #pragma unroll
     for (int t = 0; t < 8; t++) {
         const uint32_t sh = (4 * t >= 2) ? (s >> (4 * t - 2)) : (s << 2);
-        r[t] = lds_rd(lds, base + 256u * (uint32_t)(t >> 1) + 64u * (uint32_t)(t & 1) + (sh & 0x3Cu));
+        r[t] = lds_rd(lds, base + 256u * (uint32_t)(t >> 1) + ((t & 1) ? od : ev) + (sh & 0x3Cu));
     }
     return xor9(r, extra);
 }
@@ -1668,7 +1694,8 @@ __device__ __forceinline__ void stage_stream_tables(const KParams &p, uint8_t *l
     }
     for (int i = tid; i < (kStChunkTabs + kStWordTabs + kStInvTabs) * 128; i += kWgThreads) {
         const uint32_t q = (uint32_t)i >> 7, t = ((uint32_t)i >> 4) & 7u, e = (uint32_t)i & 15u;
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * q + (t >> 1)) + 64u * (t & 1u) + 4u * e) = p.blob[kBlobStream + i];
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * q + (t >> 1)) + 64u * ((t + (q & kStSkew)) & 1u) + 4u * e) =
+            p.blob[kBlobStream + i];
     }
     for (int i = tid; i < 64; i += kWgThreads)
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kStHoleK1 + (uint32_t)i / 32u) + ((uint32_t)i % 32u) * 4u) =
@@ -1699,52 +1726,45 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         return reinterpret_cast<uint32_t *>(lds + dma_hole(kStHoleMark + 2u * wave + (c >> 5)) + (c & 31u) * 4u);
     };
     auto k1_of = [&](uint32_t sg) { return lds_rd(lds, dma_hole(kStHoleK1 + sg / 32u) + (sg % 32u) * 4u); };
-    // item DMA: instruction q, lane i moves LDS piece 64 q + i = 5 l + m (chunk l at 80 l; m = 4
-    // is the pad) from arena byte X + 64 l + 16 m
-    uint32_t goff[5];
-    bool gon[5];
-#pragma unroll
-    for (int q = 0; q < 5; q++) {
-        const uint32_t pj = 64u * (uint32_t)q + (uint32_t)lane, l = pj / 5u, m = pj - 5u * l;
-        goff[q] = 64u * l + 16u * m;
-        gon[q] = m < 4u;
-    }
+    // item DMA: row q, lane i moves the 16-B piece that sits at slot byte 1024 q + 16 i: chunk
+    // l = 16 q + i / 4, piece m = (i - i / 16) mod 4 (the swizzle), arena byte X + 1024 q + goff
+    const uint32_t goff = 64u * ((uint32_t)lane >> 2) + 16u * (((uint32_t)lane - ((uint32_t)lane >> 4)) & 3u);
     const uint64_t hi16 = (p.hi4 + 15) & ~15ull;
     auto dma_item = [&](uint64_t X) {
         typedef __attribute__((address_space(3))) void lds_void;
-#pragma unroll
-        for (int q = 0; q < 5; q++) {
-            const uint64_t a = X + goff[q];
-            if (gon[q] && a < hi16) {   // first and last rows at the default policy (lines shared with neighbours)
-                if (q == 0 || q == 4)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), (lds_void *)(slot + 1024 * q), 16, 0, 0);
-                else
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), (lds_void *)(slot + 1024 * q), 16, 0,
-                                                     FCS_ST_AUX);
-            }
+        const uint64_t a = X + goff;
+        lds_void *ls = (lds_void *)slot;
+        if (X + kStItem <= hi16) {   // wave-uniform: the whole item lies inside the arena's 16-B pieces
+            // first and last rows at the default policy (lines shared with the neighbouring items)
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 1024, FCS_ST_AUX);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 2048, FCS_ST_AUX);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 3072, 0);
+        } else {
+            if (a < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 0, 0);
+            if (a + 1024 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 1024, FCS_ST_AUX);
+            if (a + 2048 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 2048, FCS_ST_AUX);
+            if (a + 3072 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 3072, 0);
         }
     };
-    const u32x4 *chunk = reinterpret_cast<const u32x4 *>(slot + 80u * (uint32_t)lane);
-    // measurement build (FCS_ST_REGLOAD): the lane loads its own 64-B chunk into registers, the next
-    // item's loads in flight while the current one is computed (no slot)
-    auto load_item = [&](uint64_t X, uint32_t (&wv)[16]) {
-        const uint64_t a = X + 64u * (uint32_t)lane;
-#pragma unroll
-        for (int i = 0; i < 4; i++) {
-            const u32x4 v = a + 16u * (uint32_t)i < hi16 ? gload<u32x4>(a + 16u * (uint32_t)i) : u32x4{0u, 0u, 0u, 0u};
-            wv[4 * i] = v.x;
-            wv[4 * i + 1] = v.y;
-            wv[4 * i + 2] = v.z;
-            wv[4 * i + 3] = v.w;
-        }
-    };
-    (void)load_item;
+    // piece m of this lane's chunk in the slot (loop invariants)
+    const uint32_t cbase = 64u * (uint32_t)lane, sw = ((uint32_t)lane >> 2) & 3u;
+    const u32x4 *pc[4] = {reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((0u + sw) & 3u)),
+                          reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((1u + sw) & 3u)),
+                          reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((2u + sw) & 3u)),
+                          reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((3u + sw) & 3u))};
     constexpr int kQ = (int)(kStUnitFrames / 64);
+    constexpr uint32_t kLenMask = (1u << kStLenBits) - 1u;
 
     constexpr uint64_t kEnd = Dispenser::kEnd;
     const uint64_t units = (p.n + kStUnitFrames - 1) / kStUnitFrames;
+#ifdef FCS_STAMPS   // [0] unit prologue [1] marks [2] slot wait [3] words + DMA + chain [4] rest [5] items [6] units [7] all
+    uint64_t sts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const uint64_t st_begin = __builtin_amdgcn_s_memtime();
+#endif
     Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kStWaves, (uint64_t)blockIdx.x * kStWaves + wave, lane, 100, 1, 8);
     for (uint64_t u = D.first(); u != kEnd; u = D.next(u)) {
+        ST_T(tu0)
         const uint64_t f0 = u * kStUnitFrames;
         const uint32_t nf = (uint32_t)((p.n - f0) < kStUnitFrames ? (p.n - f0) : kStUnitFrames);
         // ---- take the unit only if its frames are packed and 64..1536 B ----
@@ -1782,51 +1802,62 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
         const uint64_t X0 = s0 & ~15ull;
-#ifndef FCS_ST_REGLOAD
         dma_item(X0);
-#endif
         const uint64_t o0 = X0 - p.base;   // arena offset of X0
         const uint32_t last = nf - 1;
-        // The cursor: frames 64 cb + lane (batch A) and 64 (cb + 1) + lane (batch B): end (relative
-        // to X0) and length. An item's starts lie in these two batches (frames >= 64 B).
-        uint32_t cb = 0;
-        uint32_t eA = (uint32_t)(S[0] + Ln[0] - o0), lA = Ln[0];
-        uint32_t eB = (uint32_t)(S[1] + Ln[1] - o0), lB = Ln[1];
+        // every frame of the unit: end (relative to X0) << 11 | length
+        uint32_t pk[kQ];
+#pragma unroll
+        for (int q = 0; q < kQ; q++) pk[q] = ((uint32_t)(S[q] + Ln[q] - o0) << kStLenBits) | Ln[q];
         uint32_t E = 0;   // the unit's end
 #pragma unroll
         for (int q = 0; q < kQ; q++)
-            if ((last >> 6) == (uint32_t)q) E = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(S[q] + Ln[q] - o0), (int)(last & 63u));
+            if ((last >> 6) == (uint32_t)q) E = (uint32_t)__builtin_amdgcn_readlane((int)pk[q], (int)(last & 63u)) >> kStLenBits;
+        // The cursor: frames 64 cb + lane (batch A, pk[0]) and 64 (cb + 1) + lane (batch B, pk[1]);
+        // the batches after them follow in pk[2..] (shifted down as the cursor moves: no indexed
+        // register access, which the compiler would turn into scratch memory). An item's starts lie
+        // in batches A and B (frames >= 64 B).
+        uint32_t cb = 0;
         const uint32_t nitems = (E + kStItem - 1) / kStItem;
+#ifdef FCS_STAMPS
+        {
+            ST_T(tu1)
+            sts[0] += tu1 - tu0;
+            sts[6]++;
+        }
+#endif
         uint32_t nsf = 0, base_cnt = 0, closed = 0;
         uint32_t tend = 0;   // end tap of the unit's last frame (0 when it ends on an item edge)
-        // close frames 64 b .. 64 b + cnt - 1 (all ended; e, L: their ends and lengths): start term,
+        // close frames 64 b .. 64 b + cnt - 1 (all ended; pw: their end << 11 | length): start term,
         // end tap, one 256-B store
-        auto close_pass = [&](uint32_t b, uint32_t cnt, uint32_t e, uint32_t L) {
+        auto close_pass = [&](uint32_t b, uint32_t cnt, uint32_t pw) {
             wave_lds_sync();
             const uint32_t g = 64u * b + (uint32_t)lane;
+            const uint32_t e = pw >> kStLenBits, L = pw & kLenMask;
             const uint32_t st = e - L, ss = st & 63u, se = e & 63u;
             const uint32_t Ts = tap[g & 127u];
             const uint32_t Te = g < last ? tap[(g + 1u) & 127u] : tend;
             const uint32_t a0 = acc[g & 127u];
             wave_lds_sync();
             acc[g & 127u] = 0u;
+#ifdef FCS_ST_ABL_NOCLOSE   // measurement-only: the close's four shifts replaced by XORs (wrong FCS)
+            const uint32_t reg = Ts ^ Te ^ a0 ^ k1_of(ss) ^ se;
+#else
             const uint32_t U = hole_shift(lds, Ts, kStHoleWord + 4u * (15u - (ss >> 2)), k1_of(ss));
             const uint32_t js = (uint32_t)lane < cnt ? (e >> 6) - (st >> 6) - 1u : 0u;
             const uint32_t a = hole_shift(lds, U, kStHoleChunk + 4u * js, a0);
             const uint32_t inner = hole_shift(lds, a, kStHoleWord + 4u * ((se >> 2) + 1u), Te);
             const uint32_t reg = hole_shift(lds, inner, kStHoleInv + 4u * (3u - (se & 3u)), 0u);
+#endif
             emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + g, ~reg);
         };
-        auto item = [&](uint32_t t, uint32_t (&wc)[16], uint32_t (&wn)[16]) {
+        for (uint32_t t = 0; t < nitems; t++) {
             const uint32_t Xr = kStItem * t;
-#ifdef FCS_ST_REGLOAD
-            if (t + 1 < nitems) load_item(X0 + Xr + kStItem, wn);   // the next item's bytes, into registers
-#else
-            (void)wn;
-#endif
+            ST_T(ti0)
             // ---- marks: frames starting in this item, and the unit's end ----
             const uint32_t gA = 64u * cb + (uint32_t)lane, gB = gA + 64u;
-            const uint32_t sA = eA - lA, sB = eB - lB;
+            const uint32_t eA = pk[0] >> kStLenBits, eB = pk[1] >> kStLenBits;
+            const uint32_t sA = eA - (pk[0] & kLenMask), sB = eB - (pk[1] & kLenMask);
             const bool inA = gA >= nsf && gA < nf && sA < Xr + kStItem;
             const bool inB = gB >= nsf && gB < nf && sB < Xr + kStItem;
             if (inA) *mark_at((sA - Xr) >> 6) = kMarkStart | (gA << 6) | ((sA - Xr) & 63u);
@@ -1835,8 +1866,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             nsf += (uint32_t)__popcll(__ballot(inA)) + (uint32_t)__popcll(__ballot(inB));
             // chunk of the next boundary past this item: the end of the last frame started so far
             const uint32_t gl = nsf - 1u;
-            const uint32_t el = (gl >> 6) == cb ? (uint32_t)__builtin_amdgcn_readlane((int)eA, (int)(gl & 63u))
-                                                : (uint32_t)__builtin_amdgcn_readlane((int)eB, (int)(gl & 63u));
+            const uint32_t el = (uint32_t)__builtin_amdgcn_readlane((int)((gl >> 6) == cb ? eA : eB), (int)(gl & 63u));
             const uint32_t le_far = (el - Xr) >> 6;
             wave_lds_sync();
             const uint32_t mk = lds_rd(lds, mark_lane);
@@ -1844,32 +1874,34 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             const bool isst = (mk & kMarkStart) != 0, isend = (mk & kMarkEnd) != 0;
             const uint32_t sig = mk & 63u, k = sig >> 2, r = sig & 3u, bf = (mk >> 6) & 1023u;
             const uint64_t Mst = __ballot(isst), Mend = __ballot(isend), Mb = Mst | Mend;
-            const uint32_t rank = (uint32_t)__popcll(Mst & ((2ull << lane) - 1ull));
-            const int o = (int)(base_cnt + rank) - 1;                       // frame holding the chunk's last byte
+            const uint64_t upto = Mst & ((2ull << lane) - 1ull);                // starts at or before this lane
+            const int o = (int)(base_cnt + (uint32_t)__popcll(upto)) - 1;     // frame holding the chunk's last byte
             const bool contrib = o >= 0 && Xr + 64u * (uint32_t)lane + 63u < E;
             const uint64_t after = lane == 63 ? 0ull : (Mb & (~0ull << (lane + 1)));
             const uint32_t le = after ? (uint32_t)__builtin_ctzll(after) : le_far;
             const uint32_t j = contrib ? le - (uint32_t)lane - 1u : 0u;
 
-#ifdef FCS_ST_REGLOAD
-            uint32_t (&w)[16] = wc;
-            uint32_t wk = 0;
-#else
             // ---- this item's bytes; the next item's DMA ----
+            ST_T(ti1)
             __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's item has landed
-            uint32_t (&w)[16] = wc;
+            ST_T(ti2)
+#ifdef FCS_STAMPS
+            sts[1] += ti1 - ti0;
+            sts[2] += ti2 - ti1;
+#endif
+            uint32_t w[16];
 #pragma unroll
             for (int i = 0; i < 4; i++) {
-                const u32x4 x = chunk[i];
+                const u32x4 x = *pc[i];
                 w[4 * i] = x.x;
                 w[4 * i + 1] = x.y;
                 w[4 * i + 2] = x.z;
                 w[4 * i + 3] = x.w;
             }
-            const uint32_t wk = lds_rd(slot, 80u * (uint32_t)lane + 4u * k);   // the tap word
+            // the tap word: word k & 3 of piece k / 4
+            const uint32_t wk = lds_rd(slot, cbase + 16u * (((k >> 2) + sw) & 3u) + 4u * (k & 3u));
             __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
             if (t + 1 < nitems) dma_item(X0 + Xr + kStItem);
-#endif
 
             // ---- the chain over 16 words; its state before word k ----
             uint32_t x = w[0], xk = 0;
@@ -1880,12 +1912,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
 #else
 #pragma unroll
             for (int i = 0; i < 16; i++) {
-                if ((uint32_t)i == k) {
-                    xk = x;
-#ifdef FCS_ST_REGLOAD
-                    wk = w[i];
-#endif
-                }
+                if ((uint32_t)i == k) xk = x;
                 x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
             }
 #endif
@@ -1893,14 +1920,28 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             const uint32_t Tp = step4_l8(lds, xk ^ (wk & (0xFFFFFFFFu << (8u * r))), 0u, B, SEL);
             if (isst) tap[bf & 127u] = Tp;
             if (Mend) tend = (uint32_t)__builtin_amdgcn_readlane((int)Tp, (int)__builtin_ctzll(Mend));
+#ifdef FCS_STAMPS
+            ST_T(ti3)
+            sts[3] += ti3 - ti2;
+#endif
 
-            // ---- chunk contributions: one XOR per segment edge of each frame's lanes ----
+            // ---- chunk contributions: the lane ending a frame's run of lanes adds the run's sum ----
+#ifdef FCS_ST_ABL_NOSHIFT   // measurement-only: no chunk shift (wrong FCS)
+            const uint32_t Wc = x ^ j;
+#else
             const uint32_t Wc = hole_shift(lds, x, kStHoleChunk + 4u * j, 0u);
+#endif
             const uint32_t P = wave_xor_scan(contrib ? Wc : 0u);
-            const uint32_t Pp = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)P, 0x138, 0xF, 0xF, true);   // wave_shr:1
+            // the run of this lane's frame starts at the last start at or before it (if any); its sum
+            // is P here minus P just before that start
+            const int sl = upto ? 63 - __builtin_clzll(upto) : 0;
+            const uint32_t Pb = (uint32_t)__shfl((int)P, sl > 0 ? sl - 1 : 0);
             const bool seg_end = lane == 63 || ((Mst >> (lane + 1)) & 1ull);
-            const uint32_t v = (seg_end ? P : 0u) ^ ((isst && lane > 0) ? Pp : 0u);
-            if (o >= 0 && v) atomicXor(&acc[(uint32_t)o & 127u], v);
+            const uint32_t v = P ^ (sl > 0 ? Pb : 0u);
+            if (o >= 0 && seg_end && v) {
+                uint32_t *ap = &acc[(uint32_t)o & 127u];
+                *ap = *ap ^ v;
+            }
             base_cnt += (uint32_t)__popcll(Mst);
             // frames before the last one starting here have ended (all of them at the unit's end);
             // a cursor batch all of whose frames have ended closes, and the cursor moves on
@@ -1908,33 +1949,34 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             if (Mst) ended = (uint32_t)__builtin_amdgcn_readlane((int)bf, 63 - __builtin_clzll(Mst));
             if (Mend) ended = nf;
             if (ended >= 64u * (cb + 1u) && 64u * (cb + 1u) <= last) {
-                close_pass(cb, 64u, eA, lA);
+                close_pass(cb, 64u, pk[0]);
                 closed = 64u * (cb + 1u);
                 cb++;
-                eA = eB;
-                lA = lB;
-                const uint32_t g = 64u * (cb + 1u) + (uint32_t)lane;
-                const bool act = g < nf;
-                lB = act ? p.len[f0 + g] : kStMinLen;
-                eB = act ? (uint32_t)(p.off[f0 + g] - o0) + lB : 0u;
+#pragma unroll
+                for (int q = 0; q + 1 < kQ; q++) pk[q] = pk[q + 1];
             }
-        };
-        uint32_t W0[16], W1[16];
-#ifdef FCS_ST_REGLOAD
-        load_item(X0, W0);
+#ifdef FCS_STAMPS
+            ST_T(ti4)
+            sts[4] += ti4 - ti3;
+            sts[5]++;
 #endif
-        for (uint32_t t = 0; t < nitems; t += 2) {
-            item(t, W0, W1);
-            if (t + 1 < nitems) item(t + 1, W1, W0);
         }
         // the last batch (A, or B when A closed in the last item) closes at the unit's end
         if (closed < nf) {
-            if ((closed >> 6) == cb) close_pass(cb, nf - closed, eA, lA);
-            else close_pass(cb + 1u, nf - closed, eB, lB);
+            if ((closed >> 6) == cb) close_pass(cb, nf - closed, pk[0]);
+            else close_pass(cb + 1u, nf - closed, pk[1]);
             closed = nf;
         }
         wave_lds_sync();
     }
+#ifdef FCS_STAMPS
+    if (p.dbg != nullptr && lane == 0) {
+        sts[7] = __builtin_amdgcn_s_memtime() - st_begin;
+        const uint32_t wv = blockIdx.x * kStWaves + wave;
+#pragma unroll
+        for (int i = 0; i < 8; i++) p.dbg[wv * 8 + i] = sts[i];
+    }
+#endif
     flush_bad<kStBad>(p, lds);
 }
 

@@ -32,7 +32,10 @@ struct KParams {
 };
 // Arena-stream kernel geometry: units of frames handed out by the dispenser; 64-B lane chunks at
 // fixed arena positions, 64 per 4 KiB item; frames of 64..1536 B, packed within a unit.
-constexpr uint32_t kStUnitFrames = 512;
+#ifndef FCS_ST_UNIT   // measurement-only override
+#define FCS_ST_UNIT 512
+#endif
+constexpr uint32_t kStUnitFrames = FCS_ST_UNIT;
 constexpr uint32_t kStMinLen = 64, kStMaxLen = 1536;
 
 // Workgroup sizes (one workgroup per CU either way: the LDS tables take 150 KiB). The 1504..1536-B

@@ -15,7 +15,7 @@ import nstack_amd as na  # noqa: E402
 
 pytestmark = pytest.mark.gpu
 
-UNIT = 512
+UNIT = 512   # frames per unit of the product build (checked against the library below)
 
 
 @pytest.fixture(scope="module")
@@ -23,6 +23,8 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     torch.cuda.set_device(0)
+    global UNIT
+    UNIT = na.stream_unit_frames()   # measurement builds may use other unit sizes
     return torch.device("cuda:0")
 
 
@@ -89,7 +91,7 @@ def test_units_ending_on_item_boundaries(dev, oracle):
 def test_mixed_units_hand_off(dev, oracle):
     """Units broken in different ways are listed for fcs_flat_kernel; the others stream. Breaks:
     a 63-B frame, a 1537-B frame, an empty frame, a gap, two frames swapped, overlapping frames."""
-    n = 40 * UNIT
+    n = 40 * max(UNIT, 512)   # above the windowed-path threshold (16384 frames) for any unit size
     ln = _imix(n, 21).astype(np.uint64)
     breaks = {3: "short", 7: "long", 11: "empty", 17: "gap", 23: "swap", 29: "overlap"}
     ln[3 * UNIT + 100] = 63
@@ -109,7 +111,7 @@ def test_mixed_units_hand_off(dev, oracle):
 
 def test_unit_boundaries_between_streamed_units_need_not_touch(dev, oracle):
     """Units are independent: consecutive units may be separated by gaps or out of order."""
-    U = 40
+    U = 40 * max(UNIT, 512) // UNIT   # above the windowed-path threshold for any unit size
     n = U * UNIT
     ln = _imix(n, 31).astype(np.uint64)
     off = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.uint64)
