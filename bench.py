@@ -253,7 +253,7 @@ def imix_lengths(n: int, seed: int = 7):
 
 def host_inclusive_imix(torch, na, dev, stream, rng, host_gib=4.0):
     """IMIX frames packed in a pinned host arena (fcs_host_alloc) -> ether_fcs_batch_host (chunked H2D
-    of frames + offsets + lengths -> flat kernel -> D2H of the CRCs). Ceiling: plain async H2D copies
+    of frames + offsets + lengths -> arena-stream kernel -> D2H of the CRCs). Ceiling: plain async H2D copies
     of the same pinned arena plus the 12 B of metadata per frame, same process."""
     import numpy as np
     n = int(host_gib * GIB / 355.83)   # frames whose mean length is 4270 / 12 B
@@ -299,7 +299,7 @@ def host_inclusive_imix(torch, na, dev, stream, rng, host_gib=4.0):
         torch.cuda.empty_cache()
         gbs = total / secs / 1e9
         return {"what": "IMIX frames in pinned host memory + offsets/lengths in pageable host arrays -> "
-                        "ether_fcs_batch_host (chunked H2D -> flat kernel -> D2H of CRCs); PCIe bound, never `value`",
+                        "ether_fcs_batch_host (chunked H2D -> arena-stream kernel -> D2H of CRCs); PCIe bound, never `value`",
                 "frames": n, "bytes": total, "metadata_bytes": n * 12, "ms": round(secs * 1e3, 3),
                 "GB_s": round(gbs, 2), "Mframes_s": round(n / secs / 1e6, 1),
                 "roofline": {"bound": "pcie", "achieved": round(gbs, 2), "peak": 63.0, "unit": "GB/s",

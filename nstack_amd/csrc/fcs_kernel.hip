@@ -1649,6 +1649,9 @@ static_assert(kStUnitFrames * kStMaxLen + 16 < (1u << (32 - kStLenBits)) && kStM
 #else
 #define ST_T(v)
 #endif
+#ifndef FCS_ST_CHAINS   // independent chains per 64-B chunk (1 or 2; measurement override)
+#define FCS_ST_CHAINS 1
+#endif
 #ifndef FCS_ST_AUX   // cache policy of the item DMA's middle rows (measurement-only override)
 #define FCS_ST_AUX 2
 #endif
@@ -1909,6 +1912,20 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
 #pragma unroll
             for (int i = 1; i < 16; i++) x ^= w[i];
             xk = x ^ k;
+#elif FCS_ST_CHAINS == 2
+            // two independent 8-word chains, c0 over words 0..7 and c1 over 8..15, each from register
+            // 0 (half the dependent lookups of one chain): L = A_32(c0) ^ c1, and the state before
+            // word k >= 8 is c1_{k-8} ^ A_{4 (k-8)}(c0), so that tap adds A_{4 (k-7)}(c0)
+            uint32_t y = w[8];
+#pragma unroll
+            for (int i = 0; i < 8; i++) {
+                if ((uint32_t)i == k) xk = x;
+                if ((uint32_t)(i + 8) == k) xk = y;
+                x = step4_l8(lds, x, i < 7 ? w[i + 1] : 0u, B, SEL);
+                y = step4_l8(lds, y, i < 7 ? w[i + 9] : 0u, B, SEL);
+            }
+            const uint32_t c0 = x;
+            x = hole_shift(lds, c0, kStHoleWord + 4u * 8u, y);
 #else
 #pragma unroll
             for (int i = 0; i < 16; i++) {
@@ -1917,7 +1934,12 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             }
 #endif
             // the tap: word k's bytes before the boundary finish the prefix (x_k ^ w_k = s_k)
+#if FCS_ST_CHAINS == 2 && !defined(FCS_ST_NOCRC)
+            const uint32_t Tp = hole_shift(lds, k >= 8u ? c0 : 0u, kStHoleWord + 4u * (k >= 8u ? k - 7u : 0u),
+                                           step4_l8(lds, xk ^ (wk & (0xFFFFFFFFu << (8u * r))), 0u, B, SEL));
+#else
             const uint32_t Tp = step4_l8(lds, xk ^ (wk & (0xFFFFFFFFu << (8u * r))), 0u, B, SEL);
+#endif
             if (isst) tap[bf & 127u] = Tp;
             if (Mend) tend = (uint32_t)__builtin_amdgcn_readlane((int)Tp, (int)__builtin_ctzll(Mend));
 #ifdef FCS_STAMPS
