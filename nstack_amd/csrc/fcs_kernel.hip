@@ -1257,6 +1257,15 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
         if (un != kEnd) issue(un, rn);
 
         // ---- this item ----
+#ifdef FCS_SEGIL_NOCRC   // measurement-only: the window words XORed instead of the CRC work (wrong FCS)
+        {
+            uint32_t xx = ra;
+#pragma unroll
+            for (int i = 0; i <= kChunkWords; i++) xx ^= d[i];
+            acc = row_xor(xx ^ acc);
+        }
+        if (false) {
+#endif
         uint32_t w[kChunkWords];
 #pragma unroll
         for (int i = 0; i < kChunkWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ra);
@@ -1294,6 +1303,9 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
         uint32_t v = lane_shift_dma(lds, mv, lanebase);
         if (r == 0 && fdead) v = 0u;
         acc = row_xor(v);
+#ifdef FCS_SEGIL_NOCRC
+        }
+#endif
         if (r == m - 1) {   // results of consecutive units leave as one coalesced store (as fcs_dma_kernel)
             const uint32_t k = (uint32_t)(u & 15u);
             const uint32_t vq = (uint32_t)__shfl((int)~acc, (lane & 3) * kGroup);

@@ -142,10 +142,15 @@ inline bool fixed_dma(const KParams &p) {
 }
 // Frame-interleaved segment kernel (fcs_segil_kernel): fixed lengths over kDmaCover bytes, any
 // stride; units of 4 frames, 12 waves per workgroup (8 KiB LDS slots). A frame costs
-// m = ceil(len / 1524) items whatever its front segment holds, so it is selected when
-// len >= 0.75 * 1524 m (tools/ab.py against the register-load generic kernel: 2500 B +4.8 %,
-// 4573 B +0.6 %, 6100 B +3.6 %, 9000 B +8.5 %, 10000 B +10 %, 65536 B +16 %; below the bound 1530 B
-// -30 %, 1600 B -5 %, 2000 B -1.3 %, 3049 B -9 %, which keep the generic kernel).
+// m = ceil(len / 1524) items whatever its front segment holds; the register-load generic kernel
+// walks ceil(len / 1536) segments. The segment kernel is selected (tools/ab.py, one process per
+// length, round 3) when
+//   - m >= 4 (4573 B and 6100 B equal, 9000 B +3 to +8.5 %, 65536 B +16 %), or
+//   - m = 3 and the generic kernel needs 3 segments too, i.e. len > 3072 (3100 B +17 %,
+//     3300 B +16 %; 3049 B -4 %: the generic kernel covers it in 2 segments), or
+//   - m = 2 and len >= 1950 (2000 B +2.7 %, 2285 B +7.4 %; 1560-1900 B -1 to -4 %, and 1525-1536 B
+//     are a single generic segment: -26 %).
+constexpr uint32_t kSegilMinLen2 = 1950;
 constexpr int kSegilWgThreads = 768;
 inline bool fixed_segil(const KParams &p) {
 #ifdef FCS_NO_SEGIL   // measurement-only build
@@ -153,7 +158,13 @@ inline bool fixed_segil(const KParams &p) {
     return false;
 #else
     const uint64_t m = (p.flen + kDmaCover - 1) / kDmaCover;
-    return p.flen > kDmaCover && !fixed_tiny(p) && 4ull * p.flen >= 3ull * kDmaCover * m;
+    if (p.flen <= kDmaCover || fixed_tiny(p)) return false;
+#ifdef FCS_SEGIL_ANY   // measurement-only: every fixed length over 1524 B
+    return true;
+#endif
+    if (m >= 4) return true;
+    if (m == 3) return p.flen > 2u * (uint32_t)kSegBytes;
+    return p.flen >= kSegilMinLen2;
 #endif
 }
 inline int fixed_threads(const KParams &p) {

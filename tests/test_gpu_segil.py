@@ -1,12 +1,13 @@
 """GPU parity of the frame-interleaved segment kernel (fcs_segil_kernel).
 
-Fixed-length frames over 1524 B with len >= 0.75 * 1524 m (m = ceil(len / 1524)) take this kernel,
+Fixed-length frames over 1524 B take this kernel when m = ceil(len / 1524) >= 4, or m = 3 and
+len > 3072, or m = 2 and len >= 1950 (fixed_segil(), fcs_launch.hpp),
 at any stride: a front segment of len - 1524 (m - 1) bytes, then 1524-B segments; item r of a
 wave's unit is segment r of its four frames (one per quarter-wave, four DMA runs), and a frame's
 CRC state goes from item to item through lane 15's chain start. Every case is checked bit-exact
 against the oracle (the CPU restatement of src/ether_fcs.c:4-19): front segments of 1 to 1524
-bytes, both sides of the selection bound (2285 / 2286, 3428 / 3429 B: the shorter ones keep the
-register-load generic kernel), up to 688 segments (1 MiB), all base alignments, strides with no
+bytes, both sides of the selection bounds (1949 / 1950, 3072 / 3073 B: the shorter ones keep the
+register-load generic kernel; 2285 / 2286 and 3428 / 3429 were round 2's bounds), up to 688 segments (1 MiB), all base alignments, strides with no
 gap, odd gaps and large gaps, frame counts that leave partial units, batches large enough for the
 dynamic schedule, and verify mode.
 """
@@ -45,9 +46,10 @@ def run(dev, d, lead, stride, L, n):
     return out.cpu().numpy().view(np.uint32)
 
 
-# front segments of 1 .. 1524 B; the selection bound (2286 = 0.75 * 3048, 3429 = 0.75 * 4572) and one
-# byte below it; the old segmented kernel's bands (2992-3048, 8976-9144, 40392-41148)
-LENS = [1525, 1530, 1536, 1537, 2000, 2285, 2286, 2500, 2992, 3000, 3048, 3049, 3428, 3429, 4572, 4573,
+# front segments of 1 .. 1524 B; the selection bounds (1950, 3073) and one byte below them; round 2's
+# bounds (2286 = 0.75 * 3048, 3429 = 0.75 * 4572); the old segmented kernel's bands (2992-3048,
+# 8976-9144, 40392-41148)
+LENS = [1525, 1530, 1536, 1537, 1949, 1950, 2000, 3072, 3073, 3200, 2285, 2286, 2500, 2992, 3000, 3048, 3049, 3428, 3429, 4572, 4573,
         6000, 6096, 7500, 8976, 9000, 9018, 9143, 9144, 10000, 10472, 16000, 16500, 40392, 41148, 41149,
         64400, 65536, 100000]
 

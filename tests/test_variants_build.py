@@ -29,6 +29,8 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_DMA_PRIO -DFCS_DMA_EDGE_AUX=2 -DFCS_DMA_NO_TRIM -DFCS_DMA_ABL_NOALIGN "
                        "-DFCS_DMA_ABL_NOLDS"),
     ("fcs_kernel.hip", "-DFCS_NO_SEGIL -DFCS_SEGIL_TAIL_AUX=2 -DFCS_SEGIL_SKEW=0"),
+    ("fcs_kernel.hip", "-DFCS_SEGIL_NOCRC -DFCS_SEGIL_ANY"),
+    ("fcs_engine.cpp", "-DFCS_SEGIL_ANY"),
     ("fcs_kernel.hip", "-DFCS_BLOCKED"),
     ("fcs_kernel.hip", "-DFCS_XCD -DFCS_NO_WAVE_SYNC"),
     ("fcs_kernel.hip", "-DFCS_FLAT_NOCRC -DFCS_FLAT_NO_SHORTCUTS -DFCS_FLAT_CHUNK_MAX=8 "
