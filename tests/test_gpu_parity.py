@@ -372,6 +372,34 @@ def test_fixed_host_and_batch_host(dev, var_kernel, oracle):
     assert np.array_equal(out2, oracle_var(oracle, arena, off, ln))
 
 
+@pytest.mark.parametrize("layout", ["packed", "gapped", "shuffled", "jumbo_mix"])
+def test_batch_host_many_chunks(dev, oracle, layout):
+    """ether_fcs_batch_host over ~450 MB of frames: several 128-MiB pipeline chunks on two streams,
+    chunk sizes found by the shrinking min/max/sum pass; shuffled offsets take the gather path
+    (span far larger than the bytes), gapped ones are limited by their span."""
+    rng = np.random.default_rng(["packed", "gapped", "shuffled", "jumbo_mix"].index(layout) + 40)
+    n = 1_200_000
+    ln = imix(n, 17).astype(np.uint64)
+    if layout == "jumbo_mix":
+        ln[rng.integers(0, n, 3000)] = 9000
+        ln[rng.integers(0, n, 3000)] = 0
+    gap = rng.integers(0, 600, n).astype(np.uint64) if layout == "gapped" else np.zeros(n, dtype=np.uint64)
+    start = np.zeros(n, dtype=np.uint64)
+    start[1:] = np.cumsum(ln[:-1] + gap[:-1], dtype=np.uint64)
+    off = start.copy()
+    if layout == "shuffled":
+        perm = rng.permutation(n)
+        off = start[perm]
+        ln = ln[perm]
+    total = int((off + ln).max()) + 16
+    arena = rng.integers(0, 256, total, dtype=np.uint8)
+    out = np.zeros(n, dtype=np.uint32)
+    na.batch_host(arena, arena.nbytes, off, ln.astype(np.uint32), out, n)
+    exp = oracle_var(oracle, arena, off, ln.astype(np.uint32))
+    bad = np.nonzero(out != exp)[0]
+    assert bad.size == 0, f"{bad.size} frames differ, first {int(bad[0])}"
+
+
 def test_tx_mode_matches_ether_send_layout(dev, var_kernel, oracle):
     """ether_send (src/linux/ether.c:222-263): frame = hdr + payload + zero pad, FCS over
     frame_size-4 bytes stored little-endian at the end. Batched TX must produce byte-identical
