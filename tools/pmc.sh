@@ -18,8 +18,8 @@ run() {
 }
 run p1 SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_SMEM SQ_WAVE_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE
 run p2 SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VMEM_RD
-run p3 FETCH_SIZE
-run p4 WRITE_SIZE
+[ -n "${PMC_ALL:-}" ] && run p3 FETCH_SIZE
+[ -n "${PMC_ALL:-}" ] && run p4 WRITE_SIZE
 run p5 SQ_LDS_IDX_ACTIVE SQ_INST_LEVEL_LDS SQ_ACTIVE_INST_SCA SQ_INSTS_BRANCH SQ_INST_LEVEL_VMEM SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_MISC SQ_ACTIVE_INST_FLAT
-run p6 TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
+[ -n "${PMC_ALL:-}" ] && run p6 TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TCP_TCC_READ_REQ_sum TCC_HIT_sum TCC_MISS_sum
 exit 0
