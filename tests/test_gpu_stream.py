@@ -169,3 +169,60 @@ def test_verify_mode_through_stream(dev, oracle):
     okh = ok.cpu().numpy()
     assert sorted(np.nonzero(okh == 0)[0].tolist()) == bad_idx
     assert na.stream_listed() == 0
+
+
+hyp = pytest.importorskip("hypothesis")
+from hypothesis import given, settings, strategies as hst  # noqa: E402
+
+_KINDS = ["imix", "random", "fixed", "short", "long", "empty", "gap", "swap", "overlap", "jumbo"]
+
+
+@settings(max_examples=12, deadline=None, derandomize=True)
+@given(kinds=hst.lists(hst.sampled_from(_KINDS), min_size=34, max_size=48),
+       base=hst.integers(0, 4095), shuffle=hst.booleans(), seed=hst.integers(0, 2**31 - 1))
+def test_unit_mix_fuzz(dev, oracle, kinds, base, shuffle, seed):
+    """Random unit compositions above the windowed threshold: packed units of IMIX, random or fixed
+    lengths stream; units broken one way (a 63-B, 1537-B or empty frame, a gap, a swap, an overlap)
+    or made of jumbo frames are handed to fcs_flat_kernel. Units may be stored out of order with gaps
+    between them. Every frame against the oracle, and the hand-off count against the broken units."""
+    rng = np.random.default_rng(seed)
+    U = len(kinds)
+    lens, rel, broken = [], [], 0
+    for k in kinds:
+        if k == "fixed":
+            ln = np.full(UNIT, int(rng.integers(64, 1537)), dtype=np.int64)
+        elif k == "random":
+            ln = rng.integers(64, 1537, UNIT)
+        elif k == "jumbo":
+            ln = rng.integers(1537, 9019, UNIT)
+        else:
+            ln = _imix(UNIT, int(rng.integers(1 << 30))).astype(np.int64)
+        ln = ln.astype(np.int64)
+        i = int(rng.integers(0, UNIT - 1))
+        if k == "short":
+            ln[i] = int(rng.integers(1, 64))
+        elif k == "long":
+            ln[i] = int(rng.integers(1537, 3000))
+        elif k == "empty":
+            ln[i] = 0
+        o = np.concatenate([[0], np.cumsum(ln)[:-1]]).astype(np.int64)
+        if k == "gap":
+            o[i + 1:] += int(rng.integers(1, 70))
+        elif k == "swap":
+            o[i], o[i + 1] = o[i + 1], o[i]
+            ln[i], ln[i + 1] = ln[i + 1], ln[i]
+        elif k == "overlap":
+            o[i + 1] -= int(rng.integers(1, 16))
+        broken += k in ("short", "long", "empty", "gap", "swap", "overlap", "jumbo")
+        lens.append(ln)
+        rel.append(o)
+    order = rng.permutation(U) if shuffle else np.arange(U)
+    place, pos = {}, base
+    for u in order:
+        place[u] = pos
+        pos += int((rel[u] + lens[u]).max()) + int(rng.integers(0, 40))
+    off = np.concatenate([rel[u] + place[u] for u in range(U)]).astype(np.uint64)
+    ln = np.concatenate(lens).astype(np.uint32)
+    host = rng.integers(0, 256, pos + 64, dtype=np.uint8)
+    listed = _run(dev, oracle, host, off, ln)
+    assert listed == broken, (listed, broken)
