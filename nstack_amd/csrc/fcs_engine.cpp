@@ -115,11 +115,9 @@ struct Pipe {
     hipEvent_t landed[kDepth] = {nullptr, nullptr};
     uint8_t *d_in[kDepth] = {nullptr, nullptr};
     uint8_t *h_in[kDepth] = {nullptr, nullptr};           // pinned staging
-    uint64_t *d_off[kDepth] = {nullptr, nullptr};
-    uint32_t *d_len[kDepth] = {nullptr, nullptr};
+    uint64_t *d_off[kDepth] = {nullptr, nullptr};          // a chunk's n offsets, then its n lengths
     uint32_t *d_out[kDepth] = {nullptr, nullptr};
-    uint64_t *h_off[kDepth] = {nullptr, nullptr};          // pinned
-    uint32_t *h_len[kDepth] = {nullptr, nullptr};          // pinned
+    uint64_t *h_off[kDepth] = {nullptr, nullptr};          // pinned; as d_off (one H2D per chunk)
     uint32_t *h_out[kDepth] = {nullptr, nullptr};          // pinned
     uint64_t cap_bytes = 0, cap_frames = 0;
 };
@@ -530,21 +528,17 @@ int ensure_pipe(DevState *ds, uint64_t bytes, uint64_t frames) {
     if (frames > pp.cap_frames) {
         for (int b = 0; b < Pipe::kDepth; b++) {
             if (pp.d_off[b]) hipFree(pp.d_off[b]);
-            if (pp.d_len[b]) hipFree(pp.d_len[b]);
             if (pp.d_out[b]) hipFree(pp.d_out[b]);
             if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
-            if (pp.h_len[b]) hipHostFree(pp.h_len[b]);
             if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
-            pp.d_off[b] = nullptr; pp.d_len[b] = nullptr; pp.d_out[b] = nullptr;
-            pp.h_off[b] = nullptr; pp.h_len[b] = nullptr; pp.h_out[b] = nullptr;
+            pp.d_off[b] = nullptr; pp.d_out[b] = nullptr;
+            pp.h_off[b] = nullptr; pp.h_out[b] = nullptr;
         }
         pp.cap_frames = 0;
         for (int b = 0; b < Pipe::kDepth; b++) {
-            HIPTRY(hipMalloc(&pp.d_off[b], frames * 8), "hipMalloc(off)");
-            HIPTRY(hipMalloc(&pp.d_len[b], frames * 4), "hipMalloc(len)");
+            HIPTRY(hipMalloc(&pp.d_off[b], frames * 12), "hipMalloc(off, len)");
             HIPTRY(hipMalloc(&pp.d_out[b], frames * 4), "hipMalloc(out)");
-            HIPTRY(hipHostMalloc(&pp.h_off[b], frames * 8, hipHostMallocDefault), "hipHostMalloc(off)");
-            HIPTRY(hipHostMalloc(&pp.h_len[b], frames * 4, hipHostMallocDefault), "hipHostMalloc(len)");
+            HIPTRY(hipHostMalloc(&pp.h_off[b], frames * 12, hipHostMallocDefault), "hipHostMalloc(off, len)");
             HIPTRY(hipHostMalloc(&pp.h_out[b], frames * 4, hipHostMallocDefault), "hipHostMalloc(out)");
         }
         pp.cap_frames = frames;
@@ -664,9 +658,23 @@ int run_host_job(DevState *ds, const HostJob &job) {
     uint64_t i = job.i0;
     int slot = 0;
     uint64_t est = kChunkFramesMax;   // frames per chunk to try first (variable-length batches)
+#ifdef FCS_HOST_TRACE   // measurement-only: where the host thread's time goes, per call
+    using hclk = std::chrono::steady_clock;
+    double tr[5] = {0, 0, 0, 0, 0};   // drain wait, chunk plan, staging, enqueue, final drain
+    const auto tr0 = hclk::now();
+    auto trs = [&](int k, hclk::time_point a) { tr[k] += std::chrono::duration<double, std::milli>(hclk::now() - a).count(); };
+#define FCS_TR(k, a) trs(k, a)
+#define FCS_TR_AT(a) const auto a = hclk::now()
+#else
+#define FCS_TR(k, a)
+#define FCS_TR_AT(a)
+#endif
     while (i < job.i1) {
         const int b = slot % Pipe::kDepth;
+        FCS_TR_AT(ta);
         if ((rc = drain(b))) return rc;
+        FCS_TR(0, ta);
+        FCS_TR_AT(tb);
         // ---- choose the chunk [i, e) and the host byte span it needs ----
         uint64_t e = i, lo = 0, hi = 0, sum = 0;
         if (!job.off) {
@@ -722,7 +730,11 @@ int run_host_job(DevState *ds, const HostJob &job) {
                             (unsigned long long)i, (unsigned long long)job.len[i],
                             (unsigned long long)kChunkBytesHost);
         }
+        FCS_TR(1, tb);
+        FCS_TR_AT(tc);
         const uint64_t n = e - i;
+        uint64_t *ho = pp.h_off[b];
+        uint32_t *hl = reinterpret_cast<uint32_t *>(ho + n);   // lengths right after the offsets
         uint64_t span = hi - lo;
         const bool gather = job.off && (span > kChunkBytesHost || span > 2 * sum);   // sparse: pack frames
         const uint8_t *src = job.arena + lo;
@@ -730,37 +742,44 @@ int run_host_job(DevState *ds, const HostJob &job) {
             uint64_t w = 0;
             for (uint64_t q = 0; q < n; q++) {
                 std::memcpy(pp.h_in[b] + w, job.arena + job.off[i + q], job.len[i + q]);
-                pp.h_off[b][q] = w;
-                pp.h_len[b][q] = job.len[i + q];
+                ho[q] = w;
+                hl[q] = job.len[i + q];
                 w += job.len[i + q];
             }
             span = w;
             src = pp.h_in[b];
         } else {
             if (var) {
-                uint64_t *ho = pp.h_off[b];
+                const uint32_t *lp = job.len + i;
                 if (job.off) {
                     const uint64_t *op = job.off + i;
-                    for (uint64_t q = 0; q < n; q++) ho[q] = op[q] - lo;
+                    for (uint64_t q = 0; q < n; q++) {
+                        ho[q] = op[q] - lo;
+                        hl[q] = lp[q];
+                    }
                 } else {
-                    for (uint64_t q = 0; q < n; q++) ho[q] = (i + q) * job.stride - lo;
+                    for (uint64_t q = 0; q < n; q++) {
+                        ho[q] = (i + q) * job.stride - lo;
+                        hl[q] = lp[q];
+                    }
                 }
-                std::memcpy(pp.h_len[b], job.len + i, n * 4);
             }
             if (!src_pinned) {
                 fcs::staging_copy(pp.h_in[b], src, span);
                 src = pp.h_in[b];
             }
         }
+        FCS_TR(2, tc);
+        FCS_TR_AT(td);
         HIPTRY(hipMemcpyAsync(pp.d_in[b], src, span, hipMemcpyHostToDevice, pp.stream), "H2D frames");
         if (var) {
-            HIPTRY(hipMemcpyAsync(pp.d_off[b], pp.h_off[b], n * 8, hipMemcpyHostToDevice, pp.stream), "H2D off");
-            HIPTRY(hipMemcpyAsync(pp.d_len[b], pp.h_len[b], n * 4, hipMemcpyHostToDevice, pp.stream), "H2D len");
+            HIPTRY(hipMemcpyAsync(pp.d_off[b], ho, n * 12, hipMemcpyHostToDevice, pp.stream), "H2D off, len");
         }
         HIPTRY(hipEventRecord(pp.landed[b], pp.stream), "hipEventRecord");
         HIPTRY(hipStreamWaitEvent(pp.cstream, pp.landed[b], 0), "hipStreamWaitEvent");
         if (var)
-            rc = launch_var(ds, pp.d_in[b], span, pp.d_off[b], pp.d_len[b], pp.d_out[b], n, pp.cstream);
+            rc = launch_var(ds, pp.d_in[b], span, pp.d_off[b], reinterpret_cast<const uint32_t *>(pp.d_off[b] + n),
+                            pp.d_out[b], n, pp.cstream);
         else
             rc = launch_fixed(ds, pp.d_in[b], job.stride, job.flen, n, pp.d_out[b], pp.cstream);
         if (rc) return rc;
@@ -771,9 +790,18 @@ int run_host_job(DevState *ds, const HostJob &job) {
         pend[b].n = n;
         i = e;
         slot++;
+        FCS_TR(3, td);
     }
+    FCS_TR_AT(te);
     for (int b = 0; b < Pipe::kDepth; b++)
         if ((rc = drain(b))) return rc;
+    FCS_TR(4, te);
+#ifdef FCS_HOST_TRACE
+    std::fprintf(stderr, "host_trace var=%d chunks=%d total_ms=%.3f drain_ms=%.3f plan_ms=%.3f stage_ms=%.3f enqueue_ms=%.3f final_ms=%.3f\n",
+                 (int)var, slot, std::chrono::duration<double, std::milli>(hclk::now() - tr0).count(), tr[0], tr[1], tr[2], tr[3], tr[4]);
+#endif
+#undef FCS_TR
+#undef FCS_TR_AT
     return 0;
 }
 
@@ -1076,6 +1104,43 @@ int tx_one(uint8_t *frame, uint32_t len) {
 }
 
 
+// Every frame [off, off + len + tail) inside [0, arena_bytes): -EINVAL naming the first that is not.
+// The host-inclusive calls check the whole batch before anything runs, so nothing is written on an
+// error. The check is branch-free and, from 1 M frames up, split over 8 threads: one thread
+// walking IMIX offsets and lengths took ~4 % of a 4 GiB host-inclusive call (tools/ab_host.py).
+int check_frames(const uint64_t *off, const uint32_t *len, uint64_t n, uint64_t arena_bytes, uint32_t tail,
+                 const char *what) {
+    auto bad_in = [=](uint64_t a, uint64_t z) {
+        uint64_t bad = 0;
+        for (uint64_t i = a; i < z; i++) {
+            const uint64_t o = off[i], l = (uint64_t)len[i] + tail;
+            bad |= (uint64_t)(o > arena_bytes) | (uint64_t)(l > arena_bytes - o);
+        }
+        return bad != 0;
+    };
+    constexpr uint64_t kSplit = 1ull << 20;
+    constexpr int kThreads = 8;
+    bool bad = false;
+    if (n < kSplit) {
+        bad = bad_in(0, n);
+    } else {
+        bool part_bad[kThreads] = {};
+        std::thread th[kThreads - 1];
+        const uint64_t per = (n + kThreads - 1) / kThreads;
+        for (int t = 1; t < kThreads; t++)
+            th[t - 1] = std::thread([&, t] { part_bad[t] = bad_in(std::min(n, per * t), std::min(n, per * (t + 1))); });
+        part_bad[0] = bad_in(0, std::min(n, per));
+        for (auto &x : th) x.join();
+        for (int t = 0; t < kThreads; t++) bad |= part_bad[t];
+    }
+    if (!bad) return 0;
+    for (uint64_t i = 0; i < n; i++)
+        if (off[i] > arena_bytes || (uint64_t)len[i] + tail > arena_bytes - off[i])
+            return fail(EINVAL, "frame %llu [%llu, +%u)%s outside the %llu-byte arena", (unsigned long long)i,
+                        (unsigned long long)off[i], len[i], tail ? " and its FCS" : "", (unsigned long long)arena_bytes);
+    return fail(EINVAL, "%s: frame check", what);   // not reached
+}
+
 std::atomic<uint64_t> g_sharded_calls{0}, g_shard_jobs{0};
 
 // Shard [0, n) over the engine devices (contiguous ranges, byte-balanced when lengths are known:
@@ -1087,7 +1152,7 @@ int run_host_sharded(HostJob job, uint64_t n) {
     if (rc) return rc;
     const uint64_t G = std::min<uint64_t>(devs.size(), std::max<uint64_t>(1, n / 1024));
     std::vector<uint64_t> cut(G + 1, 0);
-    if ((rc = fcs_shard_plan(job.len, n, (uint32_t)G, cut.data()))) return rc;
+    if (G > 1 && (rc = fcs_shard_plan(job.len, n, (uint32_t)G, cut.data()))) return rc;
     if (G == 1) {
         job.i0 = 0;
         job.i1 = n;
@@ -1310,10 +1375,8 @@ static void destroy_state(DevState *ds) {
         if (pp.d_in[b]) hipFree(pp.d_in[b]);
         if (pp.h_in[b]) hipHostFree(pp.h_in[b]);
         if (pp.d_off[b]) hipFree(pp.d_off[b]);
-        if (pp.d_len[b]) hipFree(pp.d_len[b]);
         if (pp.d_out[b]) hipFree(pp.d_out[b]);
         if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
-        if (pp.h_len[b]) hipHostFree(pp.h_len[b]);
         if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
     }
     if (pp.stream) hipStreamDestroy(pp.stream);
@@ -1438,10 +1501,7 @@ int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t
                          const uint32_t *len, uint32_t *out, uint64_t n) {
     if (n == 0) return 0;
     if (!arena || !off || !len || !out) return fail(EINVAL, "null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (off[i] > arena_bytes || len[i] > arena_bytes - off[i])
-            return fail(EINVAL, "frame %llu [%llu, +%u) outside the %llu-byte arena", (unsigned long long)i,
-                        (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
     HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, out, nullptr, 0, n, nullptr, nullptr};
     return run_host_sharded(job, n);
 }
@@ -1480,10 +1540,7 @@ int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *o
                             uint64_t n) {
     if (n == 0) return 0;
     if (!arena || !off || !len) return fail(EINVAL, "null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (off[i] > arena_bytes || (uint64_t)len[i] + 4 > arena_bytes - off[i])
-            return fail(EINVAL, "frame %llu [%llu, +%u) and its FCS outside the %llu-byte arena",
-                        (unsigned long long)i, (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    if (int rc = check_frames(off, len, n, arena_bytes, 4, __func__)) return rc;
     if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)arena + off[0], len[0]);
     if (arena_bytes <= kZeroCopyMaxBytes && (pinned_dev_ptr(arena, arena_bytes) || is_pinned(arena))) {
         std::vector<DevState *> devs;
@@ -1528,10 +1585,7 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
                               uint8_t *ok, uint64_t n) {
     if (n == 0) return 0;
     if (!arena || !off || !len || !ok) return fail(EINVAL, "null pointer");
-    for (uint64_t i = 0; i < n; i++)
-        if (off[i] > arena_bytes || len[i] > arena_bytes - off[i])
-            return fail(EINVAL, "frame %llu [%llu, +%u) outside the %llu-byte arena", (unsigned long long)i,
-                        (unsigned long long)off[i], len[i], (unsigned long long)arena_bytes);
+    if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
     if (arena_bytes <= kZeroCopyMaxBytes) {
         if (const uint8_t *darena = pinned_dev_ptr(arena, arena_bytes)) {   // the RX queue's arena
             std::vector<DevState *> devs;
