@@ -105,20 +105,23 @@ inline bool injected_fault() { return false; }
 inline bool injected_timeout() { return false; }
 #endif
 
-// Double-buffered host pipeline resources of one device.
+// Host pipeline resources of one device: kDepth chunks in flight (double-buffered by default).
+#ifndef FCS_PIPE_DEPTH   // measurement-only override (chunks in flight per device)
+#define FCS_PIPE_DEPTH 2
+#endif
 struct Pipe {
-    static constexpr int kDepth = 2;
+    static constexpr int kDepth = FCS_PIPE_DEPTH;
     hipStream_t stream = nullptr;     // copies to the device, chunk after chunk at the full PCIe rate
     hipStream_t cstream = nullptr;    // each chunk's kernel and its D2H, once its H2D has landed, so they
                                       // overlap the next chunk's H2D (two H2D streams halved the rate)
-    hipEvent_t done[kDepth] = {nullptr, nullptr};
-    hipEvent_t landed[kDepth] = {nullptr, nullptr};
-    uint8_t *d_in[kDepth] = {nullptr, nullptr};
-    uint8_t *h_in[kDepth] = {nullptr, nullptr};           // pinned staging
-    uint64_t *d_off[kDepth] = {nullptr, nullptr};          // a chunk's n offsets, then its n lengths
-    uint32_t *d_out[kDepth] = {nullptr, nullptr};
-    uint64_t *h_off[kDepth] = {nullptr, nullptr};          // pinned; as d_off (one H2D per chunk)
-    uint32_t *h_out[kDepth] = {nullptr, nullptr};          // pinned
+    hipEvent_t done[kDepth] = {};
+    hipEvent_t landed[kDepth] = {};
+    uint8_t *d_in[kDepth] = {};
+    uint8_t *h_in[kDepth] = {};     // pinned staging
+    uint64_t *d_off[kDepth] = {};   // a chunk's n offsets, then its n lengths
+    uint32_t *d_out[kDepth] = {};
+    uint64_t *h_off[kDepth] = {};   // pinned; as d_off (one H2D per chunk)
+    uint32_t *h_out[kDepth] = {};   // pinned
     uint64_t cap_bytes = 0, cap_frames = 0;
 };
 

@@ -41,7 +41,7 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_ST_ABL_NOCLOSE -DFCS_ST_ABL_NOSHIFT -DFCS_ST_NOSKEW"),
     ("fcs_engine.cpp", "-DFCS_FAULT_HOOK -DFCS_GRID_CUS=128 -DFCS_FLAT_DYN_MIN=1000 -DFCS_FIXED_DYN_MIN=8 "
                        "-DFCS_FIXED_FLAT_MAX=0 -DFCS_ZC_MAX_MB=16 -DFCS_NO_STREAM"),
-    ("fcs_engine.cpp", "-DFCS_STAMPS -DFCS_HOST_TRACE"),
+    ("fcs_engine.cpp", "-DFCS_STAMPS -DFCS_HOST_TRACE -DFCS_PIPE_DEPTH=3"),
     ("fcs_txq.cpp", "-DFCS_TXQ_TSAN"),
     ("inet_kernel.hip", "-DFCS_NT"),
 ]
