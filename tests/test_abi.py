@@ -139,3 +139,43 @@ def test_inet_fails_loudly_without_gpu():
     p = subprocess.run(["python", "-c", "import nstack_amd as na; na.ip_checksum(bytes(20))"],
                        capture_output=True, text=True, cwd=ROOT, timeout=120)
     assert p.returncode != 0 and "no usable GPU engine" in p.stderr
+
+
+@pytest.mark.parametrize("n", [1000, (1 << 20) + 777])   # one thread / the 8-thread split
+def test_host_batch_bounds_checked_before_any_work(n):
+    """The host-inclusive entry points check every frame against the arena before anything runs
+    (nothing written on an error): -EINVAL naming the first bad frame, wherever it sits, for the
+    single-threaded check and the 8-thread one (from 1 M frames). Without a GPU, a clean batch
+    gets past the check and fails with -ENODEV instead."""
+    import numpy as np
+    lib = na.load()
+    lib.fcs_last_error.restype = ctypes.c_char_p
+    ab = 64 * n
+    off = np.arange(n, dtype=np.uint64) * 64
+    ln = np.full(n, 60, dtype=np.uint32)
+    out = np.zeros(n, dtype=np.uint32)
+    ok = np.zeros(n, dtype=np.uint8)
+    base = ctypes.c_void_p(4096)   # never dereferenced: the check reads only off and len
+
+    def call(kind):
+        if kind == "batch":
+            return lib.ether_fcs_batch_host(base, ab, off.ctypes.data, ln.ctypes.data, out.ctypes.data, n)
+        if kind == "verify":
+            return lib.ether_fcs_verify_host(base, ab, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, n)
+        return lib.ether_fcs_tx_batch_host(base, ab, off.ctypes.data, ln.ctypes.data, n)
+
+    for kind in ("batch", "verify", "tx"):
+        for bad in (0, n // 2, n - 1, (7 * n) // 8 + 1):
+            saved = (int(off[bad]), int(ln[bad]))
+            for o, L in ((ab + 1, 0), (ab - 10, 11), (2**64 - 8, 16), (64 * bad, 2**32 - 1)):
+                off[bad], ln[bad] = o, L
+                assert call(kind) == -22, (kind, bad, o, L)
+                assert f"frame {bad} " in lib.fcs_last_error().decode()
+            off[bad], ln[bad] = saved
+        if kind == "tx":   # its FCS must fit too: 61 + 4 > 64 at the arena's end
+            ln[n - 1] = 61
+            assert call(kind) == -22 and f"frame {n - 1} " in lib.fcs_last_error().decode()
+            ln[n - 1] = 60
+        if not _gpu_visible():
+            assert call(kind) == -19   # clean batch: past the check, no GPU
+    assert not out.any() and not ok.any()
