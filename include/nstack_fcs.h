@@ -89,7 +89,9 @@ int ether_fcs_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_
                         uint32_t *out, void *stream);
 
 /* ---- host batches (host memory in and out; sharded over the engine's GPUs,
- *      chunked H2D -> kernel -> D2H pipeline per GPU; synchronous) ---- */
+ *      chunked H2D -> kernel -> D2H pipeline per GPU; synchronous) ----
+ * The arena forms check every frame (and, in TX mode, its FCS bytes) against the arena before
+ * any work: on -EINVAL, which names the first bad frame, nothing has been written. */
 int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
                          const uint32_t *len, uint32_t *out, uint64_t n);
 int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64_t n,
