@@ -363,7 +363,7 @@ struct Lane {
     int j;            // lane within the frame's 16
     uint32_t base0, base1, lanebase;
     uint64_t Q;       // frame slots in the grid
-    Dispenser *D;     // fixed frames of any segment count: wave units of 4 frames (else null)
+    Dispenser *D;     // fixed frames (kUnits): wave units of 4 frames; otherwise unused
     uint32_t q;       // quarter of the wave (frame 4u + q of unit u)
 
     struct Pos {
@@ -374,9 +374,11 @@ struct Lane {
         Item it;
     };
 
+    static constexpr bool kUnits = !VAR && !SINGLE && !TINY;
+
     __device__ __forceinline__ Pos next(const Pos &c) const {
         Pos n = c;
-        if (!VAR && !SINGLE && D != nullptr) {
+        if (kUnits) {
             // every frame has p.fseg segments: the quarters wrap together, the unit step is uniform
             n.k = c.k + 1;
             if (n.k >= p.fseg) {
@@ -528,11 +530,13 @@ __device__ __forceinline__ void fcs_body(const KParams &p, const uint8_t *lds, u
     table_bases(lane, tb0, tb1);
     // Fixed frames: a wave's unit is 4 consecutive frames (one per quarter), units from the
     // dispenser (interleaved over the grid's waves, the tail dynamic when the host gave a counter).
-    constexpr bool kUnits = !VAR && !SINGLE && !TINY;
+    // L.D always points at D (the unit path is chosen at compile time): a pointer that could be null
+    // made the compiler keep D's 120 bytes in scratch memory, loaded and stored at every unit step.
+    constexpr bool kUnits = Lane<VAR, TINY, SINGLE>::kUnits;
     Dispenser D(kUnits ? p.ctr : nullptr, (p.n + 3) >> 2, (uint64_t)nblk * (NT / 64),
                 (uint64_t)blk * (NT / 64) + (threadIdx.x >> 6), lane, FCS_FIXED_DYN_PCT, 1, FCS_FIXED_CHUNK_MAX);
     Lane<VAR, TINY, SINGLE> L{p, lds, j, tb0, tb1, kLdsLane | r4, (uint64_t)nblk * kSlotsPerWg<NT>,
-                              kUnits ? &D : nullptr, (uint32_t)(threadIdx.x >> 4) & 3u};
+                              &D, (uint32_t)(threadIdx.x >> 4) & 3u};
 
     typename Lane<VAR, TINY, SINGLE>::Pos A, B;
     if (kUnits) {
