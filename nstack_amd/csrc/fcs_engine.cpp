@@ -427,7 +427,13 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         return 0;
     }
     const int grid = grid_for(ds, n, fcs::fixed_threads(p));
-    if (fcs::fixed_dma(p)) {   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
+    if (!fcs::fixed_tiny(p) && fcs::fixed_wide(p)) {   // wide LDS-DMA kernel: 128-B windows, 8 KiB slots
+        const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kWideWgThreads / 64);
+        if (items >= fcs::kDmaDynMinItemsPerWave * waves) {
+            const int rc = take_counter(ds, st, p, lease);
+            if (rc) return rc;
+        }
+    } else if (fcs::fixed_dma(p)) {   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
         p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
         const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
         if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic schedule

@@ -167,7 +167,27 @@ inline bool fixed_segil(const KParams &p) {
     return p.flen >= kSegilMinLen2;
 #endif
 }
+// Wide LDS-DMA kernel (fcs_wide_kernel): one-item frames of kWideMinLen..kWideCover bytes (128-B
+// lane windows, 12 waves, 8 KiB slots) whose four consecutive frames fit one slot, as fixed_dma().
+// Against the kernels these lengths took before (tools/ab.py, one process): 1537 B
+// +22 %, 1600-1949 B +24 to +27 % (generic kernel, two segments), 1950-1988 B +23 to +26 %
+// (segment kernel); 1525-1536 B -8 % against the single-segment kernel, which keeps them.
+#ifndef FCS_WIDE_MIN   // measurement-only override of the band's lower end
+#define FCS_WIDE_MIN 1537
+#endif
+constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
+constexpr int kWideWgThreads = 768;
+inline bool fixed_wide(const KParams &p) {
+#ifdef FCS_NO_WIDE   // measurement-only build
+    (void)p;
+    return false;
+#else
+    return p.flen >= kWideMinLen && p.flen <= kWideCover && p.stride <= 4096 &&
+           3 * p.stride + p.flen <= kWideItemBytes - 18 && p.hi4 - p.lo4 >= 2 * kWideItemBytes;
+#endif
+}
 inline int fixed_threads(const KParams &p) {
+    if (!fixed_tiny(p) && fixed_wide(p)) return kWideWgThreads;
     if (fixed_segil(p)) return kSegilWgThreads;
     if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;
     return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;

@@ -21,6 +21,7 @@
 //   chunk shifts  C_c = A_{96 c}         c = 0..15   (flat variable-length kernel: a lane's
 //                                                     chunk index is data-dependent, so the
 //                                                     table is indexed by c, not by lane)
+//   (and the LDS-DMA, arena-stream and wide kernels' tables, listed at their blob offsets below)
 // These are constants of the algorithm, computed once per process; no frame bytes are ever
 // checksummed on the host (the product has no CPU CRC path).
 #pragma once
@@ -78,6 +79,15 @@ __host__ __device__ constexpr bool dma_short_lane(int c) { return (c & 3) == 3 &
 constexpr uint32_t kDmaCover = dma_end_off(15) + kChunkBytes;   // 1524
 constexpr uint32_t kDmaMinLen = 1496;                            // front lane masks <= 28 B
 constexpr uint32_t kDmaItemBytes = 6144;                         // one wave's LDS slot: 6 x 1 KiB DMA
+// Wide LDS-DMA kernel (fcs_wide_kernel, fixed lengths just over kDmaCover): 128-byte lane windows
+// ending e_c = 124 c before the frame end. Each window's first word is its neighbour's last (masked
+// in every lane but the frame's front lane), and the 16 windows start on 16 distinct banks
+// ((e_c / 4) mod 32 = -c mod 32). 16 lanes cover e_15 + 128 = 1988 bytes; four frames per 8 KiB slot.
+constexpr uint32_t kWideWin = 128;
+constexpr uint32_t kWideWords = kWideWin / 4;                    // 32
+__host__ __device__ constexpr uint32_t wide_end_off(int c) { return 124u * (uint32_t)c; }
+constexpr uint32_t kWideCover = wide_end_off(15) + kWideWin;     // 1988
+constexpr uint32_t kWideItemBytes = 8192;
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
@@ -96,7 +106,10 @@ constexpr uint32_t kBlobMerge = kBlobLaneDma + 8 * 16 * 32;     // uint32 [11][8
 constexpr int kStChunkTabs = 24, kStWordTabs = 17, kStInvTabs = 4;
 constexpr uint32_t kBlobStream = kBlobMerge + 11 * 8 * 16;
 constexpr uint32_t kBlobStreamK1 = kBlobStream + (kStChunkTabs + kStWordTabs + kStInvTabs) * 128;
-constexpr uint32_t kBlobWords = kBlobStreamK1 + 64;
+// Wide LDS-DMA kernel: lane tables A_{124 c} in the LDS-DMA layout [8][16][32], INV[z] for z < 128.
+constexpr uint32_t kBlobLaneWide = kBlobStreamK1 + 64;
+constexpr uint32_t kBlobInvWide = kBlobLaneWide + 8 * 16 * 32;
+constexpr uint32_t kBlobWords = kBlobInvWide + kWideWin;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -188,6 +201,12 @@ struct Tables {
         for (int i = 0; i < kStWordTabs; i++) put(4L * i);
         for (int d = 1; d <= kStInvTabs; d++) put(-(long)d);
         for (int sg = 0; sg < 64; sg++) b[kBlobStreamK1 + sg] = shift(0xFFFFFFFFu, 64 - sg);
+        for (int slot = 0; slot < 32; slot++) {   // wide kernel
+            nibble_table((long)wide_end_off(slot % kGroup), nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobLaneWide + (t * 16 + e) * 32 + slot] = nt[t][e];
+        }
+        for (int z = 0; z < (int)kWideWin; z++) b[kBlobInvWide + z] = shift(0xFFFFFFFFu, -(long)z);
         return b;
     }
     // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.

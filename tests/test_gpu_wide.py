@@ -1,0 +1,119 @@
+"""GPU parity of the wide LDS-DMA kernel (fcs_wide_kernel).
+
+Fixed-length frames of 1537..1988 B whose four consecutive frames fit an 8 KiB slot (3 stride + len
+<= 8174, arena >= 16 KiB: fixed_wide(), fcs_launch.hpp) take this kernel: 16 lane windows of 128 B
+ending 124 c before the frame end, every live lane but the front one masking its first word, the
+front lane cf = (len - 1) / 124 masking zc = 124 cf + 128 - len leading bytes and starting from
+INV[zc], the lanes past it dropped. Every case is checked bit-exact against the oracle (the CPU
+restatement of src/ether_fcs.c:4-19): every front-lane boundary (124 c + 1 and 124 c + 4 for each
+cf, zc = 127 and 124 .. 0), the band's ends and the lengths just outside it, strides from no gap to
+the largest the slot takes, all base alignments, partial items, the arena-end slot clamp, batches
+large enough for the dynamic schedule, verify mode, and a fuzz over the band.
+"""
+import struct
+import zlib
+
+import numpy as np
+import pytest
+
+import nstack_amd as na
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    torch.cuda.set_device(0)
+    na.load()
+    return torch.device("cuda:0")
+
+
+def oracle_fixed(oracle, host: np.ndarray, stride, L, n):
+    out = np.empty(n, dtype=np.uint32)
+    oracle.oracle_fcs_fixed(host.ctypes.data, stride, L, n, out.ctypes.data, 1, 16)
+    return out
+
+
+def run(dev, d, lead, stride, L, n):
+    out = torch.empty(n, dtype=torch.int32, device=dev)
+    na.fixed_dev(d.data_ptr() + lead, stride, L, n, out)
+    torch.cuda.synchronize()
+    return out.cpu().numpy().view(np.uint32)
+
+
+# the band's ends and one byte outside; each front lane's first and last lengths (cf = 12 .. 15:
+# lengths 124 cf + 1 .. 124 cf + 124, zc = 127 .. 4); the QinQ / baby-giant sizes
+LENS = sorted({1524, 1525, 1526, 1530, 1536, 1537, 1548, 1549, 1552, 1600, 1611, 1672, 1673, 1676, 1700, 1796,
+               1797, 1800, 1860, 1861, 1864, 1900, 1920, 1949, 1950, 1984, 1985, 1987, 1988, 1989, 2000})
+
+
+@pytest.mark.parametrize("L", LENS)
+def test_wide_lengths(dev, oracle, L):
+    for gap in (0, 1, 3, 8, (8174 - L) // 3 - L):   # the last: the largest stride a slot takes
+        stride = L + gap
+        for n in (1, 3, 11, 13, 257):
+            host = np.random.default_rng(L * 7 + gap * 3 + n).integers(0, 256, n * stride + 16, dtype=np.uint8)
+            d = torch.from_numpy(host).to(dev)
+            for lead in (0, 1, 2, 3):
+                got = run(dev, d, lead, stride, L, n)
+                exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+                assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
+
+
+@pytest.mark.parametrize("L,stride", [(1525, 1525), (1526, 1536), (1600, 1600), (1600, 1664), (1788, 2000),
+                                      (1949, 1949), (1988, 1988), (1988, 2062)])
+def test_wide_many_items(dev, oracle, L, stride):
+    """More items than the grid's waves (the dynamic schedule) and a second launch reusing the
+    counter ring; the last items' slots clamped at the arena end."""
+    n = (300 << 20) // stride + 3
+    host = np.random.default_rng(L + stride).integers(0, 256, n * stride + 8, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    exp = oracle_fixed(oracle, host[1:], stride, L, n)
+    for _ in range(2):
+        got = run(dev, d, 1, stride, L, n)
+        assert np.array_equal(got, exp), int(np.argmax(got != exp))
+
+
+@pytest.mark.parametrize("L", [1525, 1530, 1600, 1796, 1922, 1988])
+def test_wide_verify_mode(dev, L):
+    """RX residue check through the wide kernel: frames of L bytes carrying their FCS, a few
+    corrupted; ok[] and the bad count against zlib."""
+    n = 4099
+    rng = np.random.default_rng(L)
+    host = rng.integers(0, 256, n * L, dtype=np.uint8)
+    for i in range(n):
+        f = host[i * L:i * L + L - 4].tobytes()
+        host[i * L + L - 4:i * L + L] = np.frombuffer(struct.pack("<I", zlib.crc32(f)), dtype=np.uint8)
+    bad_idx = sorted(set(int(x) for x in rng.integers(0, n, 23)) | {0, n - 1})
+    for i in bad_idx:
+        host[i * L + int(rng.integers(0, L))] ^= np.uint8(1 << int(rng.integers(0, 8)))
+    d = torch.from_numpy(host).to(dev)
+    ok = torch.empty(n, dtype=torch.uint8, device=dev)
+    bad = torch.zeros(1, dtype=torch.int64, device=dev)
+    na.verify_fixed_dev(d, L, L, n, ok, bad)
+    torch.cuda.synchronize()
+    exp = np.ones(n, dtype=np.uint8)
+    exp[bad_idx] = 0
+    assert np.array_equal(ok.cpu().numpy(), exp)
+    assert int(bad.item()) == len(bad_idx)
+
+
+hyp = pytest.importorskip("hypothesis")
+from hypothesis import given, settings, strategies as hst  # noqa: E402
+
+
+@settings(max_examples=40, deadline=None, derandomize=True)
+@given(hst.integers(1520, 1995), hst.integers(0, 200), hst.integers(1, 2000), hst.integers(0, 15))
+def test_wide_fuzz(dev, oracle, L, gap, n, lead):
+    """Random lengths across the band and just outside it, gaps, frame counts and base alignments
+    against the oracle (the wide kernel where its slot takes the item, the others elsewhere)."""
+    stride = L + gap
+    host = np.random.default_rng(L ^ (gap << 17) ^ (n << 33) ^ lead).integers(0, 256, n * stride + 32, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    got = run(dev, d, lead, stride, L, n)
+    exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+    assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))

@@ -171,3 +171,38 @@ def test_segil_decomposition_model(lds_dma, L):
     frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
     garbage = rng.integers(0, 256, 1524, dtype=np.uint8).tobytes()
     assert km.model_segil_frame(lds_dma[2], frame, garbage) == zlib.crc32(frame)
+
+
+@pytest.fixture(scope="module")
+def lds_wide():
+    return km.build_lds_wide(na.tables_blob())
+
+
+@pytest.mark.parametrize("flen,extra", [(1525, 0), (1530, 3), (1536, 0), (1537, 1), (1600, 0), (1611, 16), (1736, 0),
+                                        (1737, 5), (1860, 0), (1861, 2), (1949, 0), (1950, 100), (1987, 0), (1988, 0),
+                                        (1988, 74)])   # 3 stride + len = 8174: the largest item a slot takes
+def test_wide_kernel_model(lds_wide, flen, extra):
+    """fcs_wide_kernel's decomposition (128-B windows ending 124 c before the frame end, every
+    live lane but the front one masking its first word, the front lane cf = (len - 1) / 124 masking
+    its zc leading bytes and starting from INV[zc], lanes past it dropped, two 16-word chains merged
+    with A_64, lane shift A_{124 c}, 8 KiB slots clamped at the arena end) replayed on the CPU for
+    every item of small batches at all four base alignments, against zlib."""
+    stride = flen + extra
+    rng = random.Random(flen * 37 + extra)
+    garbage = bytes(rng.randrange(256) for _ in range(2048 + 64))
+    for b0 in (0, 1, 2, 3):
+        n = 11
+        mem = bytes(rng.randrange(256) for _ in range(b0 + n * stride + 64))
+        for f in range(0, n, 4):
+            got = km.model_wide_item(lds_wide, mem, b0, stride, flen, n, f, garbage)
+            for g in range(4):
+                if f + g < n:
+                    S = b0 + (f + g) * stride
+                    assert got[g] == zlib.crc32(mem[S:S + flen]), (flen, extra, b0, f + g)
+
+
+def test_wide_windows_bank_distinct():
+    """The 16 windows of a frame in fcs_wide_kernel start on 16 distinct dword banks (mod 32)."""
+    for E in range(0, 64, 4):
+        banks = {((E - km.wide_end_off(c) - km.WIDE_WIN) // 4) % 32 for c in range(16)}
+        assert len(banks) == 16

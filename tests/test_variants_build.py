@@ -30,6 +30,8 @@ VARIANTS = [
                        "-DFCS_DMA_ABL_NOLDS"),
     ("fcs_kernel.hip", "-DFCS_NO_SEGIL -DFCS_SEGIL_TAIL_AUX=2 -DFCS_SEGIL_SKEW=0"),
     ("fcs_kernel.hip", "-DFCS_SEGIL_NOCRC -DFCS_SEGIL_ANY"),
+    ("fcs_kernel.hip", "-DFCS_NO_WIDE"),
+    ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1525"),
     ("fcs_engine.cpp", "-DFCS_SEGIL_ANY"),
     ("fcs_kernel.hip", "-DFCS_BLOCKED"),
     ("fcs_kernel.hip", "-DFCS_XCD -DFCS_NO_WAVE_SYNC"),
