@@ -1377,8 +1377,10 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     const int zb = fdead ? 0 : zf;   // the wave masks word groups up to its largest live claim
 
     const uint64_t n = p.n, units = (n + 3) >> 2;
-    // chunks of about 64 items, and at least 16 units so that result runs fill 256-B groups
-    const uint32_t cmax = m >= 4 ? 16u : 64u / m;
+    // chunks of about 64 items, and at least 16 units so that result runs fill 256-B groups; jumbo
+    // frames (m >= 4) up to 32 units: each chunk is one device-scope atomic on the work counter, and
+    // at 16 units those were 13 % on top of the CRC bytes in WRITE_SIZE
+    const uint32_t cmax = m >= 4 ? 32u : 64u / m;
     Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kSegilWaves, (uint64_t)blockIdx.x * kSegilWaves + (uint64_t)wave,
                 lane, 100, 1, cmax);
     D.align = 16;
