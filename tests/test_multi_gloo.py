@@ -108,7 +108,7 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 4])
 def test_two_rank_sharding_matches_single_pass(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -127,8 +127,8 @@ def test_two_rank_sharding_matches_single_pass(world):
     gathered = np.concatenate([np.array(s[2], dtype=np.uint32) for s in sizes])
     assert np.array_equal(gathered, _crcs(_oracle(), 0, TOTAL))
     assert tmax == 0.5 + (world - 1)
-    value, t = bench.aggregate([(s[1] - s[0]) * L for s in sizes], [0.5, 1.5])
-    assert t == 1.5 and value == TOTAL * L / 1.5
+    value, t = bench.aggregate([(s[1] - s[0]) * L for s in sizes], [0.5 + r for r in range(world)])
+    assert t == 0.5 + (world - 1) and value == TOTAL * L / t
 
 
 def test_two_rank_imix_byte_balanced_shards_match_single_pass():
@@ -158,11 +158,11 @@ def test_shard_ranges_cover_eight_gpus():
     assert all(hi - lo == 64 << 20 for lo, hi in r)
 
 
-def test_two_rank_imix_bench_path_shards_match_single_pass():
+@pytest.mark.parametrize("world", [2, 4])
+def test_two_rank_imix_bench_path_shards_match_single_pass(world):
     """bench.py's N > 1 IMIX config (imix_shard): the global stream is `world` blocks of IMIX frames;
     the ranks' fcs_shard_plan ranges partition it, each rank's bytes start at its global byte
-    position, and the gathered CRCs equal one pass over the whole stream."""
-    world = 2
+    position, and the gathered CRCs equal one pass over the whole stream (2 and 4 ranks)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -174,8 +174,11 @@ def test_two_rank_imix_bench_path_shards_match_single_pass():
         p.join(timeout=60)
         assert p.exitcode == 0
     glob = np.tile(bench.imix_lengths(IMIX_BLK), world)
-    assert sizes[0][0] == 0 and sizes[-1][1] == len(glob) and sizes[0][1] == sizes[1][0]
-    assert sizes[0][3] == 0 and sizes[1][3] == int(glob[:sizes[1][0]].sum())   # global byte positions
-    assert sizes[0][4] + sizes[1][4] == int(glob.sum())
+    assert sizes[0][0] == 0 and sizes[-1][1] == len(glob)
+    for a, b in zip(sizes, sizes[1:]):
+        assert a[1] == b[0]
+    for s in sizes:   # each rank's bytes start at its global byte position
+        assert s[3] == int(glob[:s[0]].sum())
+    assert sum(s[4] for s in sizes) == int(glob.sum())
     gathered = np.concatenate([np.array(s[2], dtype=np.uint32) for s in sizes])
     assert np.array_equal(gathered, _crcs_var(_oracle(), glob, 0, len(glob)))
