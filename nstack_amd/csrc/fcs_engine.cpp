@@ -428,7 +428,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     }
     const int grid = grid_for(ds, n, fcs::fixed_threads(p));
     if (!fcs::fixed_tiny(p) && fcs::fixed_wide(p)) {   // wide LDS-DMA kernel: 128-B windows, 8 KiB slots
-        const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kWideWgThreads / 64);
+        const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);
         if (items >= fcs::kDmaDynMinItemsPerWave * waves) {
             const int rc = take_counter(ds, st, p, lease);
             if (rc) return rc;
@@ -1428,7 +1428,7 @@ const char *fcs_last_error(void) { return g_last_error.c_str(); }
 const char *fcs_engine_version(void) {
     return "nstack-fcs 0.6 gfx950: quarter-wave/frame, 96B lane windows as 2 slice-by-4 chains, v_perm "
            "addressing, DPP reduce; 1496-1524B: LDS-DMA (nt global_load_lds) 6KiB slot/wave, 16 waves/CU, "
-           "32KiB 8-replica tables, guided dynamic items; 1537-1988B: 128B-window LDS-DMA, 8KiB slots; "
+           "32KiB 8-replica tables, guided dynamic items; 1537-1604B / -1988B: 104B / 128B-window LDS-DMA, 7 / 8KiB slots; "
            ">1524B otherwise: frame-interleaved LDS-DMA segments; var: "
            "packed 64-1536B units as an arena stream (4KiB LDS-DMA items, taps at frame boundaries, XOR "
            "scan), other units as a flat chunk stream per 64-frame window";

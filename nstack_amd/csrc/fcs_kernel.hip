@@ -1128,50 +1128,61 @@ __global__ __launch_bounds__(kDmaWgThreads, 1) void fcs_dma_kernel(KParams p) {
 
 
 // ---------------------------------------------------------------------------------------------
-// Fixed length just over the LDS-DMA kernel's cover (fcs_wide_kernel; host-selected by
-// fixed_wide(): kWideMinLen..kWideCover bytes, four consecutive frames per 8 KiB slot).
-// fcs_dma_kernel with 128-byte lane windows: lane c of a frame's 16 reads [E - 124 c - 128,
-// E - 124 c) (E = frame end), 33 dwords from the slot, realigned. A window's first word is the
-// next lane's last, so every live lane masks it, except the front lane cf = (len - 1) / 124 (the
-// last whose window reaches into the frame), which masks its zc = 124 cf + 128 - len leading bytes
-// and starts its chain from INV[zc]; lanes past cf are dropped. cf and zc are launch constants (the
-// length is fixed), so the masks are scalars. Two 16-word chains merged with A_64, lane shift
-// A_{124 c}, row XOR, the LDS-DMA kernel's 256-B result runs. The generic register-load kernel
-// spends two 1536-B segments on a 1600-B frame; this one covers up to 1988 B in one item.
-// LDS (160 KiB): the 64 KiB table image (slice tables; holes 0..127 the lane tables A_{124 c},
-// 128..131 the merge A_64, 132..135 INV[0..127], then the verify counters) and 12 slots of 8 KiB.
+// Fixed length just over the LDS-DMA kernel's cover (fcs_wide_kernel<WD>; host-selected by
+// wide_wd(): kWideMinLen..kWideCover bytes, four consecutive frames per slot).
+// fcs_dma_kernel with wider lane windows of WD dwords (WD = 32: 128 B, 8 KiB slots, 12 waves, up to
+// 1988 B; WD = 26: 104 B, 7 KiB slots, 13 waves, up to 1604 B). Lane c of a frame's 16 reads
+// [E - s c - 4 WD, E - s c) with s = 4 WD - 4 (E = frame end), WD + 1 dwords from the slot,
+// realigned. A window's first word is the next lane's last, so every live lane masks it, except the
+// front lane cf = (len - 1) / s (the last whose window reaches into the frame), which masks its
+// zc = s cf + 4 WD - len leading bytes and starts its chain from INV[zc]; lanes past cf are dropped.
+// cf and zc are launch constants (the length is fixed), so the masks are scalars. Two chains
+// (16 + 16 or 12 + 14 words) merged with A_{4 (WD - CL0)}, lane shift A_{s c}, row XOR, the LDS-DMA
+// kernel's 256-B result runs. The generic register-load kernel spends two 1536-B segments on a
+// 1600-B frame; this one covers it in one item.
+// LDS: the 64 KiB table image (slice tables; holes 0..127 the lane tables A_{s c}, 128..131 the
+// merge, 132..135 INV[0..127], then the verify counters) and the slots.
 // CPU model: tests/kernel_model.py model_wide_item.
 // ---------------------------------------------------------------------------------------------
-constexpr int kWideWaves = kWideWgThreads / 64;
 constexpr uint32_t kWideMergeHole = 128, kWideInvHole = 132;
 constexpr uint32_t kWideBad = dma_hole(kWideInvHole + 4);
-constexpr uint32_t kWideLdsBytes = kDmaRing + (uint32_t)kWideWaves * kWideItemBytes;
-static_assert(kWideLdsBytes <= 163840, "LDS per CU");
+__host__ __device__ constexpr uint32_t wide_lds_bytes(int wd) {
+    return kDmaRing + (uint32_t)(wide_threads(wd) / 64) * wide_slot(wd);
+}
+static_assert(wide_lds_bytes(32) <= 163840 && wide_lds_bytes(26) <= 163840, "LDS per CU");
 static_assert(kDmaMergeHole == kWideMergeHole, "merge_shift_dma reads merge table 0 at the same holes");
+// chain split: chain 0 = words [0, CL0), chain 1 = [CL0, WD); chain 1 spans 4 (WD - CL0) bytes, a
+// multiple of 8 so that its merge A_{4 (WD - CL0)} is one of the blob's A_{8 k}
+__host__ __device__ constexpr int wide_cl0(int wd) { return wd == 32 ? 16 : 12; }
 
+template <int WD>
 __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds, int tid) {
-    for (int i = tid; i < 2048; i += kWideWgThreads) {   // slice tables as fcs_dma_kernel
+    constexpr int NT = wide_threads(WD);
+    constexpr uint32_t kLane = WD == 32 ? kBlobLaneWide : kBlobLaneWide26;
+    constexpr int kMergeK = 2 * (WD - wide_cl0(WD)) / 4;   // A_{8 k} with 8 k = 4 (WD - CL0)
+    for (int i = tid; i < 2048; i += NT) {   // slice tables as fcs_dma_kernel
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
         *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
     }
-    for (int i = tid; i < 4096; i += kWideWgThreads)   // lane tables [t][n][slot]: hole 16 t + n
-        *reinterpret_cast<uint32_t *>(lds + dma_hole((uint32_t)i >> 5) + (uint32_t)(i & 31) * 4u) = p.blob[kBlobLaneWide + i];
-    for (int i = tid; i < 128; i += kWideWgThreads) {   // A_64 = merge blob table k = 8
+    for (int i = tid; i < 4096; i += NT)   // lane tables [t][n][slot]: hole 16 t + n
+        *reinterpret_cast<uint32_t *>(lds + dma_hole((uint32_t)i >> 5) + (uint32_t)(i & 31) * 4u) = p.blob[kLane + i];
+    for (int i = tid; i < 128; i += NT) {   // the chain merge
         const int t = (i >> 4) & 7, e = i & 15;
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kWideMergeHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
-                                      4u * (uint32_t)e) = p.blob[kBlobMerge + 7 * 128 + i];
+                                      4u * (uint32_t)e) = p.blob[kBlobMerge + (kMergeK - 1) * 128 + i];
     }
-    for (int i = tid; i < (int)kWideWin; i += kWideWgThreads)
+    for (int i = tid; i < (int)kWideWin; i += NT)
         *reinterpret_cast<uint32_t *>(lds + dma_hole(kWideInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
             p.blob[kBlobInvWide + i];
 }
 
-// The slot DMA: eight 1 KiB rows from two address registers, each only as far as the item's bytes
-// reach; the first and eighth rows at the default cache policy, the middle ones non-temporal.
+// The slot DMA: seven or eight 1 KiB rows from two address registers, each only as far as the
+// item's bytes reach; the first and last rows at the default cache policy, the middle ones
+// non-temporal.
+template <int WD>
 __device__ __forceinline__ void wide_dma_item(const uint8_t *slot, uint64_t src, int lane, uint32_t need) {
     typedef __attribute__((address_space(3))) void lds_void;
-    static_assert(kWideItemBytes == 8 * 1024, "eight rows");
     const uint64_t a = src + 16 * (uint64_t)lane, b = a + 4096;
     lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
     const uint32_t o = 16u * (uint32_t)lane;
@@ -1181,14 +1192,23 @@ __device__ __forceinline__ void wide_dma_item(const uint8_t *slot, uint64_t src,
     if (3072u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
     if (4096u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
     if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
-    if (6144u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 2048, FCS_DMA_AUX);
-    if (7168u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 3072, FCS_DMA_EDGE_AUX);
+    if constexpr (WD == 32) {
+        if (6144u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 2048, FCS_DMA_AUX);
+        if (7168u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 3072, FCS_DMA_EDGE_AUX);
+    } else {
+        static_assert(wide_slot(WD) == 7 * 1024, "seven rows");
+        if (6144u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 2048, FCS_DMA_EDGE_AUX);
+    }
 }
 
-__global__ __launch_bounds__(kWideWgThreads, 1) void fcs_wide_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kWideLdsBytes];
+template <int WD>
+__global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p) {
+    constexpr uint32_t kWin = wide_win(WD), kStep = wide_step(WD), kSlot = wide_slot(WD);
+    constexpr uint32_t kLdsB = wide_lds_bytes(WD);
+    constexpr int kWaves = wide_threads(WD) / 64, CL0 = wide_cl0(WD);
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsB];
     const int tid = threadIdx.x;
-    stage_wide_tables(p, lds, tid);
+    stage_wide_tables<WD>(p, lds, tid);
     init_bad<kWideBad>(lds);
     __syncthreads();
 
@@ -1196,7 +1216,7 @@ __global__ __launch_bounds__(kWideWgThreads, 1) void fcs_wide_kernel(KParams p) 
     const int c = lane & (kGroup - 1);     // window index back from the frame end
     const int g = lane >> 4;               // frame of the item
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kWideItemBytes;
+    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kSlot;
     const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
     const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
     const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
@@ -1204,16 +1224,16 @@ __global__ __launch_bounds__(kWideWgThreads, 1) void fcs_wide_kernel(KParams p) 
     const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
 
     // launch constants: the front lane, its leading bytes, the words they reach (scalars)
-    const int cf = (int)((p.flen - 1u) / 124u) < 15 ? (int)((p.flen - 1u) / 124u) : 15;
-    const uint32_t zc = 124u * (uint32_t)cf + kWideWin - p.flen;   // 0 .. 127
+    const int cf = (int)((p.flen - 1u) / kStep) < 15 ? (int)((p.flen - 1u) / kStep) : 15;
+    const uint32_t zc = kStep * (uint32_t)cf + kWin - p.flen;   // 0 .. kWin - 1
     const uint32_t mwords = (zc + 3u) / 4u;
     const bool live = c <= cf, front = c == cf;
     const uint32_t x0 = front ? lds_rd(lds, dma_hole(kWideInvHole + zc / 32u) + (zc % 32u) * 4u) : 0u;
-    const int64_t klane = (int64_t)g * (int64_t)p.stride + (int64_t)p.flen - (int64_t)wide_end_off(c) - (int64_t)kWideWin;
+    const int64_t klane = (int64_t)g * (int64_t)p.stride + (int64_t)p.flen - (int64_t)(kStep * (uint32_t)c) - (int64_t)kWin;
 
     // slots are whole 16-B pieces inside [floor16(lo4), ceil16(hi4)) (as fcs_dma_kernel's)
     const uint64_t lo16 = p.lo4 & ~15ull;
-    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kWideItemBytes;
+    const uint64_t smax = ((p.hi4 + 15) & ~15ull) - kSlot;
     auto slot_src = [&](uint64_t S) {
         const uint64_t a = S & ~15ull;
         return a < lo16 ? lo16 : (a > smax ? smax : a);
@@ -1222,12 +1242,12 @@ __global__ __launch_bounds__(kWideWgThreads, 1) void fcs_wide_kernel(KParams p) 
     auto dma_of = [&](uint64_t i) {
         const uint64_t S = item_start(i), src = slot_src(S);
         const uint64_t e = S + 3 * p.stride + p.flen + 4 - src;
-        wide_dma_item(slot, src, lane, (uint32_t)(e < (uint64_t)kWideItemBytes ? e : (uint64_t)kWideItemBytes));
+        wide_dma_item<WD>(slot, src, lane, (uint32_t)(e < (uint64_t)kSlot ? e : (uint64_t)kSlot));
     };
 
     constexpr uint64_t kEnd = Dispenser::kEnd;
-    Dispenser D(p.ctr, (p.n + 3) >> 2, (uint64_t)gridDim.x * kWideWaves,
-                (uint64_t)blockIdx.x * kWideWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
+    Dispenser D(p.ctr, (p.n + 3) >> 2, (uint64_t)gridDim.x * kWaves,
+                (uint64_t)blockIdx.x * kWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
     D.align = 16;   // chunks start on 16-item groups: whole 256-B result runs
     uint64_t it = D.first();
     if (it != kEnd) dma_of(it);
@@ -1245,36 +1265,37 @@ __global__ __launch_bounds__(kWideWgThreads, 1) void fcs_wide_kernel(KParams p) 
         x = x < -(int64_t)kDmaRing ? -(int64_t)kDmaRing : x;
         const uint32_t r = (uint32_t)x & 3u;
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(slot + (x & ~3ll));
-        uint32_t d[kWideWords + 1];
+        uint32_t d[WD + 1];
 #pragma unroll
-        for (int q = 0; q < (int)kWideWords; q++) d[q] = wp[q];
-        {   // the 33rd dword matters only when r != 0; clamped so the last slot is never read past its end
-            const uint64_t a32 = (uint64_t)(wp + kWideWords), lim = (uint64_t)(lds + kWideLdsBytes - 4);
-            d[kWideWords] = *reinterpret_cast<const uint32_t *>(a32 < lim ? a32 : lim);
+        for (int q = 0; q < WD; q++) d[q] = wp[q];
+        {   // the last dword matters only when r != 0; clamped so the last slot is never read past its end
+            const uint64_t al = (uint64_t)(wp + WD), lim = (uint64_t)(lds + kLdsB - 4);
+            d[WD] = *reinterpret_cast<const uint32_t *>(al < lim ? al : lim);
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
         const uint64_t nxt = D.next(it);
         if (nxt != kEnd) dma_of(nxt);
 
-        uint32_t w[kWideWords];
+        uint32_t w[WD];
 #pragma unroll
-        for (int i = 0; i < (int)kWideWords; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+        for (int i = 0; i < WD; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
         // masks: word 0 of every live lane (its neighbour's last word) except the front lane's, whose
         // first zc bytes go (scalar masks, words below the launch-uniform bound only)
         w[0] &= front ? (zc >= 4u ? 0u : (uint32_t)(0xFFFFFFFFull << (8u * zc))) : 0u;
 #pragma unroll
-        for (int i = 1; i < (int)kWideWords; i++) {
+        for (int i = 1; i < WD; i++) {
             if ((uint32_t)i < mwords) {
                 const int t = (int)zc - 4 * i;
                 const uint32_t mk = t >= 4 ? 0u : (uint32_t)(0xFFFFFFFFull << (8 * (t < 0 ? 0 : t)));
                 w[i] &= front ? mk : 0xFFFFFFFFu;
             }
         }
-        uint32_t xa = w[0] ^ x0, xb = w[16];
+        // chain 0 over words [0, CL0), chain 1 over [CL0, WD), run side by side
+        uint32_t xa = w[0] ^ x0, xb = w[CL0];
 #pragma unroll
-        for (int i = 0; i < 16; i++) {
-            xa = step4_l8(lds, xa, i < 15 ? w[i + 1] : 0u, B, SEL);
-            xb = step4_l8(lds, xb, i < 15 ? w[17 + i] : 0u, B, SEL);
+        for (int i = 0; i < WD - CL0; i++) {
+            if (i < CL0) xa = step4_l8(lds, xa, i < CL0 - 1 ? w[i + 1] : 0u, B, SEL);
+            xb = step4_l8(lds, xb, i < WD - CL0 - 1 ? w[CL0 + i + 1] : 0u, B, SEL);
         }
         const uint32_t mv = merge_shift_dma(lds, 0, xa, xb);
         uint32_t v = live ? lane_shift_dma(lds, mv, lanebase) : 0u;
@@ -2478,7 +2499,8 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
         }
     } else if (!tiny && fixed_wide(p)) {
-        hipLaunchKernelGGL(fcs_wide_kernel, dim3(grid), dim3(kWideWgThreads), 0, st, p);
+        if (wide_wd(p) == 26) hipLaunchKernelGGL(fcs_wide_kernel<26>, dim3(grid), dim3(wide_threads(26)), 0, st, p);
+        else hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
     } else if (fixed_segil(p)) {
         hipLaunchKernelGGL(fcs_segil_kernel, dim3(grid), dim3(kSegilThreads), 0, st, p);
     } else if (!tiny && fixed_dma(p)) {

@@ -171,23 +171,34 @@ inline bool fixed_segil(const KParams &p) {
 // lane windows, 12 waves, 8 KiB slots) whose four consecutive frames fit one slot, as fixed_dma().
 // Against the kernels these lengths took before (tools/ab.py, one process): 1537 B
 // +22 %, 1600-1949 B +24 to +27 % (generic kernel, two segments), 1950-1988 B +23 to +26 %
-// (segment kernel); 1525-1536 B -8 % against the single-segment kernel, which keeps them.
+// (segment kernel); 1525-1536 B -8 % against the single-segment kernel, which keeps them. The
+// 104-B windows (WD 26) then took 1537-1604 B another +26 to +27 % (13 waves instead of 12).
 #ifndef FCS_WIDE_MIN   // measurement-only override of the band's lower end
 #define FCS_WIDE_MIN 1537
 #endif
 constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
-constexpr int kWideWgThreads = 768;
-inline bool fixed_wide(const KParams &p) {
+__host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : 832; }   // 12 / 13 waves
+// Window dwords for a fixed batch: 26 (104-B windows, 7 KiB slots, 13 waves) when the frame and its
+// item fit those, else 32 (128-B windows, 8 KiB slots, 12 waves); 0: not the wide kernel.
+inline int wide_wd(const KParams &p) {
 #ifdef FCS_NO_WIDE   // measurement-only build
     (void)p;
-    return false;
+    return 0;
 #else
-    return p.flen >= kWideMinLen && p.flen <= kWideCover && p.stride <= 4096 &&
-           3 * p.stride + p.flen <= kWideItemBytes - 18 && p.hi4 - p.lo4 >= 2 * kWideItemBytes;
+    if (p.flen < kWideMinLen || p.stride > 4096) return 0;
+#ifndef FCS_WIDE_NO26   // measurement-only: the 128-B windows for the whole band
+    if (p.flen <= kWideCover26 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&
+        p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(26))
+        return 26;
+#endif
+    if (p.flen <= kWideCover && 3 * p.stride + p.flen <= wide_slot(32) - 18 && p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(32))
+        return 32;
+    return 0;
 #endif
 }
+inline bool fixed_wide(const KParams &p) { return wide_wd(p) != 0; }
 inline int fixed_threads(const KParams &p) {
-    if (!fixed_tiny(p) && fixed_wide(p)) return kWideWgThreads;
+    if (!fixed_tiny(p) && fixed_wide(p)) return wide_threads(wide_wd(p));
     if (fixed_segil(p)) return kSegilWgThreads;
     if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;
     return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;

@@ -83,11 +83,15 @@ constexpr uint32_t kDmaItemBytes = 6144;                         // one wave's L
 // ending e_c = 124 c before the frame end. Each window's first word is its neighbour's last (masked
 // in every lane but the frame's front lane), and the 16 windows start on 16 distinct banks
 // ((e_c / 4) mod 32 = -c mod 32). 16 lanes cover e_15 + 128 = 1988 bytes; four frames per 8 KiB slot.
-constexpr uint32_t kWideWin = 128;
-constexpr uint32_t kWideWords = kWideWin / 4;                    // 32
-__host__ __device__ constexpr uint32_t wide_end_off(int c) { return 124u * (uint32_t)c; }
-constexpr uint32_t kWideCover = wide_end_off(15) + kWideWin;     // 1988
-constexpr uint32_t kWideItemBytes = 8192;
+// A second width for the band's low end: 104-byte windows every 100 B (cover 1604 B, 25 c mod 32
+// banks), four frames per 7 KiB slot, 13 waves. Template parameter WD = window dwords (32 or 26).
+constexpr uint32_t kWideWin = 128;                               // the widest window (INV table size)
+__host__ __device__ constexpr uint32_t wide_win(int wd) { return 4u * (uint32_t)wd; }
+__host__ __device__ constexpr uint32_t wide_step(int wd) { return 4u * (uint32_t)wd - 4u; }
+__host__ __device__ constexpr uint32_t wide_cover(int wd) { return 15u * wide_step(wd) + wide_win(wd); }
+__host__ __device__ constexpr uint32_t wide_slot(int wd) { return wd == 32 ? 8192u : 7168u; }
+constexpr uint32_t kWideCover = wide_cover(32);                  // 1988
+constexpr uint32_t kWideCover26 = wide_cover(26);                // 1604
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
@@ -106,9 +110,11 @@ constexpr uint32_t kBlobMerge = kBlobLaneDma + 8 * 16 * 32;     // uint32 [11][8
 constexpr int kStChunkTabs = 24, kStWordTabs = 17, kStInvTabs = 4;
 constexpr uint32_t kBlobStream = kBlobMerge + 11 * 8 * 16;
 constexpr uint32_t kBlobStreamK1 = kBlobStream + (kStChunkTabs + kStWordTabs + kStInvTabs) * 128;
-// Wide LDS-DMA kernel: lane tables A_{124 c} in the LDS-DMA layout [8][16][32], INV[z] for z < 128.
+// Wide LDS-DMA kernel: lane tables A_{124 c} (WD 32) and A_{100 c} (WD 26) in the LDS-DMA layout
+// [8][16][32], INV[z] for z < 128.
 constexpr uint32_t kBlobLaneWide = kBlobStreamK1 + 64;
-constexpr uint32_t kBlobInvWide = kBlobLaneWide + 8 * 16 * 32;
+constexpr uint32_t kBlobLaneWide26 = kBlobLaneWide + 8 * 16 * 32;
+constexpr uint32_t kBlobInvWide = kBlobLaneWide26 + 8 * 16 * 32;
 constexpr uint32_t kBlobWords = kBlobInvWide + kWideWin;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
@@ -201,10 +207,13 @@ struct Tables {
         for (int i = 0; i < kStWordTabs; i++) put(4L * i);
         for (int d = 1; d <= kStInvTabs; d++) put(-(long)d);
         for (int sg = 0; sg < 64; sg++) b[kBlobStreamK1 + sg] = shift(0xFFFFFFFFu, 64 - sg);
-        for (int slot = 0; slot < 32; slot++) {   // wide kernel
-            nibble_table((long)wide_end_off(slot % kGroup), nt);
+        for (int slot = 0; slot < 32; slot++) {   // wide kernel, both widths
+            nibble_table((long)wide_step(32) * (slot % kGroup), nt);
             for (int t = 0; t < 8; t++)
                 for (int e = 0; e < 16; e++) b[kBlobLaneWide + (t * 16 + e) * 32 + slot] = nt[t][e];
+            nibble_table((long)wide_step(26) * (slot % kGroup), nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobLaneWide26 + (t * 16 + e) * 32 + slot] = nt[t][e];
         }
         for (int z = 0; z < (int)kWideWin; z++) b[kBlobInvWide + z] = shift(0xFFFFFFFFu, -(long)z);
         return b;

@@ -320,73 +320,86 @@ def model_segil_frame(lds, frame: bytes, garbage: bytes):
 BLOB_STREAM = BLOB_MERGE + 11 * 8 * 16
 BLOB_STREAM_K1 = BLOB_STREAM + (24 + 17 + 4) * 128
 BLOB_LANE_WIDE = BLOB_STREAM_K1 + 64
-BLOB_INV_WIDE = BLOB_LANE_WIDE + 8 * 16 * 32
+BLOB_LANE_WIDE26 = BLOB_LANE_WIDE + 8 * 16 * 32
+BLOB_INV_WIDE = BLOB_LANE_WIDE26 + 8 * 16 * 32
 WIDE_WIN, WIDE_SLOT = 128, 8192
 WIDE_COVER = 124 * 15 + WIDE_WIN   # 1988
 WIDE_MERGE_HOLE, WIDE_INV_HOLE = 128, 132
+WIDE_CL0 = {32: 16, 26: 12}        # chain 0's words; chain 1 takes the rest
 
 
-def wide_end_off(c):
-    return 124 * c
+def wide_end_off(c, wd=32):
+    return (4 * wd - 4) * c
 
 
-def build_lds_wide(blob):
-    """fcs_wide_kernel's 64 KiB table image: the slice tables as fcs_dma_kernel's; holes 16t+n the
-    lane tables A_{124 c}; holes 128..131 the chain merge A_64; holes 132..135 INV[0..127]."""
+def wide_slot(wd):
+    return 8192 if wd == 32 else 7168
+
+
+def build_lds_wide(blob, wd=32):
+    """fcs_wide_kernel<WD>'s 64 KiB table image: the slice tables as fcs_dma_kernel's; holes 16t+n
+    the lane tables A_{(4 WD - 4) c}; holes 128..131 the chain merge A_{4 (WD - CL0)}; holes
+    132..135 INV[0..127]."""
+    lane_blob = BLOB_LANE_WIDE if wd == 32 else BLOB_LANE_WIDE26
+    k = (4 * (wd - WIDE_CL0[wd])) // 8
     lds = np.zeros(65536 // 4, dtype=np.uint32)
     for e in range(256):
         for sl in range(4):
             lds[(e * 256 + sl * 32) // 4:(e * 256 + sl * 32) // 4 + 8] = blob[BLOB_SLICE + 256 * (3 - sl) + e]
     for i in range(4096):
-        lds[(hole(i >> 5) + (i & 31) * 4) // 4] = blob[BLOB_LANE_WIDE + i]
+        lds[(hole(i >> 5) + (i & 31) * 4) // 4] = blob[lane_blob + i]
     for t in range(8):
         for e in range(16):
-            lds[(hole(WIDE_MERGE_HOLE + (t >> 1)) + 64 * (t & 1) + 4 * e) // 4] = blob[BLOB_MERGE + 7 * 128 + t * 16 + e]
+            lds[(hole(WIDE_MERGE_HOLE + (t >> 1)) + 64 * (t & 1) + 4 * e) // 4] = blob[BLOB_MERGE + (k - 1) * 128 + t * 16 + e]
     for z in range(WIDE_WIN):
         lds[(hole(WIDE_INV_HOLE + z // 32) + (z % 32) * 4) // 4] = blob[BLOB_INV_WIDE + z]
     return lds
 
 
-def wide_front(flen):
+def wide_front(flen, wd=32):
     """Front lane cf (the last lane whose window reaches into the frame) and its leading bytes zc."""
-    cf = min(15, (flen - 1) // 124)
-    return cf, 124 * cf + WIDE_WIN - flen
+    step = 4 * wd - 4
+    cf = min(15, (flen - 1) // step)
+    return cf, step * cf + 4 * wd - flen
 
 
-def model_wide_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f: int, garbage: bytes):
+def model_wide_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f: int, garbage: bytes, wd=32):
     """The four FCS values fcs_wide_kernel computes for the wave item whose first frame is f: lanes
     c <= cf are live; each masks its first word (its neighbour's last) except the front lane, which
     masks its zc leading bytes and starts from INV[zc]; two 16-word chains merged with A_64; lane
     shift A_{124 c}. Bytes a window reads outside the slot come from `garbage` (all masked)."""
     lo16 = (base & ~3) & ~15
     hi16 = (((base + (n - 1) * stride + flen + 3) & ~3) + 15) & ~15
-    smax = hi16 - WIDE_SLOT
+    slot = wide_slot(wd)
+    win, cl0 = 4 * wd, WIDE_CL0[wd]
+    smax = hi16 - slot
     S = base + f * stride
     src = min(max(S & ~15, lo16), smax)
     pad = 2048
-    img = bytearray(garbage[:pad]) + bytearray(WIDE_SLOT) + bytearray(garbage[pad:pad + 64])
-    chunk = mem[src:src + WIDE_SLOT]
+    img = bytearray(garbage[:pad]) + bytearray(slot) + bytearray(garbage[pad:pad + 64])
+    chunk = mem[src:src + slot]
     img[pad:pad + len(chunk)] = chunk
-    cf, zc = wide_front(flen)
+    cf, zc = wide_front(flen, wd)
     out = []
     for g in range(4):
         v = 0
         for c in range(cf + 1):
             lane = 16 * g + c
-            x = (S - src) + g * stride + flen - wide_end_off(c) - WIDE_WIN
+            x = (S - src) + g * stride + flen - wide_end_off(c, wd) - win
             r = x & 3
             a = pad + (x & ~3)
-            d = [int.from_bytes(img[a + 4 * q:a + 4 * q + 4], "little") for q in range(33)]
-            w = [alignbyte(d[i + 1], d[i], r) for i in range(32)]
+            d = [int.from_bytes(img[a + 4 * q:a + 4 * q + 4], "little") for q in range(wd + 1)]
+            w = [alignbyte(d[i + 1], d[i], r) for i in range(wd)]
             z = zc if c == cf else 4
-            for i in range(32):
+            for i in range(wd):
                 t = max(0, min(4, z - 4 * i))
                 w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
             x0 = int(lds[(hole(WIDE_INV_HOLE + zc // 32) + (zc % 32) * 4) // 4]) if c == cf else 0
-            xs = [w[0] ^ x0, w[16]]
-            for i in range(16):
-                for h in range(2):
-                    xs[h] = step4_l8(lds, xs[h], lane) ^ (w[h * 16 + i + 1] if i < 15 else 0)
+            xs = [w[0] ^ x0, w[cl0]]
+            for i in range(cl0):
+                xs[0] = step4_l8(lds, xs[0], lane) ^ (w[i + 1] if i < cl0 - 1 else 0)
+            for i in range(wd - cl0):
+                xs[1] = step4_l8(lds, xs[1], lane) ^ (w[cl0 + i + 1] if i < wd - cl0 - 1 else 0)
             m = merge_shift(lds, 0, xs[0]) ^ xs[1]   # A_64 at the merge holes (WIDE_MERGE_HOLE == MERGE_HOLE)
             lanebase = 128 + (lane & 31) * 4
             s = 0

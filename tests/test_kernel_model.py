@@ -175,13 +175,17 @@ def test_segil_decomposition_model(lds_dma, L):
 
 @pytest.fixture(scope="module")
 def lds_wide():
-    return km.build_lds_wide(na.tables_blob())
+    blob = na.tables_blob()
+    return {wd: km.build_lds_wide(blob, wd) for wd in (26, 32)}
 
 
-@pytest.mark.parametrize("flen,extra", [(1525, 0), (1530, 3), (1536, 0), (1537, 1), (1600, 0), (1611, 16), (1736, 0),
-                                        (1737, 5), (1860, 0), (1861, 2), (1949, 0), (1950, 100), (1987, 0), (1988, 0),
-                                        (1988, 74)])   # 3 stride + len = 8174: the largest item a slot takes
-def test_wide_kernel_model(lds_wide, flen, extra):
+@pytest.mark.parametrize("flen,extra,wd", [(1525, 0, 32), (1530, 3, 32), (1536, 0, 32), (1537, 1, 32), (1600, 0, 32),
+                                           (1611, 16, 32), (1736, 0, 32), (1737, 5, 32), (1860, 0, 32), (1861, 2, 32),
+                                           (1949, 0, 32), (1950, 100, 32), (1987, 0, 32), (1988, 0, 32),
+                                           (1988, 74, 32),   # 3 stride + len = 8174: the largest item a slot takes
+                                           (1537, 0, 26), (1538, 3, 26), (1501, 0, 26), (1600, 0, 26), (1601, 1, 26),
+                                           (1604, 0, 26), (1604, 178, 26)])   # 7150: the 7 KiB slot's largest
+def test_wide_kernel_model(lds_wide, flen, extra, wd):
     """fcs_wide_kernel's decomposition (128-B windows ending 124 c before the frame end, every
     live lane but the front one masking its first word, the front lane cf = (len - 1) / 124 masking
     its zc leading bytes and starting from INV[zc], lanes past it dropped, two 16-word chains merged
@@ -194,7 +198,7 @@ def test_wide_kernel_model(lds_wide, flen, extra):
         n = 11
         mem = bytes(rng.randrange(256) for _ in range(b0 + n * stride + 64))
         for f in range(0, n, 4):
-            got = km.model_wide_item(lds_wide, mem, b0, stride, flen, n, f, garbage)
+            got = km.model_wide_item(lds_wide[wd], mem, b0, stride, flen, n, f, garbage, wd)
             for g in range(4):
                 if f + g < n:
                     S = b0 + (f + g) * stride
@@ -203,6 +207,7 @@ def test_wide_kernel_model(lds_wide, flen, extra):
 
 def test_wide_windows_bank_distinct():
     """The 16 windows of a frame in fcs_wide_kernel start on 16 distinct dword banks (mod 32)."""
-    for E in range(0, 64, 4):
-        banks = {((E - km.wide_end_off(c) - km.WIDE_WIN) // 4) % 32 for c in range(16)}
-        assert len(banks) == 16
+    for wd in (26, 32):
+        for E in range(0, 64, 4):
+            banks = {((E - km.wide_end_off(c, wd) - 4 * wd) // 4) % 32 for c in range(16)}
+            assert len(banks) == 16
