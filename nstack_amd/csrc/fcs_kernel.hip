@@ -1153,12 +1153,12 @@ static_assert(wide_lds_bytes(32) <= 163840 && wide_lds_bytes(26) <= 163840, "LDS
 static_assert(kDmaMergeHole == kWideMergeHole, "merge_shift_dma reads merge table 0 at the same holes");
 // chain split: chain 0 = words [0, CL0), chain 1 = [CL0, WD); chain 1 spans 4 (WD - CL0) bytes, a
 // multiple of 8 so that its merge A_{4 (WD - CL0)} is one of the blob's A_{8 k}
-__host__ __device__ constexpr int wide_cl0(int wd) { return wd == 32 ? 16 : 12; }
+__host__ __device__ constexpr int wide_cl0(int wd) { return wd == 32 ? 16 : (wd == 30 ? 14 : 12); }
 
 template <int WD>
 __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds, int tid) {
     constexpr int NT = wide_threads(WD);
-    constexpr uint32_t kLane = WD == 32 ? kBlobLaneWide : kBlobLaneWide26;
+    constexpr uint32_t kLane = WD == 32 ? kBlobLaneWide : (WD == 30 ? kBlobLaneWide30 : kBlobLaneWide26);
     constexpr int kMergeK = 2 * (WD - wide_cl0(WD)) / 4;   // A_{8 k} with 8 k = 4 (WD - CL0)
     for (int i = tid; i < 2048; i += NT) {   // slice tables as fcs_dma_kernel
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
@@ -2499,7 +2499,9 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
         }
     } else if (!tiny && fixed_wide(p)) {
-        if (wide_wd(p) == 26) hipLaunchKernelGGL(fcs_wide_kernel<26>, dim3(grid), dim3(wide_threads(26)), 0, st, p);
+        const int wd = wide_wd(p);
+        if (wd == 26) hipLaunchKernelGGL(fcs_wide_kernel<26>, dim3(grid), dim3(wide_threads(26)), 0, st, p);
+        else if (wd == 30) hipLaunchKernelGGL(fcs_wide_kernel<30>, dim3(grid), dim3(wide_threads(30)), 0, st, p);
         else hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
     } else if (fixed_segil(p)) {
         hipLaunchKernelGGL(fcs_segil_kernel, dim3(grid), dim3(kSegilThreads), 0, st, p);

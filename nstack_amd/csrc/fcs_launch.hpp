@@ -172,14 +172,16 @@ inline bool fixed_segil(const KParams &p) {
 // Against the kernels these lengths took before (tools/ab.py, one process): 1537 B
 // +22 %, 1600-1949 B +24 to +27 % (generic kernel, two segments), 1950-1988 B +23 to +26 %
 // (segment kernel); 1525-1536 B -8 % against the single-segment kernel, which keeps them. The
-// 104-B windows (WD 26) then took 1537-1604 B another +26 to +27 % (13 waves instead of 12).
+// 104-B windows (WD 26) then took 1537-1604 B another +26 to +27 % (13 waves instead of 12), and
+// 120-B windows (WD 30) 1605-1787 B +16 to +19 %.
 #ifndef FCS_WIDE_MIN   // measurement-only override of the band's lower end
 #define FCS_WIDE_MIN 1537
 #endif
 constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
 __host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : 832; }   // 12 / 13 waves
-// Window dwords for a fixed batch: 26 (104-B windows, 7 KiB slots, 13 waves) when the frame and its
-// item fit those, else 32 (128-B windows, 8 KiB slots, 12 waves); 0: not the wide kernel.
+// Window dwords for a fixed batch: 26 (104-B windows) or 30 (120-B windows), 7 KiB slots and 13
+// waves, when the frame and its item fit those, else 32 (128-B windows, 8 KiB slots, 12 waves);
+// 0: not the wide kernel.
 inline int wide_wd(const KParams &p) {
 #ifdef FCS_NO_WIDE   // measurement-only build
     (void)p;
@@ -190,6 +192,11 @@ inline int wide_wd(const KParams &p) {
     if (p.flen <= kWideCover26 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&
         p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(26))
         return 26;
+#endif
+#ifndef FCS_WIDE_NO30   // measurement-only: no 120-B windows
+    if (p.flen <= kWideCover30 && 3 * p.stride + p.flen <= wide_slot(30) - 18 &&
+        p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(30))
+        return 30;
 #endif
     if (p.flen <= kWideCover && 3 * p.stride + p.flen <= wide_slot(32) - 18 && p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(32))
         return 32;

@@ -83,8 +83,9 @@ constexpr uint32_t kDmaItemBytes = 6144;                         // one wave's L
 // ending e_c = 124 c before the frame end. Each window's first word is its neighbour's last (masked
 // in every lane but the frame's front lane), and the 16 windows start on 16 distinct banks
 // ((e_c / 4) mod 32 = -c mod 32). 16 lanes cover e_15 + 128 = 1988 bytes; four frames per 8 KiB slot.
-// A second width for the band's low end: 104-byte windows every 100 B (cover 1604 B, 25 c mod 32
-// banks), four frames per 7 KiB slot, 13 waves. Template parameter WD = window dwords (32 or 26).
+// Narrower widths where four frames fit a 7 KiB slot (13 waves): 104-byte windows every 100 B
+// (cover 1604 B, banks 25 c mod 32) and 120-byte windows every 116 B (cover 1860 B, banks 29 c mod
+// 32). Template parameter WD = window dwords (26, 30 or 32).
 constexpr uint32_t kWideWin = 128;                               // the widest window (INV table size)
 __host__ __device__ constexpr uint32_t wide_win(int wd) { return 4u * (uint32_t)wd; }
 __host__ __device__ constexpr uint32_t wide_step(int wd) { return 4u * (uint32_t)wd - 4u; }
@@ -92,6 +93,7 @@ __host__ __device__ constexpr uint32_t wide_cover(int wd) { return 15u * wide_st
 __host__ __device__ constexpr uint32_t wide_slot(int wd) { return wd == 32 ? 8192u : 7168u; }
 constexpr uint32_t kWideCover = wide_cover(32);                  // 1988
 constexpr uint32_t kWideCover26 = wide_cover(26);                // 1604
+constexpr uint32_t kWideCover30 = wide_cover(30);                // 1860
 
 // Global "blob" the kernel copies into LDS at start; words kBlobLane.. are in LDS order.
 constexpr uint32_t kBlobSlice = 0;                      // uint32 [4][256]   (T0..T3)
@@ -114,7 +116,8 @@ constexpr uint32_t kBlobStreamK1 = kBlobStream + (kStChunkTabs + kStWordTabs + k
 // [8][16][32], INV[z] for z < 128.
 constexpr uint32_t kBlobLaneWide = kBlobStreamK1 + 64;
 constexpr uint32_t kBlobLaneWide26 = kBlobLaneWide + 8 * 16 * 32;
-constexpr uint32_t kBlobInvWide = kBlobLaneWide26 + 8 * 16 * 32;
+constexpr uint32_t kBlobLaneWide30 = kBlobLaneWide26 + 8 * 16 * 32;   // A_{116 c} (WD 30)
+constexpr uint32_t kBlobInvWide = kBlobLaneWide30 + 8 * 16 * 32;
 constexpr uint32_t kBlobWords = kBlobInvWide + kWideWin;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
@@ -214,6 +217,9 @@ struct Tables {
             nibble_table((long)wide_step(26) * (slot % kGroup), nt);
             for (int t = 0; t < 8; t++)
                 for (int e = 0; e < 16; e++) b[kBlobLaneWide26 + (t * 16 + e) * 32 + slot] = nt[t][e];
+            nibble_table((long)wide_step(30) * (slot % kGroup), nt);
+            for (int t = 0; t < 8; t++)
+                for (int e = 0; e < 16; e++) b[kBlobLaneWide30 + (t * 16 + e) * 32 + slot] = nt[t][e];
         }
         for (int z = 0; z < (int)kWideWin; z++) b[kBlobInvWide + z] = shift(0xFFFFFFFFu, -(long)z);
         return b;

@@ -321,11 +321,12 @@ BLOB_STREAM = BLOB_MERGE + 11 * 8 * 16
 BLOB_STREAM_K1 = BLOB_STREAM + (24 + 17 + 4) * 128
 BLOB_LANE_WIDE = BLOB_STREAM_K1 + 64
 BLOB_LANE_WIDE26 = BLOB_LANE_WIDE + 8 * 16 * 32
-BLOB_INV_WIDE = BLOB_LANE_WIDE26 + 8 * 16 * 32
+BLOB_LANE_WIDE30 = BLOB_LANE_WIDE26 + 8 * 16 * 32
+BLOB_INV_WIDE = BLOB_LANE_WIDE30 + 8 * 16 * 32
 WIDE_WIN, WIDE_SLOT = 128, 8192
 WIDE_COVER = 124 * 15 + WIDE_WIN   # 1988
 WIDE_MERGE_HOLE, WIDE_INV_HOLE = 128, 132
-WIDE_CL0 = {32: 16, 26: 12}        # chain 0's words; chain 1 takes the rest
+WIDE_CL0 = {32: 16, 30: 14, 26: 12}        # chain 0's words; chain 1 takes the rest
 
 
 def wide_end_off(c, wd=32):
@@ -340,7 +341,7 @@ def build_lds_wide(blob, wd=32):
     """fcs_wide_kernel<WD>'s 64 KiB table image: the slice tables as fcs_dma_kernel's; holes 16t+n
     the lane tables A_{(4 WD - 4) c}; holes 128..131 the chain merge A_{4 (WD - CL0)}; holes
     132..135 INV[0..127]."""
-    lane_blob = BLOB_LANE_WIDE if wd == 32 else BLOB_LANE_WIDE26
+    lane_blob = {32: BLOB_LANE_WIDE, 30: BLOB_LANE_WIDE30, 26: BLOB_LANE_WIDE26}[wd]
     k = (4 * (wd - WIDE_CL0[wd])) // 8
     lds = np.zeros(65536 // 4, dtype=np.uint32)
     for e in range(256):

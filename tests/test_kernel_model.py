@@ -176,7 +176,7 @@ def test_segil_decomposition_model(lds_dma, L):
 @pytest.fixture(scope="module")
 def lds_wide():
     blob = na.tables_blob()
-    return {wd: km.build_lds_wide(blob, wd) for wd in (26, 32)}
+    return {wd: km.build_lds_wide(blob, wd) for wd in (26, 30, 32)}
 
 
 @pytest.mark.parametrize("flen,extra,wd", [(1525, 0, 32), (1530, 3, 32), (1536, 0, 32), (1537, 1, 32), (1600, 0, 32),
@@ -184,7 +184,9 @@ def lds_wide():
                                            (1949, 0, 32), (1950, 100, 32), (1987, 0, 32), (1988, 0, 32),
                                            (1988, 74, 32),   # 3 stride + len = 8174: the largest item a slot takes
                                            (1537, 0, 26), (1538, 3, 26), (1501, 0, 26), (1600, 0, 26), (1601, 1, 26),
-                                           (1604, 0, 26), (1604, 178, 26)])   # 7150: the 7 KiB slot's largest
+                                           (1604, 0, 26), (1604, 178, 26),   # 7150: the 7 KiB slot's largest
+                                           (1605, 0, 30), (1700, 1, 30), (1741, 0, 30), (1742, 2, 30), (1787, 0, 30),
+                                           (1600, 3, 30)])
 def test_wide_kernel_model(lds_wide, flen, extra, wd):
     """fcs_wide_kernel's decomposition (128-B windows ending 124 c before the frame end, every
     live lane but the front one masking its first word, the front lane cf = (len - 1) / 124 masking
@@ -207,7 +209,7 @@ def test_wide_kernel_model(lds_wide, flen, extra, wd):
 
 def test_wide_windows_bank_distinct():
     """The 16 windows of a frame in fcs_wide_kernel start on 16 distinct dword banks (mod 32)."""
-    for wd in (26, 32):
+    for wd in (26, 30, 32):
         for E in range(0, 64, 4):
             banks = {((E - km.wide_end_off(c, wd) - 4 * wd) // 4) % 32 for c in range(16)}
             assert len(banks) == 16
