@@ -3,9 +3,13 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--frames-per-gpu F] [--len L]
 
+--gpus N is authoritative: started without a launcher (no WORLD_SIZE), bench.py starts the N ranks
+itself under torch.distributed.run before any GPU call; under a launcher WORLD_SIZE must equal N
+(else exit 1). config.devices lists every rank's HIP device and PCI address.
+
 A "step" is ONE launch of the FCS kernel over one batch: F (default 64 M) x 1518-B frames per
 GPU, already resident in HBM (BASELINE configs[1]; configs[4] = the same per GPU at N = 8).
-For N > 1 the driver starts one process per GPU (torch.distributed.run); frames shard
+For N > 1 one process runs per GPU (torch.distributed.run, by the driver or by bench.py); frames shard
 embarrassingly (each rank owns a contiguous slice of the global frame stream), so the only
 collectives are the timing barrier and the max-over-ranks of the elapsed time — none on the
 data path. value = bytes of all ranks / max rank time, in GiB/s.
@@ -21,7 +25,9 @@ Printed (rank 0, one JSON line): the contract fields plus
                  1 M x 1518 B (SURVEY §8d) on one host thread, the oracle port beside it; rank 0, N = 1;
   configs      — (N = 1) the other single-GPU BASELINE configs, each timed in this process after the
                  headline and freed before the next: imix_128M (configs[2]), jumbo_16M_x_9000
-                 (configs[3]) and host_inclusive_1518 (frames in pinned host memory -> H2D -> kernel
+                 (configs[3]; IMIX also beside its kernel's own load ceiling, stream_load_gbs = the
+                 arena-stream kernel's units, items and slot DMA without the CRC work) and
+                 host_inclusive_1518 (frames in pinned host memory -> H2D -> kernel
                  -> D2H, PCIe-bound; never `value`; its ceiling h2d_copy_gbs = plain async copies of
                  the same pinned arena), each with ms, GB/s, roofline frac (the HBM-bound ones also
                  against the headline run's two measured read ceilings) and a zlib spot check of
@@ -94,25 +100,46 @@ def _load_pmc_traffic(frames: int, L, kernel: str = None):
     return best
 
 
+def _profile_bundles():
+    """Committed kernel-statistics files of this command (tools/kernel_stats_split.py), oldest first:
+    profiles/rNN_bench_kernel_stats_split.csv (a round's first bundle), then any later bundle of the
+    same round (profiles/rNN_<tag>/rNN_<tag>_bench_kernel_stats_split.csv, e.g. r03_final)."""
+    import re
+    out = []
+    for p in glob.glob(os.path.join(ROOT, "profiles", "**", "r*_bench_kernel_stats_split.csv"), recursive=True):
+        m = re.match(r"r(\d+)(?:_([a-z0-9]+))?_bench_kernel_stats_split\.csv$", os.path.basename(p))
+        if m:   # a round's first bundle sorts before its tagged re-runs; tags in commit order by mtime-free name
+            out.append(((int(m.group(1)), 0 if m.group(2) is None else 1, m.group(2) or ""), p))
+    return [p for _, p in sorted(out)]
+
+
 def _load_kernel_profile(kernel: str, nbytes: int):
-    """The committed rocprofv3 kernel statistics of this command (profiles/rNN_bench_kernel_stats_split.csv,
-    newest round; tools/kernel_stats_split.py): the `kernel` row carrying the most time (the headline
-    launches; the host-inclusive pipeline launches the same kernel on small chunks). Returns the
-    traced average ms per launch and the roofline fraction it gives, beside the in-run HIP-event one."""
+    """The committed rocprofv3 kernel statistics of this command: the `kernel` row carrying the most
+    time (the headline launches; the host-inclusive pipeline launches the same kernel on small chunks)
+    of the NEWEST bundle (not the faster of two), with every bundle of that round listed
+    beside it. Returns the traced average ms per launch and the roofline fraction it gives, beside the
+    in-run HIP-event one."""
     import csv
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_bench_kernel_stats_split.csv")))
-    if not files:
+    files = _profile_bundles()
+
+    def row(path):
+        best = None
+        for r in csv.DictReader(open(path)):
+            if r["Name"].startswith(kernel) and (best is None or int(r["TotalDurationNs"]) > int(best["TotalDurationNs"])):
+                best = r
+        return best
+    rows = [(p, row(p)) for p in files]
+    rows = [(p, r) for p, r in rows if r is not None]
+    if not rows:
         return None
-    best = None
-    for r in csv.DictReader(open(files[-1])):
-        if r["Name"].startswith(kernel) and (best is None or int(r["TotalDurationNs"]) > int(best["TotalDurationNs"])):
-            best = r
-    if best is None:
-        return None
+    path, best = rows[-1]
     ms = float(best["AverageNs"]) / 1e6
+    rnd = os.path.basename(path)[:3]
     return {"profile_kernel_ms": round(ms, 4), "profile_median_ms": round(float(best["MedianNs"]) / 1e6, 4),
             "profile_calls": int(best["Calls"]), "profile_frac": round(nbytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-            "profile_source": os.path.relpath(files[-1], ROOT)}
+            "profile_source": os.path.relpath(path, ROOT),
+            "profile_bundles_this_round": {os.path.relpath(p, ROOT): round(float(r["AverageNs"]) / 1e6, 4)
+                                           for p, r in rows if os.path.basename(p).startswith(rnd)}}
 
 
 def _time_launches(fn, reps, stream, torch):
@@ -165,6 +192,10 @@ def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
     out = torch.empty(n, dtype=torch.int32, device=dev)
     ms = _time_launches(lambda: na.batch_dev(arena, total, off, ln, out, n, stream), reps, stream, torch)
     crcs = out.cpu().numpy().view(np.uint32)
+    # the arena-stream kernel's own load ceiling: the same units, items, slot DMA and schedule
+    # without marks, chain, contributions or closes (fcs_stream_load_dev)
+    lsink = torch.zeros(4, dtype=torch.int32, device=dev)
+    load_ms = _time_launches(lambda: na.stream_load_dev(arena, total, off, ln, n, lsink, stream), reps, stream, torch)
     offs = off.cpu().numpy()
     idx = rng.integers(0, n, 256)
     bad = _spot(crcs, lambda i: splitmix_bytes(SEED + 2, int(offs[i]), int(ln_np[i])).tobytes(), idx)
@@ -175,9 +206,12 @@ def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
                         "Gframes_s": round(n / ms / 1e6, 3), "metadata_bytes": n * 12,
                         "roofline": {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc[0] if pmc else None,
-                                     "traffic_source": pmc[1] if pmc else None},
+                                     "traffic_source": pmc[1] if pmc else None,
+                                     "stream_load_ms": round(load_ms, 4),
+                                     "stream_load_gbs": round(total / load_ms / 1e6, 1),
+                                     "frac_of_stream_load": round(load_ms / ms, 4)},
                         "spot_checked": len(idx), "spot_bad": bad}
-    del arena, out, off, ln, crcs, offs, ln_np
+    del arena, out, off, ln, crcs, offs, ln_np, lsink
     torch.cuda.empty_cache()
     # ---- configs[3]: 16 M x 9000-B jumbo frames ----
     n, L = 16 << 20, 9000
@@ -467,9 +501,75 @@ def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
             "value_16_threads": round(res["all"]["gibs"], 4)}
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(gpus: int, argv) -> int:
+    """`bench.py --gpus N` started without a launcher: start N rank processes of this script under
+    torch.distributed.run (one per GPU, rendezvous on 127.0.0.1) from this parent, which has made no
+    GPU call, and return their exit status. The ranks print the one JSON line (rank 0)."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+def device_entry(rank: int, local: int, torch, dry_run: bool):
+    """This rank's device identity for config.devices: HIP ordinal and PCI address (domain:bus:device)."""
+    if dry_run:
+        return {"rank": rank, "local_rank": local, "hip_device": None, "pci": None, "name": "dry-run (no GPU)"}
+    d = torch.cuda.current_device()
+    p = torch.cuda.get_device_properties(d)
+    pci = f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    return {"rank": rank, "local_rank": local, "hip_device": d, "pci": pci, "name": p.name,
+            "uuid": str(getattr(p, "uuid", ""))}
+
+
+def label_devices(entries):
+    """Mark ranks that share a physical GPU (a rehearsal of the N > 1 path on a smaller box)."""
+    seen = {}
+    for e in entries:
+        key = e.get("pci") or f"dry{e['rank']}"
+        seen.setdefault(key, []).append(e["rank"])
+    for e in entries:
+        key = e.get("pci") or f"dry{e['rank']}"
+        e["shares_gpu_with_ranks"] = [r for r in seen[key] if r != e["rank"]]
+    return entries, len(seen)
+
+
+def dry_run(args, world: int, rank: int, local: int) -> None:
+    """--dry-run: the launch and rendezvous only (gloo, no GPU call), for the CPU tests of --gpus."""
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("gloo")
+    entries = [device_entry(rank, local, torch, True)]
+    if dist:
+        allv = [None] * world
+        dist.all_gather_object(allv, entries[0])
+        entries = allv
+        dist.barrier()
+    if rank == 0:
+        devs, distinct = label_devices(entries)
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "GiB/s", "n_gpus": world, "dry_run": True,
+                          "config": {"devices": devs, "distinct_devices": distinct}}), flush=True)
+    if dist:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="GPUs (ranks). Without WORLD_SIZE in the environment and N > 1, bench.py starts the N "
+                         "ranks itself (torch.distributed.run); with WORLD_SIZE set it must equal N")
+    ap.add_argument("--dry-run", action="store_true", help="launch and rendezvous only, no GPU (CPU tests)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--frames-per-gpu", type=int, default=64 << 20)
@@ -481,13 +581,26 @@ def main():
                     help="N > 1: IMIX frames per GPU of the sharded configs[2] run (0 = skip)")
     args = ap.parse_args()
 
+    # --gpus is authoritative: no launcher -> start the ranks here, before any
+    # GPU call in this process; a launcher whose world size disagrees -> refuse
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    world = int(env_world or "1")
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}: refusing to time a different "
+              "number of GPUs than asked", file=sys.stderr, flush=True)
+        sys.exit(1)
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        dry_run(args, world, rank, local)
+        return
+
     import numpy as np
     import torch
     import nstack_amd as na
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
     if world > 1:
         # gloo on the host: the barrier and the 8-byte max-over-ranks of the elapsed time are the
@@ -501,6 +614,12 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     na.load()
+    devices = [device_entry(rank, local, torch, False)]
+    if dist:   # every rank's HIP device and PCI address, so a SCALE line shows N distinct GPUs
+        allv = [None] * world
+        dist.all_gather_object(allv, devices[0])
+        devices = allv
+    devices, distinct = label_devices(devices)
 
     L = args.len
     F = args.frames_per_gpu
@@ -642,7 +761,8 @@ def main():
             "config": {"workload": f"{F // (1 << 20)} M x {L}-B frames per GPU, one CRC-32 per frame, "
                                    "single HIP launch per step (BASELINE configs[1]; configs[4] at 8 GPUs)",
                        "frames_per_gpu": F, "frame_len": L, "global_frames": total,
-                       "parallelism": f"frames sharded over {world} GPU(s), no collective on the data path"},
+                       "parallelism": f"frames sharded over {world} GPU(s), no collective on the data path",
+                       "devices": devices, "distinct_devices": distinct},
             "pct_hbm_peak": round(100.0 * value * GIB / 1e9 / world / HBM_PEAK_GBS, 2),
             "verified": verified,
             "roofline": roofline,

@@ -30,7 +30,10 @@
  * retry fails too, or bsize >= 4 GiB (the kernels take 32-bit lengths), the call is answered by
  * the library's own host CRC instead of aborting, so the result never differs from the
  * reference. Each such call is counted (fcs_engine_host_fallbacks) and the first one is reported
- * on stderr; fcs_engine_stats counts calls, retries and recoveries.
+ * on stderr; fcs_engine_stats counts calls, retries and recoveries. The TX/RX call-site queues
+ * (nstack_txq.h, nstack_rxq.h) keep ether_send's / ether_receive's contract the same way: a batch
+ * whose GPU step fails is answered by that host CRC (fcs_engine_host_batches), never failed or
+ * dropped for FCS reasons.
  *
  * Threading: every entry point is thread-safe and may be called concurrently (the reference
  * calls ether_fcs from the main, ingress, egress and TCP-timer threads: SURVEY.md §8b).
@@ -70,6 +73,11 @@ void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t
 /* Drop-in calls answered by the host CRC because the GPU path failed twice or bsize >= 4 GiB
  * (0 on a healthy GPU: the GPU test suite asserts it). */
 uint64_t fcs_engine_host_fallbacks(void);
+/* Batches of the TX/RX call-site queues (nstack_txq.h, nstack_rxq.h) whose GPU step failed and
+ * whose FCSs were therefore computed or checked by the same host CRC, so that ether_send's and
+ * ether_receive's per-call results never depend on the GPU (0 on a healthy GPU: the GPU test
+ * suite asserts it). */
+uint64_t fcs_engine_host_batches(void);
 /* Host batch paths: calls that were split over more than one engine device, and the shard jobs
  * those calls ran (one host thread and pipeline each). Any pointer may be NULL. */
 void fcs_engine_host_stats(uint64_t *sharded_calls, uint64_t *shard_jobs);
@@ -139,6 +147,12 @@ int fcs_read_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *str
 /* The LDS-DMA read ceiling: the headline kernel's slot DMA (global_load_lds, nt), schedule and
  * window reads over [p, p+bytes) viewed as 1518-B frames, without the CRC work. */
 int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stream);
+/* The arena-stream kernel's own load ceiling (fcs_stream_kernel<true>): a windowed variable-length
+ * batch's units, unit check, 4 KiB items, slot DMA and schedule exactly as ether_fcs_batch_dev runs
+ * them, without the marks, chain, chunk contributions or closes; sink receives nothing (a store no
+ * realistic input triggers). Measurement only (bench.py configs.imix_128M.stream_load_gbs). */
+int fcs_stream_load_dev(const void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
+                        uint64_t n, uint32_t *sink, void *stream);
 /* Average device time (ms) per launch of the last `reps` timed FCS launches measured with
  * HIP events on the launch stream: fcs_timed_fixed_dev() launches ether_fcs_fixed_dev
  * `reps` times back to back, bracketed by events recorded on `stream`. */

@@ -18,7 +18,11 @@
  * Deviations, both for frames the reference mishandles: a frame shorter than the header (plus
  * trailer) is dropped and counted (the reference's min() on a negative length is undefined), and a
  * frame longer than 1518 bytes (1514 + trailer) is dropped and counted (the reference truncates it
- * to its 1514-byte buffer). Errors: -errno (the reference returns -1 with errno set).
+ * to its 1514-byte buffer). Errors: -errno from the socket (the reference returns -1 with errno
+ * set). ether_receive never fails or drops a frame for FCS reasons, so when the GPU check of a
+ * batch fails (HIP error, timeout, no GPU) the library's host CRC checks that batch instead
+ * (SURVEY.md §8b): the frames come out exactly as they would have. Such batches are counted
+ * (fcs_rxq_fallbacks, fcs_engine_host_batches) and the first is reported on stderr.
  * One consumer thread per queue (nstack's ingress thread); calls are serialised internally.
  */
 #ifndef NSTACK_RXQ_H
@@ -52,6 +56,9 @@ int fcs_rxq_receive(fcs_rxq_t *q, struct fcs_ether_hdr *hdr, uint8_t *buf, size_
  * own-MAC echoes skipped, runt or oversize frames dropped, recvmmsg batches. Any pointer may be NULL. */
 void fcs_rxq_stats(const fcs_rxq_t *q, uint64_t *frames, uint64_t *bad_fcs, uint64_t *echoes,
                    uint64_t *dropped, uint64_t *batches);
+/* Batches (and their frames) the host CRC checked because the GPU check failed. 0 on a healthy
+ * GPU. Any pointer may be NULL. */
+void fcs_rxq_fallbacks(const fcs_rxq_t *q, uint64_t *host_batches, uint64_t *host_frames);
 void fcs_rxq_destroy(fcs_rxq_t *q);
 
 #ifdef __cplusplus

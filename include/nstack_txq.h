@@ -16,8 +16,13 @@
  * producers fill batch k+1 while batch k is on the GPU/wire, so batches grow with the offered
  * load by themselves and a linger is only worth it for fire-and-forget senders.
  * fcs_txq_send() blocks until its own frame has been handed to the sink and returns that frame's
- * result. If the GPU step fails, every frame of that batch returns its -errno and none is sent:
- * no frame ever leaves with an FCS that was not computed by the engine.
+ * result. ether_send never fails for FCS reasons (it fails only on -EMSGSIZE, a bad handle or
+ * sendto, :234-269), so if the GPU step fails (HIP error, timeout, no GPU) the batch's FCSs are
+ * computed by the library's host CRC instead and the frames leave as usual: the
+ * per-call results never depend on the GPU. Such batches are counted (fcs_txq_fallbacks,
+ * fcs_engine_host_batches), the first is reported on stderr, and fcs_txq_last_error keeps the
+ * reason. A failed step's pinned arena is set aside (a late kernel may still write into it); after
+ * 16 such batches the queue stops calling the GPU and stays on the host CRC.
  */
 #ifndef NSTACK_TXQ_H
 #define NSTACK_TXQ_H
@@ -53,8 +58,8 @@ int fcs_txq_send_async(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const
 int fcs_txq_flush(fcs_txq_t *q);
 /* Flushes, stops the flusher thread and frees the queue. */
 void fcs_txq_destroy(fcs_txq_t *q);
-/* Counters since creation: frames handed to the sink (or failed by the engine), batches, and
- * frames whose result was not frame_size (send or engine errors). Any pointer may be NULL. */
+/* Counters since creation: frames handed to the sink, batches, and frames whose result was not
+ * frame_size (sink errors). Any pointer may be NULL. */
 void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint64_t *errors);
 /* Flusher time since creation, in ns, summed over batches: waiting for producers to finish
  * assembling, the GPU step (ether_fcs_tx_host), the sink, the whole per-batch busy time (their
@@ -64,6 +69,9 @@ void fcs_txq_timing(const fcs_txq_t *q, uint64_t *ns_ready, uint64_t *ns_gpu, ui
 /* Text of the most recent failed GPU step (fcs_last_error() of the flusher thread when its
  * ether_fcs_tx_batch_host call failed); "" when no batch has failed. Valid until the next call. */
 const char *fcs_txq_last_error(const fcs_txq_t *q);
+/* Batches (and their frames) whose FCSs the host CRC computed because the GPU step failed; the
+ * frames were sent all the same. 0 on a healthy GPU. Any pointer may be NULL. */
+void fcs_txq_fallbacks(const fcs_txq_t *q, uint64_t *host_batches, uint64_t *host_frames);
 
 /* ---- provided sinks ---- */
 /* ctx = pointer to an int file descriptor of a CONNECTED socket (e.g. a socketpair or a

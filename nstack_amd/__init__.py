@@ -17,18 +17,18 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "tx_batch_host", "host_buffer", "host_free", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan", "dma_stream_dev"]
+           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan", "dma_stream_dev", "stream_load_dev", "load_faults", "FAULTS_PATH"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
-    "fcs_tables_blob", "fcs_engine_stats", "fcs_engine_host_stats", "fcs_shard_plan", "fcs_dma_stream_dev",
+    "fcs_tables_blob", "fcs_engine_stats", "fcs_engine_host_stats", "fcs_shard_plan", "fcs_dma_stream_dev", "fcs_stream_load_dev",
     # include/nstack_txq.h — batched TX call site
-    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error",
+    "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error", "fcs_txq_fallbacks",
     "fcs_txq_sink_fd", "fcs_txq_sink_packet",
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
@@ -36,7 +36,7 @@ EXPORTS = [
     "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_csum_set_flat_threshold", "inet_ip_checksum",
     "inet_tcp_checksum", "inet_udp_checksum",
     # include/nstack_rxq.h — batched RX call site with FCS verification
-    "fcs_rxq_create", "fcs_rxq_receive", "fcs_rxq_stats", "fcs_rxq_destroy",
+    "fcs_rxq_create", "fcs_rxq_receive", "fcs_rxq_stats", "fcs_rxq_fallbacks", "fcs_rxq_destroy",
 ]
 
 # include/nstack_inet.h modes: the reference function each result reproduces
@@ -59,6 +59,34 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
     global _lib
     if _lib is not None:
         return _lib
+    _lib = _bind(path)
+    return _lib
+
+
+FAULTS_PATH = os.path.join(_HERE, "libnstack_fcs_faults.so")
+_faults = None
+
+
+def load_faults() -> ctypes.CDLL:
+    """The TEST-ONLY fault-hook build (-DFCS_FAULT_HOOK), bound like the product library plus its
+    fcs_debug_fail_next / fcs_debug_timeout_next / fcs_debug_fail_batches hooks. Its engine state
+    is separate from the product library's. Nothing in the product loads it."""
+    global _faults
+    if _faults is None:
+        L = _bind(FAULTS_PATH)
+        for name in ("fcs_debug_fail_next", "fcs_debug_timeout_next"):
+            f = getattr(L, name)
+            f.restype = None
+            f.argtypes = [ctypes.c_int]
+        L.fcs_debug_fail_batches.restype = None
+        L.fcs_debug_fail_batches.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.fcs_debug_batch_faults_left.restype = ctypes.c_int
+        L.fcs_debug_batch_faults_left.argtypes = []
+        _faults = L
+    return _faults
+
+
+def _bind(path: str) -> ctypes.CDLL:
     if not os.path.exists(path):
         raise FcsError(-errno.ENOENT, f"{path} not built (run `make -C nstack_amd`)")
     L = ctypes.CDLL(path)
@@ -89,11 +117,13 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_tables_blob": (i32, [vp, u64]),
         "fcs_engine_stats": (None, [c.POINTER(u64)] * 4),
         "fcs_engine_host_fallbacks": (u64, []),
+        "fcs_engine_host_batches": (u64, []),
         "fcs_debug_stream_listed": (c.c_int64, []),
         "fcs_debug_stream_unit_frames": (u32, []),
         "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
+        "fcs_stream_load_dev": (i32, [vp, u64, vp, vp, u64, vp, vp]),
         "fcs_txq_create": (vp, [vp, u32, u32, vp, vp]),
         "fcs_txq_send": (i32, [vp, vp, c.c_uint16, vp, c.c_size_t]),
         "fcs_txq_flush": (i32, [vp]),
@@ -102,6 +132,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_txq_stats": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
         "fcs_txq_timing": (None, [vp] + [c.POINTER(u64)] * 5),
         "fcs_txq_last_error": (c.c_char_p, [vp]),
+        "fcs_txq_fallbacks": (None, [vp, c.POINTER(u64), c.POINTER(u64)]),
         "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
         "fcs_txq_sink_packet": (None, [vp, vp, vp, vp, u32]),
         "fcs_pcap_scan": (i32, [c.c_char_p, c.POINTER(u64), c.POINTER(u64), c.POINTER(u32), c.POINTER(u64)]),
@@ -114,6 +145,7 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         "fcs_rxq_create": (vp, [i32, vp, u32, u32]),
         "fcs_rxq_receive": (i32, [vp, vp, vp, c.c_size_t]),
         "fcs_rxq_stats": (None, [vp] + [c.POINTER(u64)] * 5),
+        "fcs_rxq_fallbacks": (None, [vp, c.POINTER(u64), c.POINTER(u64)]),
         "fcs_rxq_destroy": (None, [vp]),
         "inet_ip_checksum": (c.c_uint16, [vp, c.c_size_t]),
         "inet_tcp_checksum": (c.c_uint16, [u32, u32, vp, c.c_size_t]),
@@ -123,7 +155,6 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
         f = getattr(L, name)
         f.restype = res
         f.argtypes = args
-    _lib = L
     return L
 
 
@@ -257,6 +288,12 @@ def dma_stream_dev(ptr, nbytes: int, sink, stream=None) -> None:
     _check(load().fcs_dma_stream_dev(_ptr(ptr), nbytes, _ptr(sink), _stream(stream)), "fcs_dma_stream_dev")
 
 
+def stream_load_dev(arena, arena_bytes: int, off, length, n: int, sink, stream=None) -> None:
+    """The arena-stream kernel's loads and schedule without its CRC work (fcs_stream_load_dev)."""
+    _check(load().fcs_stream_load_dev(_ptr(arena), arena_bytes, _ptr(off), _ptr(length), n, _ptr(sink),
+                                      _stream(stream)), "fcs_stream_load_dev")
+
+
 def read_stream_dev(ptr, nbytes: int, sink, stream=None) -> None:
     _check(load().fcs_read_stream_dev(_ptr(ptr), nbytes, _ptr(sink), _stream(stream)),
            "fcs_read_stream_dev")
@@ -277,6 +314,7 @@ def engine_stats() -> dict:
     L.fcs_engine_stats(*[c.byref(x) for x in v])
     d = dict(zip(("dropin_calls", "dropin_retries", "dropin_recovered", "lane_resets"), (x.value for x in v)))
     d["host_fallbacks"] = int(L.fcs_engine_host_fallbacks())   # drop-in calls the host CRC answered
+    d["host_batches"] = int(L.fcs_engine_host_batches())       # TX/RX queue batches the host CRC answered
     return d
 
 
@@ -321,37 +359,47 @@ class TxQueue:
     socket fd: send() has ether_send's return contract (frame_size or -errno); frames from all
     threads are FCS'd together on the GPU and leave in one sendmmsg per batch."""
 
-    def __init__(self, src_mac: bytes, fd: int, max_batch: int = 256, flush_usec: int = 0):
-        L = load()
+    def __init__(self, src_mac: bytes, fd: int, max_batch: int = 256, flush_usec: int = 0, sink=None,
+                 sink_ctx=None, lib=None):
+        """sink: None (fcs_txq_sink_fd on fd) or a C sink function pointer (e.g. fcs_txq_sink_packet)
+        with sink_ctx its context pointer; lib: the library to use (default: the product)."""
+        L = self._L = lib or load()
         self._fd = ctypes.c_int(fd)
         self._mac = (ctypes.c_uint8 * 6)(*src_mac)
-        sink = ctypes.cast(L.fcs_txq_sink_fd, ctypes.c_void_p)
-        self._q = L.fcs_txq_create(self._mac, max_batch, flush_usec, sink, ctypes.addressof(self._fd))
+        if sink is None:
+            sink, sink_ctx = ctypes.cast(L.fcs_txq_sink_fd, ctypes.c_void_p), ctypes.addressof(self._fd)
+        self._q = L.fcs_txq_create(self._mac, max_batch, flush_usec, sink, sink_ctx)
         if not self._q:
             raise FcsError(-errno.EINVAL, "fcs_txq_create")
 
     def send(self, dst: bytes, proto: int, payload: bytes) -> int:
-        return load().fcs_txq_send(self._q, bytes(dst), proto, bytes(payload), len(payload))
+        return self._L.fcs_txq_send(self._q, bytes(dst), proto, bytes(payload), len(payload))
 
     def send_async(self, dst: bytes, proto: int, payload: bytes) -> int:
-        return load().fcs_txq_send_async(self._q, bytes(dst), proto, bytes(payload), len(payload))
+        return self._L.fcs_txq_send_async(self._q, bytes(dst), proto, bytes(payload), len(payload))
 
     def flush(self) -> None:
-        _check(load().fcs_txq_flush(self._q), "fcs_txq_flush")
+        _check(self._L.fcs_txq_flush(self._q), "fcs_txq_flush")
 
     def stats(self):
         """(frames, batches, errors) since creation."""
         f, b, e = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
-        load().fcs_txq_stats(self._q, ctypes.byref(f), ctypes.byref(b), ctypes.byref(e))
+        self._L.fcs_txq_stats(self._q, ctypes.byref(f), ctypes.byref(b), ctypes.byref(e))
         return int(f.value), int(b.value), int(e.value)
+
+    def fallbacks(self):
+        """(host_batches, host_frames): batches whose FCSs the host CRC computed (GPU step failed)."""
+        hb, hf = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._L.fcs_txq_fallbacks(self._q, ctypes.byref(hb), ctypes.byref(hf))
+        return int(hb.value), int(hf.value)
 
     def last_error(self) -> str:
         """Text of the most recent failed GPU step ("" if none)."""
-        return (load().fcs_txq_last_error(self._q) or b"").decode()
+        return (self._L.fcs_txq_last_error(self._q) or b"").decode()
 
     def close(self) -> None:
         if self._q:
-            load().fcs_txq_destroy(self._q)
+            self._L.fcs_txq_destroy(self._q)
             self._q = None
 
     def __enter__(self):
@@ -367,16 +415,17 @@ class RxQueue:
     queued, negative = -errno); with trailer=True every recvmmsg batch is FCS-verified on the GPU,
     failing frames are dropped and the 4-byte trailer is stripped."""
 
-    def __init__(self, fd: int, own_mac: bytes, max_batch: int = 64, trailer: bool = True):
+    def __init__(self, fd: int, own_mac: bytes, max_batch: int = 64, trailer: bool = True, lib=None):
+        L = self._L = lib or load()
         self._mac = (ctypes.c_uint8 * 6)(*own_mac)
-        self._q = load().fcs_rxq_create(fd, self._mac, max_batch, 1 if trailer else 0)
+        self._q = L.fcs_rxq_create(fd, self._mac, max_batch, 1 if trailer else 0)
         if not self._q:
             raise FcsError(-errno.EINVAL, "fcs_rxq_create")
         self._hdr = (ctypes.c_uint8 * 14)()
         self._buf = (ctypes.c_uint8 * 2048)()
 
     def receive(self, bsize: int = 2048):
-        r = load().fcs_rxq_receive(self._q, self._hdr, self._buf, min(bsize, 2048))
+        r = self._L.fcs_rxq_receive(self._q, self._hdr, self._buf, min(bsize, 2048))
         if r <= 0:
             return r, None, None, None, b""
         h = bytes(self._hdr)
@@ -386,12 +435,18 @@ class RxQueue:
     def stats(self):
         """(frames, bad_fcs, echoes, dropped, batches) since creation."""
         v = [ctypes.c_uint64(0) for _ in range(5)]
-        load().fcs_rxq_stats(self._q, *[ctypes.byref(x) for x in v])
+        self._L.fcs_rxq_stats(self._q, *[ctypes.byref(x) for x in v])
         return tuple(int(x.value) for x in v)
+
+    def fallbacks(self):
+        """(host_batches, host_frames): batches the host CRC checked because the GPU check failed."""
+        hb, hf = ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._L.fcs_rxq_fallbacks(self._q, ctypes.byref(hb), ctypes.byref(hf))
+        return int(hb.value), int(hf.value)
 
     def close(self) -> None:
         if self._q:
-            load().fcs_rxq_destroy(self._q)
+            self._L.fcs_rxq_destroy(self._q)
             self._q = None
 
     def __enter__(self):

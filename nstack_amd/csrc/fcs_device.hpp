@@ -20,4 +20,7 @@ __attribute__((visibility("hidden"))) int mapped_submit(uint8_t *arena, uint64_t
                                                         const uint32_t *len, uint8_t *ok, uint64_t n,
                                                         uint64_t *ticket);
 __attribute__((visibility("hidden"))) int mapped_wait(uint64_t ticket);
+// A TX/RX queue batch whose GPU step failed was answered by the host CRC (fcs_host_crc.cpp):
+// counted in fcs_engine_host_batches(), the first one reported on stderr with the site and reason.
+__attribute__((visibility("hidden"))) void host_batch_answered(const char *site, const char *why);
 }  // namespace fcs

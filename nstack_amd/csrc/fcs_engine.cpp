@@ -100,10 +100,30 @@ bool injected_timeout() {
     g_inject_timeouts--;
     return true;
 }
+// ... and of the batch calls the TX/RX queues make (ether_fcs_tx_batch_host,
+// ether_fcs_verify_host, and the mapped-list submit and wait), whichever thread makes them (the TX
+// queue's GPU step runs on its flusher thread), the next `skip` run normally and the `calls` after
+// them fail. A failed wait leaves its kernel in flight.
+std::mutex g_inject_batch_mu;
+int g_inject_batch_skip = 0, g_inject_batch_calls = 0;
+bool injected_batch_fault() {
+    std::lock_guard<std::mutex> lk(g_inject_batch_mu);
+    if (g_inject_batch_skip > 0) {
+        g_inject_batch_skip--;
+        return false;
+    }
+    if (g_inject_batch_calls <= 0) return false;
+    g_inject_batch_calls--;
+    return true;
+}
 #else
 inline bool injected_fault() { return false; }
 inline bool injected_timeout() { return false; }
+inline bool injected_batch_fault() { return false; }
 #endif
+
+// Queue batches (TX/RX call sites) answered by the host CRC because their GPU step failed.
+std::atomic<uint64_t> g_host_batches{0};
 
 // Host pipeline resources of one device: kDepth chunks in flight (double-buffered by default).
 #ifndef FCS_PIPE_DEPTH   // measurement-only override (chunks in flight per device)
@@ -145,6 +165,7 @@ struct DevState {
     // kernel's list of units for fcs_flat_kernel), guarded by the same slot lease.
     uint32_t *ctr_scr[kCtrSlots] = {};
     uint64_t ctr_scr_words[kCtrSlots] = {};
+    uint32_t *d_last_listed = nullptr;   // the last arena-stream launch's unit-list length (in d_ctr's last line)
     // Streams and mapped result words of drop-in lanes given up while a kernel may still be in
     // flight on them (timeout, lost completion, device error): never reused or freed before
     // fcs_engine_fini, so a late kernel cannot write into memory that serves another call.
@@ -232,8 +253,10 @@ int make_dev_state(int dev, std::unique_ptr<DevState> *out) {
     const std::vector<uint32_t> &ki = kinit_table();
     if (ae == hipSuccess) ae = hipMalloc(&st->d_kinit, ki.size() * 4);
     if (ae == hipSuccess) ae = hipMemcpy(st->d_kinit, ki.data(), ki.size() * 4, hipMemcpyHostToDevice);
-    if (ae == hipSuccess) ae = hipMalloc(&st->d_ctr, DevState::kCtrSlots * 64);
-    if (ae == hipSuccess) ae = hipMemset(st->d_ctr, 0, DevState::kCtrSlots * 64);
+    // the counter ring plus one line for the last arena-stream launch's unit-list length
+    if (ae == hipSuccess) ae = hipMalloc(&st->d_ctr, (DevState::kCtrSlots + 1) * 64);
+    if (ae == hipSuccess) ae = hipMemset(st->d_ctr, 0, (DevState::kCtrSlots + 1) * 64);
+    if (ae == hipSuccess) st->d_last_listed = (uint32_t *)(st->d_ctr + 8 * DevState::kCtrSlots);
     hipSetDevice(cur);
     if (ae != hipSuccess) return hip_fail(ae, "uploading FCS tables");
     *out = std::move(st);
@@ -259,6 +282,7 @@ int dev_state(int dev, DevState **out) {
 // hook): a state of their own on HIP device id mod count, so the multi-device host path (shard
 // plan, one thread and pipeline per device, result assembly) runs on a one-GPU box.
 std::map<int, std::unique_ptr<DevState>> g_alias;
+std::vector<std::unique_ptr<DevState>> g_alias_retired;   // dropped by a later init; freed at fini
 
 int alias_state(int id, int ndev, DevState **out) {
     std::lock_guard<std::mutex> lk(g_mu);
@@ -317,8 +341,9 @@ uint64_t *g_dbg = nullptr;   // FCS_STAMPS builds only
 // 16384 = 4 frames x 16 waves x 256 CUs: one item per quarter-wave on a full chip.
 std::atomic<uint64_t> g_var_threshold{16384};
 
-// Device word holding the unit-list length of the last arena-stream launch (fcs_debug_stream_listed).
-std::atomic<uint32_t *> g_last_stream_count{nullptr};
+// The device whose d_last_listed holds the unit-list length of the last arena-stream launch
+// (fcs_debug_stream_listed). DevStates live until fcs_engine_fini, so the pointer stays valid.
+std::atomic<DevState *> g_last_stream_dev{nullptr};
 
 // Fixed-length batches of frames up to this length (and more than g_var_threshold frames) take the
 // flat variable-length kernel: a 64-B frame then costs one lane instead of a quarter-wave. Measured
@@ -367,7 +392,8 @@ int lease_scratch(CounterLease &lease, uint64_t words, uint32_t **out) {
     return 0;
 }
 
-int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p, CounterLease &lease) {
+// words: how many u64 counters of the slot's 64-B line the launch(es) use (1..8), all zeroed.
+int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p, CounterLease &lease, uint32_t words = 1) {
     const uint32_t slot = ds->ctr_seq.fetch_add(1, std::memory_order_relaxed) % DevState::kCtrSlots;
     ds->ctr_mu[slot].lock();
     lease.ds = ds;
@@ -379,7 +405,7 @@ int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p, CounterLease &le
         HIPTRY(hipStreamWaitEvent(st, ds->ctr_done[slot], 0), "waiting for the counter slot's last kernel");
     }
     p.ctr = ds->d_ctr + 8 * slot;
-    HIPTRY(hipMemsetAsync(p.ctr, 0, 8, st), "zeroing the work counter");
+    HIPTRY(hipMemsetAsync(p.ctr, 0, 8 * words, st), "zeroing the work counter");
     return 0;
 }
 
@@ -485,19 +511,24 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
     if (windowed && off != nullptr && p.hi4 - p.lo4 >= 2 * (uint64_t)fcs::kChunkBytes) {
         // arena stream for units of packed 64..1536-B frames, then fcs_flat_kernel for the units it
         // listed (it returns at once when there are none)
-        int rc = take_counter(ds, st, p, lease);
+        // one lease serves both kernels: the flat kernel's counter is the second word of the same
+        // 64-B counter line (taking a second slot while holding the first could land on the held
+        // slot once the ring wraps)
+        int rc = take_counter(ds, st, p, lease, 2);
         if (rc) return rc;
         const uint64_t units = (n + fcs::kStUnitFrames - 1) / fcs::kStUnitFrames;
         uint32_t *scr = nullptr;
         if ((rc = lease_scratch(lease, units + 1, &scr))) return rc;
         p.ucount = scr;
         p.ulist = scr + 1;
-        g_last_stream_count.store(scr, std::memory_order_relaxed);
         HIPTRY(hipMemsetAsync(p.ucount, 0, 4, st), "zeroing the unit list");
         HIPTRY(fcs::launch_stream(p, (int)std::min<uint64_t>((uint64_t)ds->cus, units), st), "launching fcs_stream_kernel");
+        // the unit-list length, copied out of the slot scratch for fcs_debug_stream_listed (the
+        // scratch is reused and may be regrown once the lease is released)
+        HIPTRY(hipMemcpyAsync(ds->d_last_listed, p.ucount, 4, hipMemcpyDeviceToDevice, st), "recording the unit list length");
+        g_last_stream_dev.store(ds, std::memory_order_relaxed);
         fcs::KParams q = p;
-        CounterLease lease2;
-        if ((rc = take_counter(ds, st, q, lease2))) return rc;
+        q.ctr = p.ctr + 1;
         HIPTRY(fcs::launch_fcs(true, true, q, grid, st), "launching fcs_flat_kernel<listed units>");
         return 0;
     }
@@ -1270,6 +1301,7 @@ int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off
     const uint8_t *doff = pinned_dev_ptr(off, n * 8), *dlen = pinned_dev_ptr(len, n * 4);
     uint8_t *dok = ok ? pinned_dev_ptr(ok, n) : nullptr;
     if (!da || !doff || !dlen || (ok && !dok)) return fail(EINVAL, "mapped_submit: buffers not from fcs_host_alloc");
+    if (injected_batch_fault()) return fail(EIO, "mapped_submit: injected fault (FCS_FAULT_HOOK build)");
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
     if (rc) return rc;
@@ -1322,10 +1354,20 @@ int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off
 }
 
 int fcs::mapped_wait(uint64_t ticket) {
+    // injected: give up at once, as if the wait had timed out, with the kernel still in flight
+    if (injected_batch_fault()) return fail(ETIMEDOUT, "mapped_wait: injected fault (FCS_FAULT_HOOK build)");
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
     if (rc) return rc;
     return wait_flag(devs[0]->tx_stream, devs[0]->tx_flag, ticket, "mapped-list batch");
+}
+
+void fcs::host_batch_answered(const char *site, const char *why) {
+    static std::atomic<bool> told{false};
+    if (!told.exchange(true))
+        std::fprintf(stderr, "nstack_fcs: %s: GPU step failed (%s); the batch is answered by the host CRC "
+                             "(counted in fcs_engine_host_batches; reported once)\n", site, why ? why : "");
+    g_host_batches.fetch_add(1, std::memory_order_relaxed);
 }
 
 void fcs::staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes) {
@@ -1444,10 +1486,11 @@ int fcs_engine_init(int ndev) {
         g_engine_devs.clear();
         for (int d = 0; d < use; d++) g_engine_devs.push_back(d);
         // alias states (NSTACK_FCS_ALIAS_DEVICES test hook) of ids that are no longer engine
-        // devices are released now, not at fcs_engine_fini
+        // devices are retired, not destroyed: a concurrent host call may still hold a raw pointer
+        // to one (taken from engine_devices before this init). fcs_engine_fini frees them.
         for (auto it = g_alias.begin(); it != g_alias.end();) {
             if (it->first >= use) {
-                destroy_state(it->second.get());
+                g_alias_retired.push_back(std::move(it->second));
                 it = g_alias.erase(it);
             } else {
                 ++it;
@@ -1468,8 +1511,12 @@ void fcs_engine_fini(void) {
         if (up) destroy_state(up.get());
     for (auto &kv : g_alias)
         if (kv.second) destroy_state(kv.second.get());
+    for (auto &up : g_alias_retired)
+        if (up) destroy_state(up.get());
+    g_last_stream_dev.store(nullptr, std::memory_order_relaxed);
     g_dev.clear();
     g_alias.clear();
+    g_alias_retired.clear();
     g_engine_devs.clear();
     hipSetDevice(cur);
 }
@@ -1551,6 +1598,7 @@ int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *o
     if (n == 0) return 0;
     if (!arena || !off || !len) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 4, __func__)) return rc;
+    if (injected_batch_fault()) return fail(EIO, "ether_fcs_tx_batch_host: injected fault (FCS_FAULT_HOOK build)");
     if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)arena + off[0], len[0]);
     if (arena_bytes <= kZeroCopyMaxBytes && (pinned_dev_ptr(arena, arena_bytes) || is_pinned(arena))) {
         std::vector<DevState *> devs;
@@ -1596,6 +1644,7 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
     if (n == 0) return 0;
     if (!arena || !off || !len || !ok) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
+    if (injected_batch_fault()) return fail(EIO, "ether_fcs_verify_host: injected fault (FCS_FAULT_HOOK build)");
     if (arena_bytes <= kZeroCopyMaxBytes) {
         if (const uint8_t *darena = pinned_dev_ptr(arena, arena_bytes)) {   // the RX queue's arena
             std::vector<DevState *> devs;
@@ -1649,11 +1698,13 @@ uint64_t fcs_engine_host_fallbacks(void) { return g_host_fallbacks.load(std::mem
 uint32_t fcs_debug_stream_unit_frames(void) { return fcs::kStUnitFrames; }
 
 int64_t fcs_debug_stream_listed(void) {
-    uint32_t *d = g_last_stream_count.load(std::memory_order_relaxed);
-    if (!d) return -1;
+    DevState *ds = g_last_stream_dev.load(std::memory_order_relaxed);
+    if (!ds) return -1;
+    DeviceGuard dg(ds->dev);   // read on the device that ran the launch
+    HIPTRY(dg.err, "hipSetDevice");
     HIPTRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
     uint32_t v = 0;
-    HIPTRY(hipMemcpy(&v, d, 4, hipMemcpyDeviceToHost), "reading the unit-list length");
+    HIPTRY(hipMemcpy(&v, ds->d_last_listed, 4, hipMemcpyDeviceToHost), "reading the unit-list length");
     return (int64_t)v;
 }
 
@@ -1670,9 +1721,20 @@ void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t
     if (lane_resets) *lane_resets = g_lane_resets.load(std::memory_order_relaxed);
 }
 
+uint64_t fcs_engine_host_batches(void) { return g_host_batches.load(std::memory_order_relaxed); }
+
 #ifdef FCS_FAULT_HOOK
 void fcs_debug_fail_next(int attempts) { g_inject_faults = attempts; }
 void fcs_debug_timeout_next(int attempts) { g_inject_timeouts = attempts; }
+void fcs_debug_fail_batches(int skip, int calls) {
+    std::lock_guard<std::mutex> lk(g_inject_batch_mu);
+    g_inject_batch_skip = skip;
+    g_inject_batch_calls = calls;
+}
+int fcs_debug_batch_faults_left(void) {
+    std::lock_guard<std::mutex> lk(g_inject_batch_mu);
+    return g_inject_batch_skip + g_inject_batch_calls;
+}
 #endif
 
 int fcs_shard_plan(const uint32_t *len, uint64_t n, uint32_t parts, uint64_t *cut) {
@@ -1756,6 +1818,32 @@ int fcs_dma_stream_dev(const void *p, uint64_t bytes, uint32_t *sink, void *stre
     CounterLease lease;
     if ((rc = take_counter(ds, st, k, lease))) return rc;
     HIPTRY(fcs::launch_dma_stream(k, grid, st), "launching the LDS-DMA read stream");
+    return 0;
+}
+
+int fcs_stream_load_dev(const void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
+                        uint64_t n, uint32_t *sink, void *stream) {
+    if (!arena || !off || !len || !sink) return fail(EINVAL, "null pointer");
+    if (n == 0) return 0;
+    DevState *ds = nullptr;
+    int rc = current_dev_state(&ds);
+    if (rc) return rc;
+    fcs::KParams k{};
+    k.base = (uint64_t)arena;
+    k.off = off;
+    k.len = len;
+    k.n = n;
+    k.lo4 = floor4((uint64_t)arena);
+    k.hi4 = ceil4((uint64_t)arena + arena_bytes);
+    k.zmax = fcs::kChunkBytes;
+    k.blob = ds->d_blob;
+    k.out = sink;
+    const hipStream_t st = (hipStream_t)stream;
+    const uint64_t units = (n + fcs::kStUnitFrames - 1) / fcs::kStUnitFrames;
+    CounterLease lease;
+    if ((rc = take_counter(ds, st, k, lease))) return rc;
+    HIPTRY(fcs::launch_stream(k, (int)std::min<uint64_t>((uint64_t)ds->cus, units), st, true),
+           "launching the arena-stream load walk");
     return 0;
 }
 

@@ -1,4 +1,5 @@
-// fcs_host_crc.cpp — host CRC-32 for the drop-in's failure path only (fcs_host_crc.hpp).
+// fcs_host_crc.cpp — host CRC-32 for the failure paths of the drop-in and the TX/RX queues only
+// (fcs_host_crc.hpp).
 //
 // Slice-by-16: sixteen 256-entry tables, table k advancing a byte past k further zero bytes, so
 // one step folds 16 input bytes with 16 independent lookups. The tables are derived from the

@@ -1429,6 +1429,10 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     uint32_t acc = 0;   // this quarter's frame: CRC state after its segments so far
     uint32_t cbuf = 0;    // FCSs of the current run of units, lane 4 (unit & 15) + frame
     uint64_t cmask = 0;   // lanes of cbuf that hold one (wave-uniform)
+#ifdef FCS_STAMPS   // measurement-only: per-wave slot wait, finishing time, XCD and clock (as fcs_dma_kernel)
+    uint64_t st_wait = 0, st_all = 0, st_items = 0;
+    const uint64_t st_rt0 = __builtin_amdgcn_s_memrealtime(), st_c0 = __builtin_amdgcn_s_memtime();
+#endif
     while (u != kEnd) {   // wave-uniform
         const uint64_t f = 4 * u + q;
         const bool act = f < n;
@@ -1436,7 +1440,17 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
         const uint32_t len = r ? kDmaCover : Lf;
         const int64_t x = (int64_t)(s0 & 15ull) + (int64_t)len - (int64_t)ec - kChunkBytes;   // window start in the run
         const uint32_t ra = (uint32_t)x & 3u;
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        const uint64_t ts0 = __builtin_amdgcn_s_memtime();
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's runs have landed
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        st_wait += __builtin_amdgcn_s_memtime() - ts0;
+        __builtin_amdgcn_sched_barrier(0);
+#endif
         const uint32_t *wp = reinterpret_cast<const uint32_t *>(run + (x & ~3ll));
         uint32_t d[kChunkWords + 1];
 #pragma unroll
@@ -1515,7 +1529,27 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
         }
         u = un;
         r = rn;
+#ifdef FCS_STAMPS
+        __builtin_amdgcn_sched_barrier(0);
+        st_all += __builtin_amdgcn_s_memtime() - ts0;
+        st_items++;
+        __builtin_amdgcn_sched_barrier(0);
+#endif
     }
+#ifdef FCS_STAMPS
+    if (p.dbg != nullptr && lane == 0) {
+        const uint32_t wv = blockIdx.x * kSegilWaves + (uint32_t)wave;
+        const uint64_t rt1 = __builtin_amdgcn_s_memrealtime();
+        p.dbg[wv * 8 + 0] = st_wait;
+        p.dbg[wv * 8 + 1] = st_all;
+        p.dbg[wv * 8 + 2] = st_items;
+        p.dbg[wv * 8 + 3] = rt1 - st_rt0;
+        p.dbg[wv * 8 + 4] = __builtin_amdgcn_s_memtime() - st_c0;
+        p.dbg[wv * 8 + 5] = st_rt0;
+        p.dbg[wv * 8 + 6] = rt1;
+        p.dbg[wv * 8 + 7] = __builtin_amdgcn_s_getreg(/*HW_REG_XCC_ID*/ (20 << 0) | (0 << 6) | (3 << 11));
+    }
+#endif
     flush_bad<kDmaBad>(p, lds);
 }
 
@@ -1916,6 +1950,10 @@ __device__ __forceinline__ void stage_stream_tables(const KParams &p, uint8_t *l
     for (int i = tid; i < 16 * 256; i += kWgThreads) reinterpret_cast<uint32_t *>(lds + kStRings)[i] = 0u;
 }
 
+// LOAD: the measurement form behind fcs_stream_load_dev: the same units, unit
+// check, items, slot DMA and schedule, but no marks, chain, contributions or closes; each lane only
+// XORs its chunk's words (the stream kernel's own load ceiling).
+template <bool LOAD>
 __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kStLdsBytes];
     const int tid = threadIdx.x;
@@ -1974,6 +2012,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
     const uint64_t st_begin = __builtin_amdgcn_s_memtime();
 #endif
     Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kStWaves, (uint64_t)blockIdx.x * kStWaves + wave, lane, 100, 1, 8);
+    uint32_t lx = 0;   // LOAD only: the XOR of every word this lane read
     for (uint64_t u = D.first(); u != kEnd; u = D.next(u)) {
         ST_T(tu0)
         const uint64_t f0 = u * kStUnitFrames;
@@ -2006,7 +2045,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             bad |= g + 1 < nf && ns != S[q] + Ln[q];
         }
         if (__any(bad)) {
-            if (lane == 0) p.ulist[atomicAdd(p.ucount, 1u)] = (uint32_t)u;
+            if (!LOAD && lane == 0) p.ulist[atomicAdd(p.ucount, 1u)] = (uint32_t)u;
             continue;
         }
         // ---- geometry, relative to X0 (the first item's start) ----
@@ -2062,6 +2101,21 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
 #endif
             emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + g, ~reg);
         };
+        if (LOAD) {   // the item walk alone: slot wait, word reads, next DMA
+            for (uint32_t t = 0; t < nitems; t++) {
+                const uint32_t Xr = kStItem * t;
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const u32x4 x = *pc[i];
+                    lx ^= x.x ^ x.y ^ x.z ^ x.w;
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                if (t + 1 < nitems) dma_item(X0 + Xr + kStItem);
+            }
+            wave_lds_sync();
+            continue;
+        }
         for (uint32_t t = 0; t < nitems; t++) {
             const uint32_t Xr = kStItem * t;
             ST_T(ti0)
@@ -2207,6 +2261,10 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         for (int i = 0; i < 8; i++) p.dbg[wv * 8 + i] = sts[i];
     }
 #endif
+    if (LOAD) {   // keep the word reads live: a store no realistic input triggers
+        if (lx == 0x5EEDF00Du && p.out) p.out[0] = lx;
+        return;
+    }
     flush_bad<kStBad>(p, lds);
 }
 
@@ -2554,9 +2612,12 @@ hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_stream(const KParams &p, int grid, hipStream_t st) {
+hipError_t launch_stream(const KParams &p, int grid, hipStream_t st, bool load_only) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
-    hipLaunchKernelGGL(fcs_stream_kernel, dim3(grid), dim3(kWgThreads), 0, st, p);
+    if (load_only)
+        hipLaunchKernelGGL(fcs_stream_kernel<true>, dim3(grid), dim3(kWgThreads), 0, st, p);
+    else
+        hipLaunchKernelGGL(fcs_stream_kernel<false>, dim3(grid), dim3(kWgThreads), 0, st, p);
     return hipGetLastError();
 }
 

@@ -219,7 +219,8 @@ hipError_t launch_small_list(const ListArgs &a, hipStream_t st);
 hipError_t launch_fill(void *p, uint64_t bytes, uint64_t seed, uint64_t off, hipStream_t st);
 hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hipStream_t st);
 hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st);
-hipError_t launch_stream(const KParams &p, int grid, hipStream_t st);
+// load_only: fcs_stream_kernel<true>, the measurement form behind fcs_stream_load_dev
+hipError_t launch_stream(const KParams &p, int grid, hipStream_t st, bool load_only = false);
 hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,
                            uint64_t n, hipStream_t st);
 

@@ -3,7 +3,9 @@
 // Mirrors ether_receive (/root/reference/src/linux/ether.c:180-212) per call while the frames
 // arrive in recvmmsg batches and, with FCS_RXQ_TRAILER, are verified on the GPU (CRC residue over
 // frame + trailer). Two buffers alternate: while the GPU checks one batch, the next recvmmsg fills
-// the other. The CRC itself is never computed here.
+// the other. ether_receive never fails or drops frames for FCS reasons, so when the GPU check of a
+// batch fails (HIP error, timeout, no GPU) the library's host CRC checks it instead
+// (fcs_host_crc.cpp), counted per queue and in fcs_engine_host_batches.
 #include <arpa/inet.h>
 #include <sys/socket.h>
 
@@ -17,6 +19,7 @@
 #include "../../include/nstack_fcs.h"
 #include "../../include/nstack_rxq.h"
 #include "fcs_device.hpp"
+#include "fcs_host_crc.hpp"
 
 namespace {
 constexpr uint32_t kHeaderLen = 14;     // ETHER_HEADER_LEN (src/nstack_ether.h:27)
@@ -24,6 +27,8 @@ constexpr uint32_t kFcsLen = 4;         // ETHER_FCS_LEN
 constexpr uint32_t kMaxLen = 1514;      // ETHER_MAXLEN: ether_receive's buffer (:183)
 constexpr uint32_t kSlot = 2048;        // receive slot: a longer frame shows up as truncated
 constexpr uint32_t kMaxBatch = 4096;
+constexpr uint32_t kResidue = 0x2144DF1Cu;   // CRC-32 of any frame followed by its own LE FCS
+constexpr size_t kMaxQuarantine = 64;   // ok arrays set aside after failed GPU checks (then host-only)
 }  // namespace
 
 // One receive buffer: recvmmsg slots plus the frame list the verify kernel reads. With the
@@ -35,6 +40,7 @@ struct RxBuf {
     uint32_t *len = nullptr;
     uint8_t *ok = nullptr;
     bool pinned = false;                // all four from fcs_host_alloc
+    bool ok_pinned = false;             // ok from fcs_host_alloc (it may be replaced, see quarantine)
     uint32_t n = 0, next = 0;           // frames in the buffer, next one to hand out
     uint64_t ticket = 0;
     enum State { kEmpty, kInFlight, kReady } state = kEmpty;
@@ -50,16 +56,22 @@ struct fcs_rxq {
     std::vector<mmsghdr> msgs;
     std::vector<iovec> iov;
     uint64_t n_frames = 0, n_bad = 0, n_echo = 0, n_drop = 0, n_batches = 0;
+    uint64_t n_host_batches = 0, n_host_frames = 0;   // batches the host CRC checked
+    // ok arrays of batches whose GPU check failed after a launch: a late kernel may still write
+    // them, so they are never reused before fcs_rxq_destroy. After kMaxQuarantine such batches the
+    // queue stops using the GPU (host_only).
+    std::vector<std::pair<uint8_t *, bool>> quarantine;   // (array, from fcs_host_alloc)
+    bool host_only = false;
     std::mutex mu;
 };
 
 namespace {
 void free_buf(RxBuf &B) {
     void *p[4] = {B.arena, B.off, B.len, B.ok};
-    for (void *x : p)
-        if (x) {
-            if (B.pinned) fcs_host_free(x);
-            else std::free(x);
+    for (int i = 0; i < 4; i++)
+        if (p[i]) {
+            if (i == 3 ? B.ok_pinned : B.pinned) fcs_host_free(p[i]);
+            else std::free(p[i]);
         }
     B = RxBuf{};
 }
@@ -79,6 +91,7 @@ bool alloc_buf(RxBuf &B, uint32_t cap, bool pinned) {
     B.len = (uint32_t *)p[2];
     B.ok = (uint8_t *)p[3];
     B.pinned = pinned;
+    B.ok_pinned = pinned;
     return true;
 }
 
@@ -114,36 +127,58 @@ int recv_into(fcs_rxq *q, RxBuf &B, int flags) {
     return (int)n;
 }
 
-// Start B's trailer check (pipelined: launch only), or do it at once. No unchecked frame is
-// handed out: on failure the batch is dropped and -errno returned.
-int start_check(fcs_rxq *q, RxBuf &B) {
-    if (!(q->flags & FCS_RXQ_TRAILER)) {
-        B.state = RxBuf::kReady;
-        return 0;
-    }
-    if (q->pipelined) {
-        const int rc = fcs::mapped_submit(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n, &B.ticket);
-        if (rc) {
-            B.state = RxBuf::kEmpty;
-            return rc;
+// The GPU check of B failed: check it with the host CRC instead (ether_receive
+// never drops a frame for FCS reasons). launched: a kernel of the failed step may still be in
+// flight and write B.ok, so that array is set aside and B gets a fresh one.
+void host_check(fcs_rxq *q, RxBuf &B, bool launched) {
+    const char *why = q->host_only ? "queue in host-only mode after repeated GPU failures" : fcs_last_error();
+    if (launched && !q->host_only) {
+        uint8_t *fresh = B.pinned ? (uint8_t *)fcs_host_alloc(q->cap) : nullptr;
+        const bool fresh_pinned = fresh != nullptr;
+        if (!fresh) fresh = (uint8_t *)std::malloc(q->cap);
+        if (fresh && q->quarantine.size() < kMaxQuarantine) {
+            q->quarantine.emplace_back(B.ok, B.ok_pinned);
+            B.ok = fresh;
+            B.ok_pinned = fresh_pinned;
+            if (!fresh_pinned) q->host_only = true;   // mapped_submit needs an fcs_host_alloc array
+        } else {
+            if (fresh) fresh_pinned ? fcs_host_free(fresh) : std::free(fresh);
+            q->host_only = true;
         }
-        B.state = RxBuf::kInFlight;
-        return 0;
     }
-    const int64_t bad = ether_fcs_verify_host(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n);
-    if (bad < 0) {
-        B.state = RxBuf::kEmpty;
-        return (int)bad;
+    for (uint32_t i = 0; i < B.n; i++) {
+        const uint32_t L = B.len[i];   // 0: runt or oversize, dropped anyway
+        B.ok[i] = L >= kFcsLen && fcs::host_crc32(B.arena + B.off[i], L) == kResidue;
     }
+    fcs::host_batch_answered("fcs_rxq_receive", why);
+    q->n_host_batches++;
+    q->n_host_frames += B.n;
     B.state = RxBuf::kReady;
-    return 0;
 }
 
-int finish_check(RxBuf &B) {
-    if (B.state != RxBuf::kInFlight) return 0;
-    const int rc = fcs::mapped_wait(B.ticket);
-    B.state = rc ? RxBuf::kEmpty : RxBuf::kReady;
-    return rc;
+// Start B's trailer check (pipelined: launch only), or do it at once. Every frame handed out has
+// been checked, by the GPU or, when its step failed, by the host CRC.
+void start_check(fcs_rxq *q, RxBuf &B) {
+    if (!(q->flags & FCS_RXQ_TRAILER)) {
+        B.state = RxBuf::kReady;
+        return;
+    }
+    if (q->host_only) return host_check(q, B, false);
+    if (q->pipelined && B.ok_pinned) {
+        if (fcs::mapped_submit(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n, &B.ticket))
+            return host_check(q, B, false);   // nothing launched
+        B.state = RxBuf::kInFlight;
+        return;
+    }
+    const int64_t bad = ether_fcs_verify_host(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n);
+    if (bad < 0) return host_check(q, B, true);
+    B.state = RxBuf::kReady;
+}
+
+void finish_check(fcs_rxq *q, RxBuf &B) {
+    if (B.state != RxBuf::kInFlight) return;
+    if (fcs::mapped_wait(B.ticket)) return host_check(q, B, true);
+    B.state = RxBuf::kReady;
 }
 }  // namespace
 
@@ -199,33 +234,32 @@ int fcs_rxq_receive(fcs_rxq_t *q, struct fcs_ether_hdr *hdr, uint8_t *buf, size_
             B.state = RxBuf::kEmpty;
         }
         RxBuf &O = q->b[1 - q->cur];
+        if (O.state == RxBuf::kReady) {   // received after B and already checked (by the host CRC)
+            q->cur = 1 - q->cur;
+            continue;
+        }
         if (O.state == RxBuf::kInFlight) {
             // the GPU checks O: meanwhile take whatever is already queued into B (no waiting, so
             // O's frames are not held back by a quiet link), then hand out O
             const int r = recv_into(q, B, MSG_DONTWAIT);
-            if (r < 0) return r;
-            if (r > 0) {
-                const int rc = start_check(q, B);
-                if (rc) return rc;
+            if (r < 0) {
+                finish_check(q, O);   // O's frames stay queued for the next call
+                q->cur = 1 - q->cur;
+                return r;
             }
-            const int rc = finish_check(O);
-            if (rc) return rc;
+            if (r > 0) start_check(q, B);
+            finish_check(q, O);
             q->cur = 1 - q->cur;
             continue;
         }
         const int r = recv_into(q, B, MSG_WAITFORONE);   // the socket's own blocking mode
         if (r <= 0) return r;   // 0: nothing queued (:196-198); -errno
-        int rc = start_check(q, B);
-        if (rc) return rc;
+        start_check(q, B);
         if (q->pipelined) {   // the next batch, if one is already queued, goes to the GPU behind B
             const int r2 = recv_into(q, O, MSG_DONTWAIT);
-            if (r2 > 0 && (rc = start_check(q, O))) {
-                finish_check(B);
-                B.state = RxBuf::kEmpty;
-                return rc;
-            }
+            if (r2 > 0) start_check(q, O);
         }
-        if ((rc = finish_check(B))) return rc;
+        finish_check(q, B);
     }
 }
 
@@ -241,12 +275,21 @@ void fcs_rxq_stats(const fcs_rxq_t *q, uint64_t *frames, uint64_t *bad_fcs, uint
     if (batches) *batches = m->n_batches;
 }
 
+void fcs_rxq_fallbacks(const fcs_rxq_t *q, uint64_t *host_batches, uint64_t *host_frames) {
+    if (!q) return;
+    fcs_rxq *m = const_cast<fcs_rxq *>(q);
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (host_batches) *host_batches = m->n_host_batches;
+    if (host_frames) *host_frames = m->n_host_frames;
+}
+
 void fcs_rxq_destroy(fcs_rxq_t *q) {
     if (!q) return;
     for (RxBuf &B : q->b) {
-        finish_check(B);   // the GPU may still be writing ok[] of an in-flight batch
+        finish_check(q, B);   // the GPU may still be writing ok[] of an in-flight batch
         free_buf(B);
     }
+    for (auto &x : q->quarantine) x.second ? fcs_host_free(x.first) : std::free(x.first);
     delete q;
 }
 

@@ -56,6 +56,7 @@ def test_rx_verify_drops_corrupted_frames(max_batch):
             assert dst == OWN and src == PEER
             got.append((n, proto, pl))
         frames, bad, echoes, dropped, batches = q.stats()
+        assert q.fallbacks() == (0, 0)                          # the GPU checked every batch
     a.close(), b.close()
     assert got == good
     assert frames == len(sent) and dropped == 0
@@ -109,6 +110,7 @@ def test_rx_pipeline_with_live_sender(max_batch):
                 break
             got.append(None)
         st = q.stats()
+        assert q.fallbacks() == (0, 0)
     a.close(), b.close()
     assert got == good
     assert st[1] == len(frames) - len(good)

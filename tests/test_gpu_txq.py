@@ -69,6 +69,7 @@ def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec)
             x.join()
         q.flush()
         frames, batches, errors = q.stats()
+        assert q.fallbacks() == (0, 0)                           # every batch's FCSs came from the GPU
     rd.join(timeout=60)
     a.close(), b.close()
     assert all(r == want for rs in results for r, want in rs)   # per-call return = frame_size

@@ -1,14 +1,22 @@
-"""GPU parity of the wide LDS-DMA kernel (fcs_wide_kernel).
+"""GPU parity of the wide LDS-DMA kernel (fcs_wide_kernel<WD>).
 
-Fixed-length frames of 1537..1988 B whose four consecutive frames fit an 8 KiB slot (3 stride + len
-<= 8174, arena >= 16 KiB: fixed_wide(), fcs_launch.hpp) take this kernel: 16 lane windows of 128 B
-ending 124 c before the frame end, every live lane but the front one masking its first word, the
-front lane cf = (len - 1) / 124 masking zc = 124 cf + 128 - len leading bytes and starting from
-INV[zc], the lanes past it dropped. Every case is checked bit-exact against the oracle (the CPU
-restatement of src/ether_fcs.c:4-19): every front-lane boundary (124 c + 1 and 124 c + 4 for each
-cf, zc = 127 and 124 .. 0), the band's ends and the lengths just outside it, strides from no gap to
-the largest the slot takes, all base alignments, partial items, the arena-end slot clamp, batches
-large enough for the dynamic schedule, verify mode, and a fuzz over the band.
+Fixed-length frames of 1537..1988 B whose four consecutive frames fit one LDS slot take this kernel
+(wide_wd(), fcs_launch.hpp), at one of three window widths:
+  - WD 26: 104-B windows every 100 B (cover 1604 B), 7 KiB slots (3 stride + len <= 7150), 13 waves;
+  - WD 30: 120-B windows every 116 B (cover 1860 B), 7 KiB slots, 13 waves: 1605..1787 B at
+    stride = len (from 1788 B four frames no longer fit 7 KiB);
+  - WD 32: 128-B windows every 124 B (cover 1988 B), 8 KiB slots (3 stride + len <= 8174), 12 waves:
+    everything else in the band.
+Lane c of a frame reads the window ending step * c before the frame end; every live lane but the
+front one masks its first word (its neighbour's last), the front lane cf = (len - 1) / step masks
+its leading bytes and starts from INV[zc], the lanes past it are dropped. Every case is checked
+bit-exact against the oracle (the CPU restatement of src/ether_fcs.c:4-19): every front-lane
+boundary of each width (WD 26: 1600/1601/1604, WD 30: 1624/1625, 1740/1741, WD 32: 124 c + 1 and
+124 c + 4), the width switches (1604/1605, 1787/1788) and the band's ends with the lengths just
+outside it; strides from no gap to the largest each slot takes (3 stride + len = 7150 and 7151 for
+the 7 KiB widths, the largest stride under 8174 for the 8 KiB one); all base alignments, partial
+items, the arena-end slot clamp, batches large enough for the dynamic schedule at each width,
+verify mode, and a fuzz over the band.
 """
 import struct
 import zlib
@@ -47,13 +55,17 @@ def run(dev, d, lead, stride, L, n):
 
 # the band's ends and one byte outside; each front lane's first and last lengths (cf = 12 .. 15:
 # lengths 124 cf + 1 .. 124 cf + 124, zc = 127 .. 4); the QinQ / baby-giant sizes
-LENS = sorted({1524, 1525, 1526, 1530, 1536, 1537, 1548, 1549, 1552, 1600, 1611, 1672, 1673, 1676, 1700, 1796,
-               1797, 1800, 1860, 1861, 1864, 1900, 1920, 1949, 1950, 1984, 1985, 1987, 1988, 1989, 2000})
+LENS = sorted({1524, 1525, 1526, 1530, 1536, 1537, 1548, 1549, 1552, 1600, 1601, 1604, 1605, 1611, 1624, 1625,
+               1672, 1673, 1676, 1700, 1740, 1741, 1787, 1788, 1796, 1797, 1800, 1860, 1861, 1864, 1900, 1920,
+               1949, 1950, 1984, 1985, 1987, 1988, 1989, 2000})
 
 
 @pytest.mark.parametrize("L", LENS)
 def test_wide_lengths(dev, oracle, L):
-    for gap in (0, 1, 3, 8, (8174 - L) // 3 - L):   # the last: the largest stride a slot takes
+    gaps = [0, 1, 3, 8, (8174 - L) // 3 - L]          # the last: the largest stride an 8 KiB slot takes
+    if L <= 1860:
+        gaps.append((7150 - L) // 3 - L)               # the largest stride a 7 KiB slot takes
+    for gap in gaps:
         stride = L + gap
         for n in (1, 3, 11, 13, 257):
             host = np.random.default_rng(L * 7 + gap * 3 + n).integers(0, 256, n * stride + 16, dtype=np.uint8)
@@ -64,8 +76,9 @@ def test_wide_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(1525, 1525), (1526, 1536), (1600, 1600), (1600, 1664), (1788, 2000),
-                                      (1949, 1949), (1988, 1988), (1988, 2062)])
+@pytest.mark.parametrize("L,stride", [(1525, 1525), (1526, 1536), (1560, 1560), (1600, 1600), (1600, 1664),
+                                      (1700, 1700), (1787, 1787), (1788, 2000), (1949, 1949), (1988, 1988),
+                                      (1988, 2062)])
 def test_wide_many_items(dev, oracle, L, stride):
     """More items than the grid's waves (the dynamic schedule) and a second launch reusing the
     counter ring; the last items' slots clamped at the arena end."""
@@ -78,7 +91,22 @@ def test_wide_many_items(dev, oracle, L, stride):
         assert np.array_equal(got, exp), int(np.argmax(got != exp))
 
 
-@pytest.mark.parametrize("L", [1525, 1530, 1600, 1796, 1922, 1988])
+@pytest.mark.parametrize("L,stride", [(1552, 1866), (1553, 1866), (1702, 1816), (1703, 1816), (1600, 1850),
+                                      (1600, 1851)])
+def test_wide_seven_kib_slot_bound(dev, oracle, L, stride):
+    """3 stride + len = 7150 is the largest item a 7 KiB slot takes (WD 26 / WD 30); 7151 moves the
+    batch to the 128-B windows and 8 KiB slots. Both sides, with enough items for the dynamic
+    schedule, at two base alignments."""
+    n = (64 << 20) // stride + 5
+    host = np.random.default_rng(L * stride).integers(0, 256, n * stride + 16, dtype=np.uint8)
+    d = torch.from_numpy(host).to(dev)
+    for lead in (0, 3):
+        got = run(dev, d, lead, stride, L, n)
+        exp = oracle_fixed(oracle, host[lead:], stride, L, n)
+        assert np.array_equal(got, exp), (L, stride, lead, int(np.argmax(got != exp)))
+
+
+@pytest.mark.parametrize("L", [1525, 1530, 1560, 1600, 1700, 1787, 1796, 1922, 1988])
 def test_wide_verify_mode(dev, L):
     """RX residue check through the wide kernel: frames of L bytes carrying their FCS, a few
     corrupted; ok[] and the bad count against zlib."""

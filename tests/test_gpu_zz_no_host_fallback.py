@@ -1,7 +1,10 @@
 """Runs last in the GPU suite (file order): the product library answered every drop-in ether_fcs
 call of this session on the GPU. fcs_engine_host_fallbacks counts the calls its host CRC answered
 (only after the GPU attempt and its retry both failed, or for buffers >= 4 GiB); on a
-healthy MI355X it must be 0, which shows the HIP path served every drop-in call of the suite."""
+healthy MI355X it must be 0, which shows the HIP path served every drop-in call of the suite.
+fcs_engine_host_batches counts the TX/RX queue batches its host CRC answered after a failed GPU
+step (test_gpu_txq.py, test_gpu_rxq.py and the pcap/RX paths run through the product library);
+it must be 0 too. The fault-injection tests use the separate libnstack_fcs_faults.so."""
 import pytest
 
 import nstack_amd as na
@@ -17,3 +20,4 @@ def test_product_library_never_used_its_host_crc():
     st = na.engine_stats()
     assert st["dropin_calls"] > 0
     assert st["host_fallbacks"] == 0, st
+    assert st["host_batches"] == 0, st

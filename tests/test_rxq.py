@@ -2,7 +2,8 @@
 
 ether_receive (src/linux/ether.c:180-212): 0 when nothing is queued (:196-198), own-MAC echoes
 skipped (:202), host-order ethertype (:206), min(len - 14, bsize) payload bytes copied and len - 14
-returned (:208-211). Without a GPU the FCS-trailer mode must refuse to hand out unchecked frames.
+returned (:208-211). Without a GPU the FCS-trailer mode checks each batch with the library's host
+CRC (ether_receive never drops frames for FCS reasons), counted as a fallback.
 """
 import os
 import socket
@@ -52,12 +53,33 @@ def test_receive_semantics_without_trailer(pair):
         assert (frames, bad, echoes, dropped) == (6, 0, 1, 2) and batches >= 2
 
 
-@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")
-def test_trailer_mode_fails_loudly_without_gpu(pair):
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU path")
+def test_trailer_mode_without_gpu_host_crc_checks(pair):
+    """No GPU: the host CRC checks each batch, so the good frames still come out in
+    order, the corrupted one is dropped, and the fallback is counted."""
+    import struct
+    import zlib
     a, b = pair
-    with na.RxQueue(b.fileno(), OWN, max_batch=8, trailer=True) as q:
-        a.send(frame(PEER, 0x0800, bytes(60)) + bytes(4))
-        assert q.receive()[0] == -19                                # -ENODEV: nothing unchecked
+    good = [frame(PEER, 0x0800 + i, bytes([i]) * (46 + 100 * i)) for i in range(5)]
+    with na.RxQueue(b.fileno(), OWN, max_batch=3, trailer=True) as q:
+        for i, f in enumerate(good):
+            t = bytearray(f + struct.pack("<I", zlib.crc32(f)))
+            a.send(bytes(t))
+            if i == 2:                                               # a corrupted copy
+                t[20] ^= 4
+                a.send(bytes(t))
+        out = []
+        while True:
+            n, dst, src, proto, pl = q.receive()
+            assert n >= 0, n
+            if n == 0:
+                break
+            out.append((proto, pl))
+        frames, bad, echoes, dropped, batches = q.stats()
+        host_batches, host_frames = q.fallbacks()
+    assert out == [(0x0800 + i, bytes([i]) * (46 + 100 * i)) for i in range(5)]
+    assert (frames, bad, echoes, dropped) == (6, 1, 0, 0)
+    assert host_batches == batches and host_frames == 6
 
 
 def test_bad_arguments():

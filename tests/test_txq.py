@@ -1,12 +1,16 @@
 """Batched TX call site (include/nstack_txq.h) — host logic that needs no GPU.
 
 ether_send (src/linux/ether.c:214-272) rejects frame_size > 1518 with -EMSGSIZE before touching
-anything (:234-237); frame_size = 14 + max(bsize, 56) + 4 (:222-224). Without a GPU the queue
-must fail every frame with -ENODEV and send nothing (no unchecked FCS leaves).
+anything (:234-237); frame_size = 14 + max(bsize, 56) + 4 (:222-224), and it never fails for FCS
+reasons. Without a GPU the queue's GPU step fails, so every batch's FCSs come from the library's
+host CRC: each frame must still leave byte-identical to ether_send's (checked against
+the oracle's restatement of src/ether_fcs.c), each caller gets frame_size, and the fallback is counted.
 """
 import os
 import socket
+import struct
 import threading
+from collections import Counter
 
 import pytest
 
@@ -36,40 +40,59 @@ def test_bad_arguments():
     assert lib.fcs_txq_flush(None) == -22
 
 
-@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU error path")
-def test_no_gpu_fails_every_frame_and_sends_nothing():
+def ether_send_frame(oracle, dst, proto, payload):
+    frame_size = 14 + max(len(payload), 56) + 4                 # :222-224
+    f = dst + MAC + struct.pack(">H", proto) + payload          # :257-260
+    f += b"\0" * (frame_size - 4 - len(f))                      # :261
+    return f + struct.pack("<I", oracle.oracle_ether_fcs(f, len(f)))   # :262-263
+
+
+@pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU path")
+def test_no_gpu_host_crc_sends_every_frame(oracle):
+    """The GPU step fails (no GPU): the host CRC answers, the frames leave as ether_send builds them."""
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     b.setblocking(False)
     res = []
+    plans = [(bytes([k]) * 6, 0x0806 + k, bytes([k]) * (10 * k + (k % 3) * 500)) for k in range(10)]
     with na.TxQueue(MAC, a.fileno(), max_batch=4, flush_usec=50) as q:
-        th = [threading.Thread(target=lambda k=k: res.append(q.send(DST, 0x0806, bytes([k]) * (10 * k))))
-              for k in range(10)]
+        th = [threading.Thread(target=lambda p=p: res.append((q.send(*p), 14 + max(len(p[2]), 56) + 4)))
+              for p in plans]
         for t in th:
             t.start()
         for t in th:
             t.join()
         q.flush()
         frames, batches, errors = q.stats()
+        host_batches, host_frames = q.fallbacks()
         why = q.last_error()
-    assert res == [-19] * 10                                     # -ENODEV for every caller
-    assert why                                                   # the failing step's reason
-    assert frames == 10 and batches >= 3 and errors == 10       # batches of at most 4
+    assert all(r == want for r, want in res) and len(res) == 10   # frame_size for every caller
+    assert why                                                   # the failing GPU step's reason
+    assert frames == 10 and batches >= 3 and errors == 0        # batches of at most 4
+    assert host_batches == batches and host_frames == 10
+    assert na.engine_stats()["host_batches"] >= host_batches
+    got = [b.recv(2048) for _ in range(10)]
     with pytest.raises(BlockingIOError):
         b.recv(2048)
+    assert Counter(got) == Counter(ether_send_frame(oracle, *p) for p in plans)
     a.close(), b.close()
 
 
 @pytest.mark.timeout(120)
-@pytest.mark.skipif(_gpu_visible(), reason="checks the queue machinery on the no-GPU error path")
+@pytest.mark.skipif(_gpu_visible(), reason="checks the queue machinery on the no-GPU (host CRC) path")
 @pytest.mark.parametrize("max_batch,linger", [(1, 0), (8, 0), (64, 20), (4096, 2000)])
 def test_many_producers_no_lost_frames(max_batch, linger):
     """Lock-free slot reservation under contention: sync and fire-and-forget producers together,
     tiny and large batches, spinning and sleeping lingers. Every frame is accounted for once and
-    every sync caller gets its (here -ENODEV) result; flush() and close() return."""
+    every sync caller gets its result (frame_size, from the host CRC here); flush() and close()
+    return."""
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     res = []
     lock = threading.Lock()
     n_sync, n_async, per = 12, 4, 150
+    total = (n_sync + n_async) * per
+    received = []
+    drain = threading.Thread(target=lambda: received.extend(b.recv(2048) for _ in range(total)))
+    drain.start()   # the frames now leave (host CRC): keep the socket from filling up
     with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=linger) as q:
         def sync_worker(k):
             mine = [q.send(DST, 0x0800, bytes([k]) * (k * 37 % 1400)) for _ in range(per)]
@@ -88,8 +111,9 @@ def test_many_producers_no_lost_frames(max_batch, linger):
             t.join()
         q.flush()
         frames, batches, errors = q.stats()
-    total = (n_sync + n_async) * per
-    assert res == [-19] * (n_sync * per)
-    assert frames == total and errors == total
+    drain.join(timeout=60)
+    assert len(received) == total
+    assert sorted(res) == sorted(14 + max(k * 37 % 1400, 56) + 4 for k in range(n_sync) for _ in range(per))
+    assert frames == total and errors == 0
     assert batches >= -(-total // max_batch)
     a.close(), b.close()

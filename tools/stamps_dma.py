@@ -1,5 +1,6 @@
 #!/usr/bin/env python3
-"""Per-wave s_memtime stamps of an FCS_STAMPS build of fcs_dma_kernel (measurement tool): cycles per
+"""Per-wave s_memtime stamps of an FCS_STAMPS build of fcs_dma_kernel or fcs_segil_kernel (--len over
+1524 B, e.g. 9000; measurement tool): cycles per
 item spent waiting for the slot DMA (vmcnt at the loop top) vs. the whole item, and the in-kernel
 shader clock (s_memtime / s_memrealtime at 100 MHz, MI355X_MICROARCH.md DVFS item 6).
 
@@ -62,6 +63,15 @@ def main():
         if int(sel.sum()):
             print(f"  XCC {x}: waves {int(sel.sum())}  end median {float(en[sel].median()):.3f} ms  max {float(en[sel].max()):.3f}")
     print(f"in-kernel shader clock {clk:.3f} GHz; loop wall time per wave (s_memrealtime, 100 MHz) {rt_ms:.3f} ms")
+    # what decides the end: the spread of the waves' finishing times against the kernel's span,
+    # per XCD, and the last waves' share of items
+    span = float(en.max())
+    med = float(en.median())
+    print(f"tail: last wave ends {span - med:.3f} ms after the median wave ({100 * (span - med) / span:.2f} % of the span);"
+          f" items per wave min/median/max {int(d[:, 2].min())}/{int(d[:, 2].median())}/{int(d[:, 2].max())}")
+    per_x = [float(en[xcc == x].median()) for x in range(8) if int((xcc == x).sum())]
+    if per_x:
+        print(f"XCD median end spread {max(per_x) - min(per_x):.3f} ms ({100 * (max(per_x) - min(per_x)) / span:.2f} %)")
 
 
 if __name__ == "__main__":
