@@ -2,7 +2,10 @@
  * oracle/fcs_oracle.c — TEST INFRASTRUCTURE ONLY (the parity checker, never the product).
  *
  * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this.
- * The product library (nstack_amd/libnstack_fcs.so) contains no CPU CRC path.
+ * The product library (nstack_amd/libnstack_fcs.so) never loads or calls it. The product's own
+ * host CRC (nstack_amd/csrc/fcs_host_crc.cpp, slice-by-16 with tables derived at run time) is a
+ * separate implementation used only when a GPU step fails (the drop-in after its retry, the TX/RX
+ * queues per batch), counted, and asserted unused by the GPU suite.
  *
  * What it restates:
  *   ether_fcs()  /root/reference/src/ether_fcs.c:4-19
