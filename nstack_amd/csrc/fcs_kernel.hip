@@ -2052,7 +2052,10 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
         const uint64_t X0 = s0 & ~15ull;
-        dma_item(X0);
+#ifdef FCS_ST_LOADG
+        if (!LOAD)
+#endif
+            dma_item(X0);
         const uint64_t o0 = X0 - p.base;   // arena offset of X0
         const uint32_t last = nf - 1;
         // every frame of the unit: end (relative to X0) << 11 | length
@@ -2101,6 +2104,41 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
 #endif
             emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + g, ~reg);
         };
+#ifdef FCS_ST_LOADG
+        // measurement-only: the load pattern of lane-chunks of G x 64 B (items of G x 4 KiB, walked
+        // as G sub-items; sub-item s of item t holds bytes [256 l + 64 s, + 64) of lane l's
+        // lane-chunk, DMA rows of 16 sub-chunks at a 64 G-byte stride, trimmed at the unit's end)
+        if (LOAD) {
+            constexpr uint32_t G = FCS_ST_LOADG, kIt = kStItem * G;
+            const uint32_t nsub = G * ((E + kIt - 1) / kIt);
+            const uint64_t uend = X0 + ((E + 15u) & ~15u);
+            const uint32_t g2 = 64u * G * ((uint32_t)lane >> 2) + 16u * (((uint32_t)lane - ((uint32_t)lane >> 4)) & 3u);
+            auto dma_sub = [&](uint32_t n) {
+                typedef __attribute__((address_space(3))) void lds_void;
+                const uint64_t a = X0 + (uint64_t)kIt * (n / G) + 64u * (n % G) + g2;
+                const uint64_t a1 = a + 1024u * G, a2 = a1 + 1024u * G, a3 = a2 + 1024u * G;
+                if (a < uend) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), (lds_void *)slot, 16, 0, 0);
+                if (a1 < uend)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a1), (lds_void *)(slot + 1024), 16, 0, FCS_ST_AUX);
+                if (a2 < uend)
+                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a2), (lds_void *)(slot + 2048), 16, 0, FCS_ST_AUX);
+                if (a3 < uend) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a3), (lds_void *)(slot + 3072), 16, 0, 0);
+            };
+            dma_sub(0u);
+            for (uint32_t t = 0; t < nsub; t++) {
+                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
+#pragma unroll
+                for (int i = 0; i < 4; i++) {
+                    const u32x4 x = *pc[i];
+                    lx ^= x.x ^ x.y ^ x.z ^ x.w;
+                }
+                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
+                if (t + 1 < nsub) dma_sub(t + 1);
+            }
+            wave_lds_sync();
+            continue;
+        }
+#endif
         if (LOAD) {   // the item walk alone: slot wait, word reads, next DMA
             for (uint32_t t = 0; t < nitems; t++) {
                 const uint32_t Xr = kStItem * t;

@@ -21,8 +21,9 @@ def main():
     ap.add_argument("--len", type=int, default=1518)
     ap.add_argument("--rounds", type=int, default=6)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--what", default="fcs", help="comma list of fcs,stream,dma,inet (stream: plain read stream; dma: the LDS-DMA "
-                         "kernel's loads without the CRC work; inet: ip_checksum, fixed)")
+    ap.add_argument("--what", default="fcs", help="comma list of fcs,stream,dma,stload,inet (stream: plain read "
+                         "stream; dma: the LDS-DMA kernel's loads without the CRC work; stload (--imix): the "
+                         "arena-stream kernel's loads and schedule without its CRC work; inet: ip_checksum, fixed)")
     ap.add_argument("--mix", default="64,576,1518:7,4,1",
                     help="with --imix: lengths:weights of the variable-length mix")
     ap.add_argument("--imix", action="store_true",
@@ -41,6 +42,8 @@ def main():
                                             ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p]
         lib.fcs_read_stream_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         lib.fcs_dma_stream_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+        lib.fcs_stream_load_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         lib.inet_csum_fixed_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.inet_csum_batch_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -76,6 +79,9 @@ def main():
             return lib.fcs_read_stream_dev(arena.data_ptr(), total, sink.data_ptr(), st.cuda_stream)
         if w == "dma":
             return lib.fcs_dma_stream_dev(arena.data_ptr(), total, sink.data_ptr(), st.cuda_stream)
+        if w == "stload":   # the arena-stream kernel's loads and schedule without its CRC work (--imix)
+            return lib.fcs_stream_load_dev(arena.data_ptr(), total, off.data_ptr(), ln.data_ptr(), n,
+                                           sink.data_ptr(), st.cuda_stream)
         if w == "inet" and a.imix:
             return lib.inet_csum_batch_dev(0, arena.data_ptr(), total, off.data_ptr(), ln.data_ptr(), None,
                                            outs[i].data_ptr(), n, st.cuda_stream)
@@ -101,7 +107,7 @@ def main():
                     times[(w, i)].append(e0.elapsed_time(e1) / a.reps)
         for i, p in enumerate(a.libs):
             med, mn = statistics.median(times[(w, i)]), min(times[(w, i)])
-            same = bool(torch.equal(outs[i], outs[0])) if w not in ("stream", "dma") else None
+            same = bool(torch.equal(outs[i], outs[0])) if w not in ("stream", "dma", "stload") else None
             print(f"{w:6s} {os.path.basename(p):28s} median {med:8.3f} ms  min {mn:8.3f} ms  "
                   f"{total / med / 1e6:8.1f} GB/s  same_as_first={same}", flush=True)
 

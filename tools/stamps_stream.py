@@ -60,6 +60,10 @@ def main():
         print(f"  {names[i]}: {float(d[:, i].sum()) / items:.0f}")
     acc = float(d[:, :5].sum())
     print(f"  unaccounted (unit closes, dispenser): {(tot - acc) / items:.0f}")
+    # every wave runs from about the kernel's start to its end, so a wave's whole s_memtime count
+    # over the launch time is the in-kernel shader clock (an upper bound on the wave's span)
+    print(f"in-kernel shader clock ~{float(d[:, 7].median()) / (ms * 1e-3) / 1e9:.3f} GHz "
+          f"(median wave cycles {float(d[:, 7].median()):.0f} over {ms:.3f} ms)")
 
 
 if __name__ == "__main__":
