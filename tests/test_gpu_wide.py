@@ -63,9 +63,10 @@ LENS = sorted({1524, 1525, 1526, 1530, 1536, 1537, 1548, 1549, 1552, 1600, 1601,
 @pytest.mark.parametrize("L", LENS)
 def test_wide_lengths(dev, oracle, L):
     gaps = [0, 1, 3, 8, (8174 - L) // 3 - L]          # the last: the largest stride an 8 KiB slot takes
-    if L <= 1860:
-        gaps.append((7150 - L) // 3 - L)               # the largest stride a 7 KiB slot takes
-    for gap in gaps:
+    s7 = (7150 - L) // 3                               # the largest stride a 7 KiB slot takes ...
+    if s7 >= L:                                        # ... (up to 1787 B; from 1788 B none does)
+        gaps += [s7 - L, s7 + 1 - L]                   # 3 stride + len <= 7150, and the first stride past it
+    for gap in sorted(set(g for g in gaps if g >= 0)):
         stride = L + gap
         for n in (1, 3, 11, 13, 257):
             host = np.random.default_rng(L * 7 + gap * 3 + n).integers(0, 256, n * stride + 16, dtype=np.uint8)
