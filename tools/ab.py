@@ -43,7 +43,7 @@ def main():
         lib.fcs_read_stream_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         lib.fcs_dma_stream_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         lib.fcs_stream_load_dev.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
-                                            ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+                                            ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
         lib.inet_csum_fixed_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                             ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         lib.inet_csum_batch_dev.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p,
@@ -71,7 +71,7 @@ def main():
     outs = [torch.zeros(n, dtype=torch.int32, device=dev) for _ in libs]
     sink = torch.zeros(4, dtype=torch.int32, device=dev)
     st = torch.cuda.current_stream()
-    whats = a.what.split(",")
+    whats = a.what.replace("+", ",").split(",")   # "+" too: tools/gpu_run.sh turns commas into spaces
     times = {(w, i): [] for w in whats for i in range(len(libs))}
 
     def launch(w, i, lib):
