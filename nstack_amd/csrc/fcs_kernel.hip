@@ -2063,10 +2063,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
         const uint64_t X0 = s0 & ~15ull;
-#ifdef FCS_ST_LOADG
-        if (!LOAD)
-#endif
-            dma_item(X0);
+        dma_item(X0);
         const uint64_t o0 = X0 - p.base;   // arena offset of X0
         const uint32_t last = nf - 1;
         // every frame of the unit: end (relative to X0) << 11 | length
@@ -2115,41 +2112,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
 #endif
             emit<kStBad>(p, lds, (uint32_t)lane < cnt, f0 + g, ~reg);
         };
-#ifdef FCS_ST_LOADG
-        // measurement-only: the load pattern of lane-chunks of G x 64 B (items of G x 4 KiB, walked
-        // as G sub-items; sub-item s of item t holds bytes [256 l + 64 s, + 64) of lane l's
-        // lane-chunk, DMA rows of 16 sub-chunks at a 64 G-byte stride, trimmed at the unit's end)
-        if (LOAD) {
-            constexpr uint32_t G = FCS_ST_LOADG, kIt = kStItem * G;
-            const uint32_t nsub = G * ((E + kIt - 1) / kIt);
-            const uint64_t uend = X0 + ((E + 15u) & ~15u);
-            const uint32_t g2 = 64u * G * ((uint32_t)lane >> 2) + 16u * (((uint32_t)lane - ((uint32_t)lane >> 4)) & 3u);
-            auto dma_sub = [&](uint32_t n) {
-                typedef __attribute__((address_space(3))) void lds_void;
-                const uint64_t a = X0 + (uint64_t)kIt * (n / G) + 64u * (n % G) + g2;
-                const uint64_t a1 = a + 1024u * G, a2 = a1 + 1024u * G, a3 = a2 + 1024u * G;
-                if (a < uend) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), (lds_void *)slot, 16, 0, 0);
-                if (a1 < uend)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a1), (lds_void *)(slot + 1024), 16, 0, FCS_ST_AUX);
-                if (a2 < uend)
-                    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a2), (lds_void *)(slot + 2048), 16, 0, FCS_ST_AUX);
-                if (a3 < uend) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a3), (lds_void *)(slot + 3072), 16, 0, 0);
-            };
-            dma_sub(0u);
-            for (uint32_t t = 0; t < nsub; t++) {
-                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const u32x4 x = *pc[i];
-                    lx ^= x.x ^ x.y ^ x.z ^ x.w;
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-                if (t + 1 < nsub) dma_sub(t + 1);
-            }
-            wave_lds_sync();
-            continue;
-        }
-#endif
         if (LOAD) {   // the item walk alone: slot wait, word reads, next DMA
             for (uint32_t t = 0; t < nitems; t++) {
                 const uint32_t Xr = kStItem * t;
@@ -2315,297 +2277,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         return;
     }
     flush_bad<kStBad>(p, lds);
-}
-
-// ---------------------------------------------------------------------------------------------
-// Variable-length frames, lane-chunk carry stream (fcs_lcs_kernel, round 4; launched in place of
-// fcs_stream_kernel when built with FCS_LCS). The same units, packed check and hand-off of the
-// other units to fcs_flat_kernel; a different walk (CPU model and its algebra against zlib:
-// tests/lcs_model.py, tests/test_lcs_model.py):
-// - Lane l of item t owns the lane-chunk [X0 + kLcChunk (64 t + l), + kLcChunk): kLcG sub-chunks
-//   of 64 B. Sub-item s of an item is one 4 KiB LDS-DMA of every lane's sub-chunk s (rows of 16
-//   lane-chunks, four lanes per 64-B sub-chunk), into the wave's slot, trimmed at the unit's end.
-// - The lane's chain runs over its whole lane-chunk from register 0 and is RESET at a frame
-//   boundary (word k, byte r of a sub-chunk; at most one per sub-chunk, frames >= 64 B): before
-//   word k it saves its state, the frame ending there gets its end tap T = A_4(s_k ^ (w_k & the
-//   bytes before the boundary)) (ring tap[f]), and the chain goes on from INV_r ^ (w_k & the bytes
-//   from the boundary on), INV_r = A_{-r}(~0), as if the next frame had started from ~0: one
-//   compare and two selects per word instead of a start tap and a chunk shift per 64 B.
-// - So after its lane-chunk a lane holds the register of its tail frame (the frame holding the
-//   lane-chunk's last byte): the whole frame so far if it started in this lane-chunk, else this
-//   lane-chunk's bytes from 0. It goes to that frame shifted by whole lane-chunks to the lane-chunk
-//   holding the frame's end, A_{kLcChunk j} (j <= 11 at 128-B lane-chunks): one data-dependent
-//   shift per kLcChunk bytes. A wave XOR scan sums each frame's run of lanes into acc[f].
-// - Close (64 frames per pass, a frame per lane), the end at sub-chunk s_e, word k_e, byte r_e of
-//   its lane-chunk: R(~0, frame) = A_{-(4 - r_e)}(A_{64 s_e}(A_{4 (k_e + 1)}(acc)) ^ T_e), T_e = 0
-//   when the frame ends on a lane-chunk edge (no tap there belongs to it).
-// Boundaries come from the frames' starts (and the unit's end) as marks (starting frame + 1) << 6 |
-// byte, per sub-chunk and lane. LDS (160 KiB): the 64 KiB table image (slice tables; in the
-// holes A_{kLcChunk j}, A_{4 i}, A_{64 s}, A_{-d}, INV_r, the verify counters and the marks), 16
-// slots of 4 KiB, per wave acc and tap rings of kLcRing frames.
-// ---------------------------------------------------------------------------------------------
-constexpr uint32_t kLcItem = 64 * kLcChunk;
-constexpr uint32_t kLcRing = 256;   // frames per wave ring
-// live ring entries: the frame open at an item's start, the frames starting in the item, and up to
-// 63 already ended ones of the batch not yet closed
-static_assert(kLcItem / kStMinLen + 1 + 63 <= kLcRing, "ring");
-constexpr uint32_t kLcTabs = kLcChunkTabs + kStWordTabs + kLcG + kStInvTabs;
-constexpr uint32_t kLcHoleChunk = 0;                                  // A_{kLcChunk j}: 4 holes each
-constexpr uint32_t kLcHoleWord = kLcHoleChunk + 4 * kLcChunkTabs;    // A_{4 i}, i = 0..16
-constexpr uint32_t kLcHoleSub = kLcHoleWord + 4 * kStWordTabs;       // A_{64 s}, s = 0..kLcG-1
-constexpr uint32_t kLcHoleInv = kLcHoleSub + 4 * kLcG;               // A_{-d}, d = 1..4
-constexpr uint32_t kLcHoleK = kLcHoleInv + 4 * kStInvTabs;           // INV_r, r = 0..3
-constexpr uint32_t kLcBad = dma_hole(kLcHoleK + 1);                   // 16 x 8 B
-constexpr uint32_t kLcHoleMark = kLcHoleK + 2;                        // 2 kLcG holes per wave
-static_assert(kLcHoleMark + 16 * 2 * kLcG <= 256, "holes");
-constexpr uint32_t kLcSlots = 65536;
-constexpr uint32_t kLcRings = kLcSlots + 16 * 4096;
-constexpr uint32_t kLcLdsBytes = kLcRings + 16 * 2 * 4 * kLcRing;
-static_assert(kLcLdsBytes <= 163840, "LDS per CU");
-
-__device__ __forceinline__ void stage_lcs_tables(const KParams &p, uint8_t *lds, int tid) {
-    for (int i = tid; i < 2048; i += kWgThreads) {   // slice tables as fcs_dma_kernel
-        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
-        u32x4 vv = {v, v, v, v};
-        *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
-    }
-    for (int i = tid; i < (int)kLcTabs * 128; i += kWgThreads) {   // nibble tables, hole_shift's layout
-        const uint32_t q = (uint32_t)i >> 7, t = ((uint32_t)i >> 4) & 7u, e = (uint32_t)i & 15u;
-        uint32_t src;
-        if (q < kLcChunkTabs) src = kBlobLcs + q * 128u;                                        // A_{kLcChunk j}
-        else if (q < kLcChunkTabs + kStWordTabs) src = kBlobStream + (kStChunkTabs + q - kLcChunkTabs) * 128u;   // A_{4 i}
-        else if (q < kLcChunkTabs + kStWordTabs + kLcG) src = kBlobStream + (q - kLcChunkTabs - kStWordTabs) * 128u;   // A_{64 s}
-        else src = kBlobStream + (kStChunkTabs + kStWordTabs + q - kLcChunkTabs - kStWordTabs - kLcG) * 128u;      // A_{-d}
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(4u * q + (t >> 1)) + 64u * ((t + (q & kStSkew)) & 1u) + 4u * e) =
-            p.blob[src + ((uint32_t)i & 127u)];
-    }
-    for (int i = tid; i < 4; i += kWgThreads)
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kLcHoleK) + 4u * (uint32_t)i) = p.blob[kBlobInvWide + i];
-    for (int i = tid; i < (int)(16 * 2 * kLcG * 32); i += kWgThreads)   // marks: empty
-        *reinterpret_cast<uint32_t *>(lds + dma_hole(kLcHoleMark + (uint32_t)i / 32u) + ((uint32_t)i % 32u) * 4u) = 0u;
-    for (int i = tid; i < (int)(16 * 2 * kLcRing); i += kWgThreads) reinterpret_cast<uint32_t *>(lds + kLcRings)[i] = 0u;
-}
-
-// LOAD: the measurement form behind fcs_stream_load_dev in FCS_LCS builds (the same units, unit
-// check, sub-item DMA and schedule; each lane only XORs its words).
-template <bool LOAD>
-__global__ __launch_bounds__(kWgThreads, 1) void fcs_lcs_kernel(KParams p) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kLcLdsBytes];
-    const int tid = threadIdx.x;
-    stage_lcs_tables(p, lds, tid);
-    init_bad<kLcBad>(lds);
-    __syncthreads();
-
-    const int lane = tid & 63;
-    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
-    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
-    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
-    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
-                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
-    uint8_t *slot = lds + kLcSlots + wave * 4096u;
-    uint32_t *acc = reinterpret_cast<uint32_t *>(lds + kLcRings + wave * 8u * kLcRing);   // per frame (mod kLcRing)
-    uint32_t *tap = acc + kLcRing;                                                        // end tap per frame
-    // mark of sub-chunk s of lane l's lane-chunk (bank l mod 32: a sub-item's reads are conflict free)
-    auto mark_at = [&](uint32_t s, uint32_t l) {
-        return reinterpret_cast<uint32_t *>(lds + dma_hole(kLcHoleMark + 2u * kLcG * wave + 2u * s + (l >> 5)) + 4u * (l & 31u));
-    };
-    // the lane's sub-chunk in the slot: piece m at 64 lane + 16 ((m + lane / 4) mod 4) (conflict-free reads)
-    const uint32_t cbase = 64u * (uint32_t)lane, sw = ((uint32_t)lane >> 2) & 3u;
-    const u32x4 *pc[4] = {reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((0u + sw) & 3u)),
-                          reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((1u + sw) & 3u)),
-                          reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((2u + sw) & 3u)),
-                          reinterpret_cast<const u32x4 *>(slot + cbase + 16u * ((3u + sw) & 3u))};
-    // sub-item DMA: row q, lane i moves the 16-B piece (i - i / 16) mod 4 of sub-chunk s of the
-    // item's lane-chunk 16 q + i / 4 to slot byte 1024 q + 16 i
-    const uint32_t g2 = kLcChunk * ((uint32_t)lane >> 2) + 16u * (((uint32_t)lane - ((uint32_t)lane >> 4)) & 3u);
-    constexpr int kQ = (int)(kStUnitFrames / 64);
-    constexpr uint32_t kLenMask = (1u << kStLenBits) - 1u;
-    constexpr uint64_t kEnd = Dispenser::kEnd;
-    const uint64_t units = (p.n + kStUnitFrames - 1) / kStUnitFrames;
-    Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kStWaves, (uint64_t)blockIdx.x * kStWaves + wave, lane, 100, 1, 8);
-    uint32_t lx = 0;   // LOAD only: the XOR of every word this lane read
-    for (uint64_t u = D.first(); u != kEnd; u = D.next(u)) {
-        const uint64_t f0 = u * kStUnitFrames;
-        const uint32_t nf = (uint32_t)((p.n - f0) < kStUnitFrames ? (p.n - f0) : kStUnitFrames);
-        uint64_t S[kQ];
-        uint32_t Ln[kQ];
-        if (__any(unit_unpacked(p, f0, nf, lane, S, Ln))) {
-            if (!LOAD && lane == 0) p.ulist[atomicAdd(p.ucount, 1u)] = (uint32_t)u;
-            continue;
-        }
-        // ---- geometry, relative to X0 (the 16-B boundary at or below the first frame) ----
-        const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
-                                      (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
-        const uint64_t X0 = s0 & ~15ull;
-        const uint64_t o0 = X0 - p.base;
-        const uint32_t last = nf - 1;
-        uint32_t pk[kQ];   // every frame of the unit: end (relative to X0) << 11 | length
-#pragma unroll
-        for (int q = 0; q < kQ; q++) pk[q] = ((uint32_t)(S[q] + Ln[q] - o0) << kStLenBits) | Ln[q];
-        uint32_t E = 0;    // the unit's end
-#pragma unroll
-        for (int q = 0; q < kQ; q++)
-            if ((last >> 6) == (uint32_t)q) E = (uint32_t)__builtin_amdgcn_readlane((int)pk[q], (int)(last & 63u)) >> kStLenBits;
-        const uint64_t uend = X0 + ((E + 15u) & ~15u);
-        const uint32_t nitems = (E + kLcItem - 1) / kLcItem, nsub = kLcG * nitems;
-        auto dma_sub = [&](uint32_t n) {   // sub-item n = kLcG t + s of the unit
-            typedef __attribute__((address_space(3))) void lds_void;
-            const uint64_t a0 = X0 + (uint64_t)kLcItem * (n / kLcG) + 64u * (n % kLcG) + g2;
-            const uint64_t a1 = a0 + 16u * kLcChunk, a2 = a1 + 16u * kLcChunk, a3 = a2 + 16u * kLcChunk;
-            if (a0 < uend) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a0), (lds_void *)slot, 16, 0, 0);
-            if (a1 < uend)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a1), (lds_void *)(slot + 1024), 16, 0, FCS_ST_AUX);
-            if (a2 < uend)
-                __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a2), (lds_void *)(slot + 2048), 16, 0, FCS_ST_AUX);
-            if (a3 < uend) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a3), (lds_void *)(slot + 3072), 16, 0, 0);
-        };
-        dma_sub(0u);
-        if (LOAD) {   // the sub-item walk alone: slot wait, word reads, next DMA
-            for (uint32_t n = 0; n < nsub; n++) {
-                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const u32x4 x = *pc[i];
-                    lx ^= x.x ^ x.y ^ x.z ^ x.w;
-                }
-                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0)
-                if (n + 1 < nsub) dma_sub(n + 1);
-            }
-            wave_lds_sync();
-            continue;
-        }
-        // batches cb + q of the unit's frames sit in pk[q] (shifted down as batches close: no indexed
-        // register access)
-        uint32_t cb = 0, closed = 0;
-        uint32_t open = 0;   // the frame holding the byte before the current item (nf: none)
-        // close frames 64 b .. 64 b + cnt - 1 (all ended; pw: their end << 11 | length)
-        auto close_pass = [&](uint32_t b, uint32_t cnt, uint32_t pw) {
-            wave_lds_sync();
-            const uint32_t g = 64u * b + (uint32_t)lane;
-            const uint32_t within = (pw >> kStLenBits) & (kLcChunk - 1u);
-            const uint32_t se = within >> 6, ke = (within >> 2) & 15u, re = within & 3u;
-            const uint32_t T = within ? tap[g % kLcRing] : 0u;
-            const uint32_t a0 = acc[g % kLcRing];
-            wave_lds_sync();
-            acc[g % kLcRing] = 0u;
-            const uint32_t U = hole_shift(lds, a0, kLcHoleWord + 4u * (ke + 1u), 0u);
-            const uint32_t V = hole_shift(lds, U, kLcHoleSub + 4u * se, T);
-            const uint32_t R = hole_shift(lds, V, kLcHoleInv + 4u * (3u - re), 0u);
-            emit<kLcBad>(p, lds, (uint32_t)lane < cnt, f0 + g, ~R);
-        };
-        for (uint32_t t = 0; t < nitems; t++) {
-            const uint32_t Xr = kLcItem * t;
-            // ---- marks: every frame starting in this item (the frame before it ends there), and the
-            // unit's end ----
-            wave_lds_sync();
-#pragma unroll
-            for (int q = 0; q < kQ; q++) {
-                const uint32_t g = 64u * (cb + (uint32_t)q) + (uint32_t)lane;
-                const uint32_t st = (pk[q] >> kStLenBits) - (pk[q] & kLenMask);
-                if (g < nf && st >= Xr && st < Xr + kLcItem) {
-                    const uint32_t d = st - Xr;
-                    *mark_at((d >> 6) % kLcG, (d >> 6) / kLcG) = ((g + 1u) << 6) | (d & 63u);
-                }
-            }
-            if (lane == 0 && E >= Xr && E < Xr + kLcItem) {
-                const uint32_t d = E - Xr;
-                *mark_at((d >> 6) % kLcG, (d >> 6) / kLcG) = ((nf + 1u) << 6) | (d & 63u);
-            }
-            wave_lds_sync();
-            // ---- the lane-chunk, sub-item by sub-item: chain with resets, end taps ----
-            uint32_t x = 0, lastm = 0;   // chain state; the mark of the lane-chunk's last boundary
-#pragma unroll
-            for (uint32_t s = 0; s < kLcG; s++) {
-                const uint32_t n = kLcG * t + s;
-                uint32_t *mp = mark_at(s, (uint32_t)lane);
-                const uint32_t m = *mp;
-                const bool bnd = m >= 64u;
-                const uint32_t sig = m & 63u, r = sig & 3u;
-                const uint32_t k = bnd ? sig >> 2 : 16u;   // 16: no boundary, no word matches
-                const uint32_t hm = 0xFFFFFFFFu << (8u * r);   // the bytes from the boundary on
-                const uint32_t inv = lds_rd(lds, dma_hole(kLcHoleK) + 4u * r);
-                __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this sub-item has landed
-                uint32_t w[16];
-#pragma unroll
-                for (int i = 0; i < 4; i++) {
-                    const u32x4 v4 = *pc[i];
-                    w[4 * i] = v4.x;
-                    w[4 * i + 1] = v4.y;
-                    w[4 * i + 2] = v4.z;
-                    w[4 * i + 3] = v4.w;
-                }
-                // the boundary word: word k & 3 of piece (k & 15) / 4
-                const uint32_t wk = lds_rd(slot, cbase + 16u * ((((k & 15u) >> 2) + sw) & 3u) + 4u * (k & 3u));
-                __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
-                if (n + 1 < nsub) dma_sub(n + 1);
-                if (bnd) *mp = 0;
-                // x holds (state ^ word) before each step; at word k: save it, restart as the next
-                // frame from ~0 (INV_r before the word's bytes from the boundary on)
-                const uint32_t restart = inv ^ (wk & hm);
-                uint32_t xs = x ^ w[0], save = 0u;
-#pragma unroll
-                for (int i = 0; i < 16; i++) {
-                    if ((uint32_t)i == k) {
-                        save = xs;
-                        xs = restart;
-                    }
-                    xs = step4_l8(lds, xs, i < 15 ? w[i + 1] : 0u, B, SEL);
-                }
-                x = xs;
-                // the end tap of the frame ending at the boundary: s_k ^ (w_k & bytes before it)
-                const uint32_t T = step4_l8(lds, save ^ (wk & hm), 0u, B, SEL);
-                if (bnd) {
-                    tap[((m >> 6) - 2u) % kLcRing] = T;   // ending frame = starting frame - 1 (-1: the unit's start)
-                    lastm = m;
-                }
-            }
-            // ---- the lane-chunk's register goes to its tail frame, at the lane-chunk of its end ----
-            const uint64_t Mb = __ballot(lastm != 0u);
-            const uint32_t gs = (lastm >> 6) - 1u;                       // the frame starting at the last boundary
-            const uint64_t upto = Mb & ((2ull << lane) - 1ull);          // boundary lanes at or before this one
-            const int sl = upto ? 63 - __builtin_clzll(upto) : -1;
-            const uint32_t ot = (uint32_t)__shfl((int)gs, sl >= 0 ? sl : 0);
-            const uint32_t o = sl >= 0 ? ot : open;                      // this lane's tail frame (nf: none)
-            const uint32_t olast = Mb ? (uint32_t)__builtin_amdgcn_readlane((int)gs, 63 - __builtin_clzll(Mb)) : open;
-            uint32_t ef = 0;   // the end of the frame open past this item
-#pragma unroll
-            for (int q = 0; q < kQ; q++)
-                if ((olast >> 6) == cb + (uint32_t)q)
-                    ef = (uint32_t)__builtin_amdgcn_readlane((int)pk[q], (int)(olast & 63u)) >> kStLenBits;
-            const uint32_t le_far = olast < nf ? (ef - Xr) / kLcChunk : 64u;
-            const uint64_t after = lane == 63 ? 0ull : (Mb & (~0ull << (lane + 1)));
-            const uint32_t le = after ? (uint32_t)__builtin_ctzll(after) : le_far;
-            const bool contrib = o < nf && Xr + kLcChunk * ((uint32_t)lane + 1u) <= E;
-            const uint32_t j = contrib ? le - (uint32_t)lane - 1u : 0u;
-            const uint32_t W = hole_shift(lds, x, kLcHoleChunk + 4u * j, 0u);
-            const uint32_t P = wave_xor_scan(contrib ? W : 0u);
-            // the run of this lane's tail frame starts at lane sl (or lane 0): its sum is P here minus
-            // P just before the run
-            const uint32_t Pb = (uint32_t)__shfl((int)P, sl > 0 ? sl - 1 : 0);
-            const uint32_t v = P ^ (sl > 0 ? Pb : 0u);
-            const bool seg_end = lane == 63 || ((Mb >> (lane + 1)) & 1ull);
-            if (contrib && seg_end && v) {
-                uint32_t *ap = &acc[o % kLcRing];
-                *ap = *ap ^ v;
-            }
-            open = olast;
-            // ---- every batch all of whose frames have ended (those before the open one) closes ----
-            while (olast >= 64u * (cb + 1u)) {
-                close_pass(cb, 64u, pk[0]);
-                closed = 64u * (cb + 1u);
-                cb++;
-#pragma unroll
-                for (int q = 0; q + 1 < kQ; q++) pk[q] = pk[q + 1];
-            }
-        }
-        if (closed < nf) close_pass(cb, nf - closed, pk[0]);
-        wave_lds_sync();
-    }
-    if (LOAD) {   // keep the word reads live: a store no realistic input triggers
-        if (lx == 0x5EEDF00Du && p.out) p.out[0] = lx;
-        return;
-    }
-    flush_bad<kLcBad>(p, lds);
 }
 
 // Counter-based byte generator: 8-byte word q of the stream = splitmix64(seed + q).
@@ -2954,13 +2625,6 @@ hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st) {
 
 hipError_t launch_stream(const KParams &p, int grid, hipStream_t st, bool load_only) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
-#ifdef FCS_LCS
-    if (load_only)
-        hipLaunchKernelGGL(fcs_lcs_kernel<true>, dim3(grid), dim3(kWgThreads), 0, st, p);
-    else
-        hipLaunchKernelGGL(fcs_lcs_kernel<false>, dim3(grid), dim3(kWgThreads), 0, st, p);
-    return hipGetLastError();
-#endif
     if (load_only)
         hipLaunchKernelGGL(fcs_stream_kernel<true>, dim3(grid), dim3(kWgThreads), 0, st, p);
     else

@@ -21,8 +21,7 @@
 //   chunk shifts  C_c = A_{96 c}         c = 0..15   (flat variable-length kernel: a lane's
 //                                                     chunk index is data-dependent, so the
 //                                                     table is indexed by c, not by lane)
-//   (and the LDS-DMA, arena-stream, lane-chunk and wide kernels' tables, listed at their blob
-//   offsets below)
+//   (and the LDS-DMA, arena-stream and wide kernels' tables, listed at their blob offsets below)
 // These are constants of the algorithm, computed once per process. (Frame bytes are checksummed
 // on the host only by fcs_host_crc.cpp, the error path's slice-by-16, not from these tables.)
 #pragma once
@@ -119,18 +118,7 @@ constexpr uint32_t kBlobLaneWide = kBlobStreamK1 + 64;
 constexpr uint32_t kBlobLaneWide26 = kBlobLaneWide + 8 * 16 * 32;
 constexpr uint32_t kBlobLaneWide30 = kBlobLaneWide26 + 8 * 16 * 32;   // A_{116 c} (WD 30)
 constexpr uint32_t kBlobInvWide = kBlobLaneWide30 + 8 * 16 * 32;
-// Lane-chunk carry kernel (fcs_lcs_kernel): lane-chunk shifts A_{64 G j}, nibble tables [8][16], for
-// j up to the most whole lane-chunks between a lane-chunk of a <= 1536-B frame and the one holding
-// its end (its word, sub-chunk and inverse shifts are the arena-stream tables above; INV_r is
-// kBlobInvWide[r]).
-#ifndef FCS_LC_G   // sub-chunks of 64 B per lane-chunk (measurement override)
-#define FCS_LC_G 2
-#endif
-constexpr uint32_t kLcG = FCS_LC_G;
-constexpr uint32_t kLcChunk = 64 * kLcG;                 // lane-chunk bytes
-constexpr int kLcChunkTabs = (int)((kLcChunk + 1535) / kLcChunk);   // 12 at 128-B lane-chunks
-constexpr uint32_t kBlobLcs = kBlobInvWide + kWideWin;
-constexpr uint32_t kBlobWords = kBlobLcs + kLcChunkTabs * 128;
+constexpr uint32_t kBlobWords = kBlobInvWide + kWideWin;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -234,11 +222,6 @@ struct Tables {
                 for (int e = 0; e < 16; e++) b[kBlobLaneWide30 + (t * 16 + e) * 32 + slot] = nt[t][e];
         }
         for (int z = 0; z < (int)kWideWin; z++) b[kBlobInvWide + z] = shift(0xFFFFFFFFu, -(long)z);
-        for (int j = 0; j < kLcChunkTabs; j++) {   // lane-chunk carry kernel: A_{64 G j}
-            nibble_table((long)kLcChunk * j, nt);
-            for (int t = 0; t < 8; t++)
-                for (int e = 0; e < 16; e++) b[kBlobLcs + j * 128 + t * 16 + e] = nt[t][e];
-        }
         return b;
     }
     // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.
