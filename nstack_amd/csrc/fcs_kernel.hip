@@ -2047,6 +2047,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
 #endif
     Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kStWaves, (uint64_t)blockIdx.x * kStWaves + wave, lane, 100, 1, 8);
     uint32_t lx = 0;   // LOAD only: the XOR of every word this lane read
+#if defined(FCS_ST_PROBE_LDS) || defined(FCS_ST_PROBE_VALU)
+    uint32_t probe = 0;   // measurement-only sensitivity probes (kept live below)
+#endif
     for (uint64_t u = D.first(); u != kEnd; u = D.next(u)) {
         ST_T(tu0)
         const uint64_t f0 = u * kStUnitFrames;
@@ -2223,8 +2226,19 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             // ---- chunk contributions: the lane ending a frame's run of lanes adds the run's sum ----
 #ifdef FCS_ST_ABL_NOSHIFT   // measurement-only: no chunk shift (wrong FCS)
             const uint32_t Wc = x ^ j;
+#elif defined(FCS_ST_SKIPJ0)   // measurement-only: lanes with j = 0 (A_0 = identity) skip the lookups
+            uint32_t Wc = x;
+            if (j) Wc = hole_shift(lds, x, kStHoleChunk + 4u * j, 0u);
 #else
             const uint32_t Wc = hole_shift(lds, x, kStHoleChunk + 4u * j, 0u);
+#endif
+#ifdef FCS_ST_PROBE_LDS   // measurement-only: N extra conflict-free LDS reads per item, off the critical path
+#pragma unroll
+            for (int i = 0; i < FCS_ST_PROBE_LDS; i++) probe ^= lds_rd(lds, ((uint32_t)lane & 31u) * 4u + (uint32_t)i * 256u);
+#endif
+#ifdef FCS_ST_PROBE_VALU   // measurement-only: N extra VALU operations per item, off the critical path
+#pragma unroll
+            for (int i = 0; i < FCS_ST_PROBE_VALU; i++) probe = xor3(probe, w[i & 15], (uint32_t)i) + (uint32_t)i;
 #endif
             const uint32_t P = wave_xor_scan(contrib ? Wc : 0u);
             // the run of this lane's frame starts at the last start at or before it (if any); its sum
@@ -2276,6 +2290,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         if (lx == 0x5EEDF00Du && p.out) p.out[0] = lx;
         return;
     }
+#if defined(FCS_ST_PROBE_LDS) || defined(FCS_ST_PROBE_VALU)
+    if (probe == 0x5EEDF00Du && p.out) p.out[0] = probe;
+#endif
     flush_bad<kStBad>(p, lds);
 }
 
