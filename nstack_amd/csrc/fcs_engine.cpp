@@ -440,7 +440,8 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
     p.dbg = g_dbg;
-    if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed)) {
+    if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed) &&
+        !(!fcs::fixed_tiny(p) && fcs::fixed_wide(p))) {   // (the mid-length wide kernels go first)
         // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame
         // instead of a 16-lane quarter-wave (len == null tells it the length is p.flen)
         p.zmax = fcs::kChunkBytes;

@@ -1149,17 +1149,24 @@ constexpr uint32_t kWideBad = dma_hole(kWideInvHole + 4);
 __host__ __device__ constexpr uint32_t wide_lds_bytes(int wd) {
     return kDmaRing + (uint32_t)(wide_threads(wd) / 64) * wide_slot(wd);
 }
-static_assert(wide_lds_bytes(32) <= 163840 && wide_lds_bytes(26) <= 163840, "LDS per CU");
+static_assert(wide_lds_bytes(32) <= 163840 && wide_lds_bytes(26) <= 163840 && wide_lds_bytes(kWideMidMax) <= 163840,
+              "LDS per CU");
 static_assert(kDmaMergeHole == kWideMergeHole, "merge_shift_dma reads merge table 0 at the same holes");
 // chain split: chain 0 = words [0, CL0), chain 1 = [CL0, WD); chain 1 spans 4 (WD - CL0) bytes, a
-// multiple of 8 so that its merge A_{4 (WD - CL0)} is one of the blob's A_{8 k}
-__host__ __device__ constexpr int wide_cl0(int wd) { return wd == 32 ? 16 : (wd == 30 ? 14 : 12); }
+// multiple of 8 so that its merge A_{4 (WD - CL0)} is one of the blob's A_{8 k} (k <= 11)
+__host__ __device__ constexpr int wide_cl0(int wd) {
+    return wd == 32 ? 16 : (wd == 30 ? 14 : (wd == 26 ? 12 : wd - 2 * (wd / 4)));
+}
 
 template <int WD>
 __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds, int tid) {
     constexpr int NT = wide_threads(WD);
-    constexpr uint32_t kLane = WD == 32 ? kBlobLaneWide : (WD == 30 ? kBlobLaneWide30 : kBlobLaneWide26);
+    static_assert(WD == 26 || WD == 30 || WD == 32 || wide_mid_ok(WD), "window width");
+    constexpr uint32_t kLane = WD == 32 ? kBlobLaneWide
+                                        : (WD == 30 ? kBlobLaneWide30
+                                                    : (WD == 26 ? kBlobLaneWide26 : kBlobLaneMid + (uint32_t)(WD - kWideMidMin) * 4096u));
     constexpr int kMergeK = 2 * (WD - wide_cl0(WD)) / 4;   // A_{8 k} with 8 k = 4 (WD - CL0)
+    static_assert((WD - wide_cl0(WD)) % 2 == 0 && kMergeK >= 1 && kMergeK <= 11, "merge table");
     for (int i = tid; i < 2048; i += NT) {   // slice tables as fcs_dma_kernel
         const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
         u32x4 vv = {v, v, v, v};
@@ -1177,7 +1184,7 @@ __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds
             p.blob[kBlobInvWide + i];
 }
 
-// The slot DMA: seven or eight 1 KiB rows from two address registers, each only as far as the
+// The slot DMA: six, seven or eight 1 KiB rows from two address registers, each only as far as the
 // item's bytes reach; the first and last rows at the default cache policy, the middle ones
 // non-temporal.
 template <int WD>
@@ -1191,12 +1198,15 @@ __device__ __forceinline__ void wide_dma_item(const uint8_t *slot, uint64_t src,
     if (2048u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, FCS_DMA_AUX);
     if (3072u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, FCS_DMA_AUX);
     if (4096u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 0, FCS_DMA_AUX);
-    if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
-    if constexpr (WD == 32) {
+    if constexpr (wide_slot(WD) == 6 * 1024) {   // six rows: the last one at the edge policy
+        if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_EDGE_AUX);
+    } else if constexpr (WD == 32) {
+        if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
         if (6144u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 2048, FCS_DMA_AUX);
         if (7168u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 3072, FCS_DMA_EDGE_AUX);
     } else {
         static_assert(wide_slot(WD) == 7 * 1024, "seven rows");
+        if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 1024, FCS_DMA_AUX);
         if (6144u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(b), lb, 16, 2048, FCS_DMA_EDGE_AUX);
     }
 }
@@ -2586,9 +2596,14 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
         }
     } else if (!tiny && fixed_wide(p)) {
         const int wd = wide_wd(p);
-        if (wd == 26) hipLaunchKernelGGL(fcs_wide_kernel<26>, dim3(grid), dim3(wide_threads(26)), 0, st, p);
-        else if (wd == 30) hipLaunchKernelGGL(fcs_wide_kernel<30>, dim3(grid), dim3(wide_threads(30)), 0, st, p);
-        else hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
+#define FCS_WIDE(W) \
+    case W: hipLaunchKernelGGL(fcs_wide_kernel<W>, dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
+        switch (wd) {
+            FCS_WIDE(10) FCS_WIDE(11) FCS_WIDE(12) FCS_WIDE(14) FCS_WIDE(15) FCS_WIDE(16) FCS_WIDE(18)
+            FCS_WIDE(19) FCS_WIDE(20) FCS_WIDE(22) FCS_WIDE(23) FCS_WIDE(24) FCS_WIDE(26) FCS_WIDE(30)
+            default: hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
+        }
+#undef FCS_WIDE
     } else if (fixed_segil(p)) {
         hipLaunchKernelGGL(fcs_segil_kernel, dim3(grid), dim3(kSegilThreads), 0, st, p);
     } else if (!tiny && fixed_dma(p)) {

@@ -178,7 +178,19 @@ inline bool fixed_segil(const KParams &p) {
 #define FCS_WIDE_MIN 1537
 #endif
 constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
-__host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : 832; }   // 12 / 13 waves
+__host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : (wd > 24 ? 832 : 1024); }   // 12 / 13 / 16 waves
+// Mid-length band (round 4): fixed lengths kWideMidMinLen..wide_cover(kWideMidMax) (1476 B) take the
+// narrowest bank-safe width whose 16 windows cover the frame (wide_mid_ok), 6 KiB slots, 16 waves,
+// instead of the flat kernel.
+#ifndef FCS_WIDE_MID_MIN   // measurement-only override of the band's lower end (0: no mid band)
+#define FCS_WIDE_MID_MIN 581
+#endif
+constexpr uint32_t kWideMidMinLen = FCS_WIDE_MID_MIN;
+__host__ __device__ constexpr int wide_mid_wd(uint32_t len) {
+    for (int wd = kWideMidMin; wd <= kWideMidMax; wd++)
+        if (wide_mid_ok(wd) && wide_cover(wd) >= len) return wd;
+    return 0;
+}
 // Window dwords for a fixed batch: 26 (104-B windows) or 30 (120-B windows), 7 KiB slots and 13
 // waves, when the frame and its item fit those, else 32 (128-B windows, 8 KiB slots, 12 waves);
 // 0: not the wide kernel.
@@ -187,6 +199,11 @@ inline int wide_wd(const KParams &p) {
     (void)p;
     return 0;
 #else
+    if (kWideMidMinLen && p.flen >= kWideMidMinLen && p.flen <= wide_cover(kWideMidMax)) {
+        const int wd = wide_mid_wd(p.flen);
+        return (p.stride <= 2048 && 3 * p.stride + p.flen <= wide_slot(wd) - 18 &&
+                p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(wd)) ? wd : 0;
+    }
     if (p.flen < kWideMinLen || p.stride > 4096) return 0;
 #ifndef FCS_WIDE_NO26   // measurement-only: the 128-B windows for the whole band
     if (p.flen <= kWideCover26 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&

@@ -90,7 +90,12 @@ constexpr uint32_t kWideWin = 128;                               // the widest w
 __host__ __device__ constexpr uint32_t wide_win(int wd) { return 4u * (uint32_t)wd; }
 __host__ __device__ constexpr uint32_t wide_step(int wd) { return 4u * (uint32_t)wd - 4u; }
 __host__ __device__ constexpr uint32_t wide_cover(int wd) { return 15u * wide_step(wd) + wide_win(wd); }
-__host__ __device__ constexpr uint32_t wide_slot(int wd) { return wd == 32 ? 8192u : 7168u; }
+__host__ __device__ constexpr uint32_t wide_slot(int wd) { return wd == 32 ? 8192u : (wd > 24 ? 7168u : 6144u); }
+// Mid-length windows (round 4): WD = kWideMidMin..kWideMidMax dwords, 6 KiB slots (four frames of up
+// to 1476 B), 16 waves. Only widths whose 16 window starts fall on 16 distinct dword banks are used:
+// (WD - 1) c mod 32 must differ for c = 0..15, so WD - 1 must not be a multiple of 4.
+constexpr int kWideMidMin = 10, kWideMidMax = 24;
+__host__ __device__ constexpr bool wide_mid_ok(int wd) { return wd >= kWideMidMin && wd <= kWideMidMax && (wd - 1) % 4 != 0; }
 constexpr uint32_t kWideCover = wide_cover(32);                  // 1988
 constexpr uint32_t kWideCover26 = wide_cover(26);                // 1604
 constexpr uint32_t kWideCover30 = wide_cover(30);                // 1860
@@ -118,7 +123,10 @@ constexpr uint32_t kBlobLaneWide = kBlobStreamK1 + 64;
 constexpr uint32_t kBlobLaneWide26 = kBlobLaneWide + 8 * 16 * 32;
 constexpr uint32_t kBlobLaneWide30 = kBlobLaneWide26 + 8 * 16 * 32;   // A_{116 c} (WD 30)
 constexpr uint32_t kBlobInvWide = kBlobLaneWide30 + 8 * 16 * 32;
-constexpr uint32_t kBlobWords = kBlobInvWide + kWideWin;
+// Mid-length wide kernels: lane tables A_{(4 WD - 4) c} for WD = kWideMidMin..kWideMidMax in the
+// LDS-DMA layout [8][16][32] (one set per width, unused widths included so the offsets stay simple).
+constexpr uint32_t kBlobLaneMid = kBlobInvWide + kWideWin;
+constexpr uint32_t kBlobWords = kBlobLaneMid + (kWideMidMax - kWideMidMin + 1) * 8 * 16 * 32;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -222,6 +230,13 @@ struct Tables {
                 for (int e = 0; e < 16; e++) b[kBlobLaneWide30 + (t * 16 + e) * 32 + slot] = nt[t][e];
         }
         for (int z = 0; z < (int)kWideWin; z++) b[kBlobInvWide + z] = shift(0xFFFFFFFFu, -(long)z);
+        for (int wd = kWideMidMin; wd <= kWideMidMax; wd++)   // mid-length wide kernels
+            for (int slot = 0; slot < 32; slot++) {
+                nibble_table((long)wide_step(wd) * (slot % kGroup), nt);
+                for (int t = 0; t < 8; t++)
+                    for (int e = 0; e < 16; e++)
+                        b[kBlobLaneMid + (wd - kWideMidMin) * 4096 + (t * 16 + e) * 32 + slot] = nt[t][e];
+            }
         return b;
     }
     // Tables of the single-frame kernel (fcs_launch.hpp OneArgs): T0..T3, then A_{24 * 2^k}.

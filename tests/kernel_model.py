@@ -326,7 +326,9 @@ BLOB_INV_WIDE = BLOB_LANE_WIDE30 + 8 * 16 * 32
 WIDE_WIN, WIDE_SLOT = 128, 8192
 WIDE_COVER = 124 * 15 + WIDE_WIN   # 1988
 WIDE_MERGE_HOLE, WIDE_INV_HOLE = 128, 132
-WIDE_CL0 = {32: 16, 30: 14, 26: 12}        # chain 0's words; chain 1 takes the rest
+WIDE_MID = [wd for wd in range(10, 25) if (wd - 1) % 4]   # mid-length widths (fcs_tables.hpp wide_mid_ok)
+BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 10..24
+WIDE_CL0 = {32: 16, 30: 14, 26: 12, **{wd: wd - 2 * (wd // 4) for wd in WIDE_MID}}   # chain 0's words
 
 
 def wide_end_off(c, wd=32):
@@ -334,14 +336,25 @@ def wide_end_off(c, wd=32):
 
 
 def wide_slot(wd):
-    return 8192 if wd == 32 else 7168
+    return 8192 if wd == 32 else (7168 if wd > 24 else 6144)
+
+
+def wide_cover(wd):
+    return 15 * (4 * wd - 4) + 4 * wd
+
+
+def wide_mid_wd(flen):
+    """The width the host picks for a mid-length frame (fcs_launch.hpp wide_mid_wd)."""
+    return next(wd for wd in WIDE_MID if wide_cover(wd) >= flen)
 
 
 def build_lds_wide(blob, wd=32):
     """fcs_wide_kernel<WD>'s 64 KiB table image: the slice tables as fcs_dma_kernel's; holes 16t+n
     the lane tables A_{(4 WD - 4) c}; holes 128..131 the chain merge A_{4 (WD - CL0)}; holes
     132..135 INV[0..127]."""
-    lane_blob = {32: BLOB_LANE_WIDE, 30: BLOB_LANE_WIDE30, 26: BLOB_LANE_WIDE26}[wd]
+    lane_blob = {32: BLOB_LANE_WIDE, 30: BLOB_LANE_WIDE30, 26: BLOB_LANE_WIDE26}.get(wd)
+    if lane_blob is None:
+        lane_blob = BLOB_LANE_MID + (wd - 10) * 4096
     k = (4 * (wd - WIDE_CL0[wd])) // 8
     lds = np.zeros(65536 // 4, dtype=np.uint32)
     for e in range(256):

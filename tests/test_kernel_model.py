@@ -176,7 +176,7 @@ def test_segil_decomposition_model(lds_dma, L):
 @pytest.fixture(scope="module")
 def lds_wide():
     blob = na.tables_blob()
-    return {wd: km.build_lds_wide(blob, wd) for wd in (26, 30, 32)}
+    return {wd: km.build_lds_wide(blob, wd) for wd in (26, 30, 32, *km.WIDE_MID)}
 
 
 @pytest.mark.parametrize("flen,extra,wd", [(1525, 0, 32), (1530, 3, 32), (1536, 0, 32), (1537, 1, 32), (1600, 0, 32),
@@ -186,7 +186,13 @@ def lds_wide():
                                            (1537, 0, 26), (1538, 3, 26), (1501, 0, 26), (1600, 0, 26), (1601, 1, 26),
                                            (1604, 0, 26), (1604, 178, 26),   # 7150: the 7 KiB slot's largest
                                            (1605, 0, 30), (1700, 1, 30), (1741, 0, 30), (1742, 2, 30), (1787, 0, 30),
-                                           (1600, 3, 30)])
+                                           (1600, 3, 30)] +
+                         # mid-length widths (6 KiB slots): each width's narrowest and widest frame,
+                         # a gap, and the largest stride a 6 KiB slot takes (3 stride + len = 6126)
+                         [(L, x, wd) for wd in km.WIDE_MID
+                          for L in sorted({km.wide_cover(wd), max(581, min(km.wide_cover(wd) - 63, km.wide_cover(wd)))})
+                          if L <= km.wide_cover(wd) and km.wide_mid_wd(L) in (wd, km.WIDE_MID[0])
+                          for x in (0, 5, (6126 - L) // 3 - L)])
 def test_wide_kernel_model(lds_wide, flen, extra, wd):
     """fcs_wide_kernel's decomposition (128-B windows ending 124 c before the frame end, every
     live lane but the front one masking its first word, the front lane cf = (len - 1) / 124 masking
@@ -209,7 +215,7 @@ def test_wide_kernel_model(lds_wide, flen, extra, wd):
 
 def test_wide_windows_bank_distinct():
     """The 16 windows of a frame in fcs_wide_kernel start on 16 distinct dword banks (mod 32)."""
-    for wd in (26, 30, 32):
+    for wd in (26, 30, 32, *km.WIDE_MID):
         for E in range(0, 64, 4):
             banks = {((E - km.wide_end_off(c, wd) - 4 * wd) // 4) % 32 for c in range(16)}
             assert len(banks) == 16
