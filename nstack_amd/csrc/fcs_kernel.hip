@@ -1302,10 +1302,11 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
         }
         // chain 0 over words [0, CL0), chain 1 over [CL0, WD), run side by side
         uint32_t xa = w[0] ^ x0, xb = w[CL0];
+        constexpr int CL1 = WD - CL0, CLM = CL0 > CL1 ? CL0 : CL1;   // either chain may be the longer one
 #pragma unroll
-        for (int i = 0; i < WD - CL0; i++) {
+        for (int i = 0; i < CLM; i++) {
             if (i < CL0) xa = step4_l8(lds, xa, i < CL0 - 1 ? w[i + 1] : 0u, B, SEL);
-            xb = step4_l8(lds, xb, i < WD - CL0 - 1 ? w[CL0 + i + 1] : 0u, B, SEL);
+            if (i < CL1) xb = step4_l8(lds, xb, i < CL1 - 1 ? w[CL0 + i + 1] : 0u, B, SEL);
         }
         const uint32_t mv = merge_shift_dma(lds, 0, xa, xb);
         uint32_t v = live ? lane_shift_dma(lds, mv, lanebase) : 0u;
