@@ -2600,8 +2600,7 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #define FCS_WIDE(W) \
     case W: hipLaunchKernelGGL(fcs_wide_kernel<W>, dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
         switch (wd) {
-            FCS_WIDE(10) FCS_WIDE(11) FCS_WIDE(12) FCS_WIDE(14) FCS_WIDE(15) FCS_WIDE(16) FCS_WIDE(18)
-            FCS_WIDE(19) FCS_WIDE(20) FCS_WIDE(22) FCS_WIDE(23) FCS_WIDE(24) FCS_WIDE(26) FCS_WIDE(30)
+            FCS_WIDE(20) FCS_WIDE(22) FCS_WIDE(23) FCS_WIDE(24) FCS_WIDE(26) FCS_WIDE(30)
             default: hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
         }
 #undef FCS_WIDE

@@ -179,11 +179,13 @@ inline bool fixed_segil(const KParams &p) {
 #endif
 constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
 __host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : (wd > 24 ? 832 : 1024); }   // 12 / 13 / 16 waves
-// Mid-length band (round 4): fixed lengths kWideMidMinLen..wide_cover(kWideMidMax) (1476 B) take the
-// narrowest bank-safe width whose 16 windows cover the frame (wide_mid_ok), 6 KiB slots, 16 waves,
-// instead of the flat kernel.
+// Mid-length band (round 4): fixed lengths kWideMidMinLen..wide_cover(kWideMidMax) (1157..1476 B)
+// take the narrowest bank-safe width whose 16 windows cover the frame (wide_mid_ok), 6 KiB slots,
+// 16 waves, instead of the flat kernel: tools/ab.py, one process per length,
+// 1160 B +4.3 %, 1250 B +4.2 %, 1300 B +4.3 %, 1350 B +7.2 %, 1413 B +5.6 %, 1476 B +7.7 %; the
+// narrower widths lost to the flat kernel (700 B -7.4 %, 1000 B -2.9 %, 1100 B -0.5 %).
 #ifndef FCS_WIDE_MID_MIN   // measurement-only override of the band's lower end (0: no mid band)
-#define FCS_WIDE_MID_MIN 581
+#define FCS_WIDE_MID_MIN 1157
 #endif
 constexpr uint32_t kWideMidMinLen = FCS_WIDE_MID_MIN;
 __host__ __device__ constexpr int wide_mid_wd(uint32_t len) {

@@ -326,8 +326,8 @@ BLOB_INV_WIDE = BLOB_LANE_WIDE30 + 8 * 16 * 32
 WIDE_WIN, WIDE_SLOT = 128, 8192
 WIDE_COVER = 124 * 15 + WIDE_WIN   # 1988
 WIDE_MERGE_HOLE, WIDE_INV_HOLE = 128, 132
-WIDE_MID = [wd for wd in range(10, 25) if (wd - 1) % 4]   # mid-length widths (fcs_tables.hpp wide_mid_ok)
-BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 10..24
+WIDE_MID = [wd for wd in range(20, 25) if (wd - 1) % 4]   # mid-length widths (fcs_tables.hpp wide_mid_ok)
+BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 20..24
 WIDE_CL0 = {32: 16, 30: 14, 26: 12, **{wd: wd - 2 * (wd // 4) for wd in WIDE_MID}}   # chain 0's words
 
 
@@ -354,7 +354,7 @@ def build_lds_wide(blob, wd=32):
     132..135 INV[0..127]."""
     lane_blob = {32: BLOB_LANE_WIDE, 30: BLOB_LANE_WIDE30, 26: BLOB_LANE_WIDE26}.get(wd)
     if lane_blob is None:
-        lane_blob = BLOB_LANE_MID + (wd - 10) * 4096
+        lane_blob = BLOB_LANE_MID + (wd - WIDE_MID[0]) * 4096
     k = (4 * (wd - WIDE_CL0[wd])) // 8
     lds = np.zeros(65536 // 4, dtype=np.uint32)
     for e in range(256):

@@ -190,8 +190,8 @@ def lds_wide():
                          # mid-length widths (6 KiB slots): each width's narrowest and widest frame,
                          # a gap, and the largest stride a 6 KiB slot takes (3 stride + len = 6126)
                          [(L, x, wd) for wd in km.WIDE_MID
-                          for L in sorted({km.wide_cover(wd), max(581, min(km.wide_cover(wd) - 63, km.wide_cover(wd)))})
-                          if L <= km.wide_cover(wd) and km.wide_mid_wd(L) in (wd, km.WIDE_MID[0])
+                          for L in sorted({km.wide_cover(wd), max(1157, km.wide_cover(wd) - 63)})
+                          if km.wide_mid_wd(L) == wd
                           for x in (0, 5, (6126 - L) // 3 - L)])
 def test_wide_kernel_model(lds_wide, flen, extra, wd):
     """fcs_wide_kernel's decomposition (128-B windows ending 124 c before the frame end, every
