@@ -1471,7 +1471,7 @@ const char *fcs_last_error(void) { return g_last_error.c_str(); }
 const char *fcs_engine_version(void) {
     return "nstack-fcs 0.6 gfx950: quarter-wave/frame, 96B lane windows as 2 slice-by-4 chains, v_perm "
            "addressing, DPP reduce; 1496-1524B: LDS-DMA (nt global_load_lds) 6KiB slot/wave, 16 waves/CU, "
-           "32KiB 8-replica tables, guided dynamic items; 1537-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
+           "32KiB 8-replica tables, guided dynamic items; 1157-1476B: 80-96B-window LDS-DMA, 6KiB slots; 1537-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
            ">1524B otherwise: frame-interleaved LDS-DMA segments; var: "
            "packed 64-1536B units as an arena stream (4KiB LDS-DMA items, taps at frame boundaries, XOR "
            "scan), other units as a flat chunk stream per 64-frame window";
