@@ -206,6 +206,11 @@ inline int wide_wd(const KParams &p) {
         return (p.stride <= 2048 && 3 * p.stride + p.flen <= wide_slot(wd) - 18 &&
                 p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(wd)) ? wd : 0;
     }
+#ifdef FCS_WIDE_PRE   // measurement-only: 1477..1495 B (between the mid band and the LDS-DMA kernel) on WD 26
+    if (p.flen > wide_cover(kWideMidMax) && p.flen < kDmaMinLen)
+        return (p.stride <= 2048 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&
+                p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(26)) ? 26 : 0;
+#endif
     if (p.flen < kWideMinLen || p.stride > 4096) return 0;
 #ifndef FCS_WIDE_NO26   // measurement-only: the 128-B windows for the whole band
     if (p.flen <= kWideCover26 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&

@@ -34,6 +34,7 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_WIDE_NO26 -DFCS_WIDE_NO30"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1525"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MID_MIN=0"),
+    ("fcs_engine.cpp", "-DFCS_WIDE_PRE"),
     ("fcs_engine.cpp", "-DFCS_SEGIL_ANY"),
     ("fcs_kernel.hip", "-DFCS_BLOCKED"),
     ("fcs_kernel.hip", "-DFCS_XCD -DFCS_NO_WAVE_SYNC"),
