@@ -348,7 +348,10 @@ std::atomic<DevState *> g_last_stream_dev{nullptr};
 // Fixed-length batches of frames up to this length (and more than g_var_threshold frames) take the
 // flat variable-length kernel: a 64-B frame then costs one lane instead of a quarter-wave. Measured
 // against the quarter-wave kernel (tools/ab.py): 64 B 11x, 576 B 2.1x, 1300 B
-// +6.5 %; 1504..1536 B stay on the single kernel (the flat kernel is 9 % slower at 1518 B).
+// +6.5 %; 1504..1536 B stay on the single kernel (the flat kernel is 9 % slower at 1518 B). The
+// slot kernels go first where their slots take the batch: the mid-length and 104-B-window wide
+// kernels (1157..1495 B) and the LDS-DMA kernel (1496..1503 B: +10 % against the flat kernel,
+// tools/ab.py, round 4).
 #ifndef FCS_FIXED_FLAT_MAX   // measurement-only override (0 = never)
 #define FCS_FIXED_FLAT_MAX 1503
 #endif
@@ -441,7 +444,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.blob = ds->d_blob;
     p.dbg = g_dbg;
     if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed) &&
-        !(!fcs::fixed_tiny(p) && fcs::fixed_wide(p))) {   // (the mid-length wide kernels go first)
+        !(!fcs::fixed_tiny(p) && (fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {   // (slot kernels first)
         // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame
         // instead of a 16-lane quarter-wave (len == null tells it the length is p.flen)
         p.zmax = fcs::kChunkBytes;

@@ -1411,8 +1411,16 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     const uint64_t n = p.n, units = (n + 3) >> 2;
     // chunks of about 64 items, and at least 16 units so that result runs fill 256-B groups; jumbo
     // frames (m >= 4) up to 32 units: each chunk is one device-scope atomic on the work counter, and
-    // at 16 units those were 13 % on top of the CRC bytes in WRITE_SIZE
-    const uint32_t cmax = m >= 4 ? 32u : 64u / m;
+    // at 16 units those were 13 % on top of the CRC bytes in WRITE_SIZE. Frames of
+    // m > 6 items take at most about kSegilChunkItems items per chunk, so that the last chunks still
+    // balance across the waves (tools/ab.py, round 4: 16384 B +3 %, 65536 B +10.6 %; 9000 B, m = 6,
+    // unchanged).
+#ifndef FCS_SEGIL_CMAX_ITEMS   // measurement-only override
+#define FCS_SEGIL_CMAX_ITEMS 192
+#endif
+    constexpr uint32_t kSegilChunkItems = FCS_SEGIL_CMAX_ITEMS;
+    const uint32_t cmax = m >= 4 ? (kSegilChunkItems / m > 32u ? 32u : (kSegilChunkItems / m < 1u ? 1u : kSegilChunkItems / m))
+                                 : 64u / m;
     Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kSegilWaves, (uint64_t)blockIdx.x * kSegilWaves + (uint64_t)wave,
                 lane, 100, 1, cmax);
     D.align = 16;

@@ -171,11 +171,13 @@ inline bool fixed_segil(const KParams &p) {
 // lane windows, 12 waves, 8 KiB slots) whose four consecutive frames fit one slot, as fixed_dma().
 // Against the kernels these lengths took before (tools/ab.py, one process): 1537 B
 // +22 %, 1600-1949 B +24 to +27 % (generic kernel, two segments), 1950-1988 B +23 to +26 %
-// (segment kernel); 1525-1536 B -8 % against the single-segment kernel, which keeps them. The
-// 104-B windows (WD 26) then took 1537-1604 B another +26 to +27 % (13 waves instead of 12), and
-// 120-B windows (WD 30) 1605-1787 B +16 to +19 %.
+// (segment kernel). The 104-B windows (WD 26) then took 1537-1604 B another +26 to +27 % (13 waves
+// instead of 12), and 120-B windows (WD 30) 1605-1787 B +16 to +19 %. Round 4 (one process per
+// length): WD 26 also takes 1525-1536 B (+15 to +17 % against the single-segment kernel; the 128-B
+// windows had lost there) and 1477-1495 B, between the mid band and the LDS-DMA kernel (+7 %
+// against the flat kernel).
 #ifndef FCS_WIDE_MIN   // measurement-only override of the band's lower end
-#define FCS_WIDE_MIN 1537
+#define FCS_WIDE_MIN 1525
 #endif
 constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
 __host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : (wd > 24 ? 832 : 1024); }   // 12 / 13 / 16 waves
@@ -206,12 +208,13 @@ inline int wide_wd(const KParams &p) {
         return (p.stride <= 2048 && 3 * p.stride + p.flen <= wide_slot(wd) - 18 &&
                 p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(wd)) ? wd : 0;
     }
-#ifdef FCS_WIDE_PRE   // measurement-only: 1477..1495 B (between the mid band and the LDS-DMA kernel) on WD 26
-    if (p.flen > wide_cover(kWideMidMax) && p.flen < kDmaMinLen)
-        return (p.stride <= 2048 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&
-                p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(26)) ? 26 : 0;
+    // 1477..1495 B: above the mid band, below the LDS-DMA kernel
+#ifdef FCS_WIDE_NO_PRE   // measurement-only: those on the flat kernel
+    const bool pre = false;
+#else
+    const bool pre = p.flen > wide_cover(kWideMidMax) && p.flen < kDmaMinLen;
 #endif
-    if (p.flen < kWideMinLen || p.stride > 4096) return 0;
+    if ((p.flen < kWideMinLen && !pre) || p.stride > 4096) return 0;
 #ifndef FCS_WIDE_NO26   // measurement-only: the 128-B windows for the whole band
     if (p.flen <= kWideCover26 && 3 * p.stride + p.flen <= wide_slot(26) - 18 &&
         p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(26))

@@ -1,8 +1,9 @@
 """GPU parity of the LDS-DMA fixed kernel (fcs_dma_kernel).
 
 Fixed-length batches of 1496..1524-B frames whose four consecutive frames fit a 6 KiB slot
-(3 stride + len <= 6126) and whose arena holds two slots take this kernel; smaller ones the
-register-load single kernel. Every case is checked bit-exact against the oracle (the CPU
+(3 stride + len <= 6126) and whose arena holds two slots take this kernel, large batches of
+1496..1503 B too (round 4: they took the flat kernel before); smaller ones the register-load
+single kernel. Every case is checked bit-exact against the oracle (the CPU
 restatement of src/ether_fcs.c:4-19), at all four base alignments, with batch sizes on both sides
 of the selection threshold and grids from one partial item to many sweeps, so the slot clamping at
 the arena end and frames past n in a wave's last item are exercised. Verify mode (frames carrying
@@ -94,7 +95,8 @@ def test_dma_verify_mode(dev, L):
     assert int(bad.item()) == len(bad_idx)
 
 
-@pytest.mark.parametrize("L,stride,lead", [(1518, 1518, 0), (1518, 1518, 3), (1514, 1518, 1), (1524, 1524, 2)])
+@pytest.mark.parametrize("L,stride,lead", [(1518, 1518, 0), (1518, 1518, 3), (1514, 1518, 1), (1524, 1524, 2),
+                                           (1496, 1496, 1), (1503, 1503, 3), (1500, 1536, 0)])
 def test_dma_dynamic_tail(dev, oracle, L, stride, lead):
     """Batches of >= 16 items (64 frames) per wave of the grid hand the last quarter of their items out
     through the device work counter (guided chunks): every frame of a 1 M-frame batch against the

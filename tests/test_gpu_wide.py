@@ -1,8 +1,10 @@
 """GPU parity of the wide LDS-DMA kernel (fcs_wide_kernel<WD>).
 
-Fixed-length frames of 1537..1988 B whose four consecutive frames fit one LDS slot take this kernel
+Fixed-length frames of 1525..1988 B whose four consecutive frames fit one LDS slot take this kernel
 (wide_wd(), fcs_launch.hpp), at one of three window widths:
   - WD 26: 104-B windows every 100 B (cover 1604 B), 7 KiB slots (3 stride + len <= 7150), 13 waves;
+    also 1477..1495 B, between the mid-length band (test_gpu_wide_mid.py) and the LDS-DMA kernel
+    (front lane 14, lane 15 dropped);
   - WD 30: 120-B windows every 116 B (cover 1860 B), 7 KiB slots, 13 waves: 1605..1787 B at
     stride = len (from 1788 B four frames no longer fit 7 KiB);
   - WD 32: 128-B windows every 124 B (cover 1988 B), 8 KiB slots (3 stride + len <= 8174), 12 waves:
@@ -55,7 +57,7 @@ def run(dev, d, lead, stride, L, n):
 
 # the band's ends and one byte outside; each front lane's first and last lengths (cf = 12 .. 15:
 # lengths 124 cf + 1 .. 124 cf + 124, zc = 127 .. 4); the QinQ / baby-giant sizes
-LENS = sorted({1524, 1525, 1526, 1530, 1536, 1537, 1548, 1549, 1552, 1600, 1601, 1604, 1605, 1611, 1624, 1625,
+LENS = sorted({1476, 1477, 1478, 1480, 1490, 1494, 1495, 1496, 1501, 1524, 1525, 1526, 1530, 1536, 1537, 1548, 1549, 1552, 1600, 1601, 1604, 1605, 1611, 1624, 1625,
                1672, 1673, 1676, 1700, 1740, 1741, 1787, 1788, 1796, 1797, 1800, 1860, 1861, 1864, 1900, 1920,
                1949, 1950, 1984, 1985, 1987, 1988, 1989, 2000})
 
@@ -77,7 +79,7 @@ def test_wide_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(1525, 1525), (1526, 1536), (1560, 1560), (1600, 1600), (1600, 1664),
+@pytest.mark.parametrize("L,stride", [(1477, 1477), (1495, 1536), (1525, 1525), (1526, 1536), (1536, 1536), (1560, 1560), (1600, 1600), (1600, 1664),
                                       (1700, 1700), (1787, 1787), (1788, 2000), (1949, 1949), (1988, 1988),
                                       (1988, 2062)])
 def test_wide_many_items(dev, oracle, L, stride):
@@ -107,7 +109,7 @@ def test_wide_seven_kib_slot_bound(dev, oracle, L, stride):
         assert np.array_equal(got, exp), (L, stride, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L", [1525, 1530, 1560, 1600, 1700, 1787, 1796, 1922, 1988])
+@pytest.mark.parametrize("L", [1477, 1490, 1525, 1530, 1536, 1560, 1600, 1700, 1787, 1796, 1922, 1988])
 def test_wide_verify_mode(dev, L):
     """RX residue check through the wide kernel: frames of L bytes carrying their FCS, a few
     corrupted; ok[] and the bad count against zlib."""
@@ -136,7 +138,7 @@ from hypothesis import given, settings, strategies as hst  # noqa: E402
 
 
 @settings(max_examples=40, deadline=None, derandomize=True)
-@given(hst.integers(1520, 1995), hst.integers(0, 200), hst.integers(1, 2000), hst.integers(0, 15))
+@given(hst.integers(1470, 1995), hst.integers(0, 200), hst.integers(1, 2000), hst.integers(0, 15))
 def test_wide_fuzz(dev, oracle, L, gap, n, lead):
     """Random lengths across the band and just outside it, gaps, frame counts and base alignments
     against the oracle (the wide kernel where its slot takes the item, the others elsewhere)."""

@@ -183,7 +183,8 @@ def lds_wide():
                                            (1611, 16, 32), (1736, 0, 32), (1737, 5, 32), (1860, 0, 32), (1861, 2, 32),
                                            (1949, 0, 32), (1950, 100, 32), (1987, 0, 32), (1988, 0, 32),
                                            (1988, 74, 32),   # 3 stride + len = 8174: the largest item a slot takes
-                                           (1537, 0, 26), (1538, 3, 26), (1501, 0, 26), (1600, 0, 26), (1601, 1, 26),
+                                           (1537, 0, 26), (1538, 3, 26), (1501, 0, 26), (1477, 0, 26), (1495, 7, 26), (1525, 0, 26),
+                                           (1536, 1, 26), (1600, 0, 26), (1601, 1, 26),
                                            (1604, 0, 26), (1604, 178, 26),   # 7150: the 7 KiB slot's largest
                                            (1605, 0, 30), (1700, 1, 30), (1741, 0, 30), (1742, 2, 30), (1787, 0, 30),
                                            (1600, 3, 30)] +

@@ -32,9 +32,10 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_SEGIL_NOCRC -DFCS_SEGIL_ANY"),
     ("fcs_kernel.hip", "-DFCS_NO_WIDE"),
     ("fcs_kernel.hip", "-DFCS_WIDE_NO26 -DFCS_WIDE_NO30"),
-    ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1525"),
+    ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1537"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MID_MIN=0"),
-    ("fcs_engine.cpp", "-DFCS_WIDE_PRE"),
+    ("fcs_engine.cpp", "-DFCS_WIDE_NO_PRE"),
+    ("fcs_kernel.hip", "-DFCS_SEGIL_CMAX_ITEMS=100000"),
     ("fcs_engine.cpp", "-DFCS_SEGIL_ANY"),
     ("fcs_kernel.hip", "-DFCS_BLOCKED"),
     ("fcs_kernel.hip", "-DFCS_XCD -DFCS_NO_WAVE_SYNC"),
