@@ -350,7 +350,7 @@ std::atomic<DevState *> g_last_stream_dev{nullptr};
 // against the quarter-wave kernel (tools/ab.py): 64 B 11x, 576 B 2.1x, 1300 B
 // +6.5 %; 1504..1536 B stay on the single kernel (the flat kernel is 9 % slower at 1518 B). The
 // slot kernels go first where their slots take the batch: the mid-length and 104-B-window wide
-// kernels (1157..1495 B) and the LDS-DMA kernel (1496..1503 B: +10 % against the flat kernel,
+// kernels (870..1495 B) and the LDS-DMA kernel (1496..1503 B: +10 % against the flat kernel,
 // tools/ab.py, round 4).
 #ifndef FCS_FIXED_FLAT_MAX   // measurement-only override (0 = never)
 #define FCS_FIXED_FLAT_MAX 1503
@@ -1474,7 +1474,7 @@ const char *fcs_last_error(void) { return g_last_error.c_str(); }
 const char *fcs_engine_version(void) {
     return "nstack-fcs 0.6 gfx950: quarter-wave/frame, 96B lane windows as 2 slice-by-4 chains, v_perm "
            "addressing, DPP reduce; 1496-1524B: LDS-DMA (nt global_load_lds) 6KiB slot/wave, 16 waves/CU, "
-           "32KiB 8-replica tables, guided dynamic items; 1157-1476B: 80-96B-window LDS-DMA, 6KiB slots; 1537-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
+           "32KiB 8-replica tables, guided dynamic items; 870-1476B: 60-96B-window LDS-DMA, 6KiB slots; 1477-1495B, 1525-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
            ">1524B otherwise: frame-interleaved LDS-DMA segments; var: "
            "packed 64-1536B units as an arena stream (4KiB LDS-DMA items, taps at frame boundaries, XOR "
            "scan), other units as a flat chunk stream per 64-frame window";

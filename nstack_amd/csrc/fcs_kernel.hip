@@ -1239,6 +1239,9 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
     const uint32_t mwords = (zc + 3u) / 4u;
     const bool live = c <= cf, front = c == cf;
     const uint32_t x0 = front ? lds_rd(lds, dma_hole(kWideInvHole + zc / 32u) + (zc % 32u) * 4u) : 0u;
+    const uint32_t m0 = front ? (zc >= 4u ? 0u : (uint32_t)(0xFFFFFFFFull << (8u * zc))) : 0u;
+    uint32_t keep = front ? 0u : 0xFFFFFFFFu;
+    asm volatile("" : "+v"(keep));   // opaque: kept a register, not re-derived as a per-word select
     const int64_t klane = (int64_t)g * (int64_t)p.stride + (int64_t)p.flen - (int64_t)(kStep * (uint32_t)c) - (int64_t)kWin;
 
     // slots are whole 16-B pieces inside [floor16(lo4), ceil16(hi4)) (as fcs_dma_kernel's)
@@ -1291,6 +1294,7 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
         for (int i = 0; i < WD; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
         // masks: word 0 of every live lane (its neighbour's last word) except the front lane's, whose
         // first zc bytes go (scalar masks, words below the launch-uniform bound only)
+#ifdef FCS_WIDE_OLD_MASK   // measurement-only: round-3 form (a select and an AND per word)
         w[0] &= front ? (zc >= 4u ? 0u : (uint32_t)(0xFFFFFFFFull << (8u * zc))) : 0u;
 #pragma unroll
         for (int i = 1; i < WD; i++) {
@@ -1300,6 +1304,19 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
                 w[i] &= front ? mk : 0xFFFFFFFFu;
             }
         }
+#else
+        // word 0 by a per-lane loop invariant; word i >= 1 by mk_i | keep (keep = ~0 outside the front
+        // lane), which the compiler hoists into a register per word: one AND per word and item. (A
+        // branch on the launch-uniform mwords was if-converted into a select per word.)
+        (void)mwords;
+        w[0] &= m0;
+#pragma unroll
+        for (int i = 1; i < WD; i++) {
+            const int t = (int)zc - 4 * i;
+            const uint32_t mk = t >= 4 ? 0u : (uint32_t)(0xFFFFFFFFull << (8 * (t < 0 ? 0 : t)));
+            w[i] &= mk | keep;
+        }
+#endif
         // chain 0 over words [0, CL0), chain 1 over [CL0, WD), run side by side
         uint32_t xa = w[0] ^ x0, xb = w[CL0];
         constexpr int CL1 = WD - CL0, CLM = CL0 > CL1 ? CL0 : CL1;   // either chain may be the longer one
@@ -2608,6 +2625,27 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #define FCS_WIDE(W) \
     case W: hipLaunchKernelGGL(fcs_wide_kernel<W>, dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
         switch (wd) {
+#if FCS_WIDE_MID_WD_MIN <= 11   // the mid-length widths from kWideMidMin (11 .. 12: measurement builds)
+            FCS_WIDE(11)
+#endif
+#if FCS_WIDE_MID_WD_MIN <= 12
+            FCS_WIDE(12)
+#endif
+#if FCS_WIDE_MID_WD_MIN <= 14
+            FCS_WIDE(14)
+#endif
+#if FCS_WIDE_MID_WD_MIN <= 15
+            FCS_WIDE(15)
+#endif
+#if FCS_WIDE_MID_WD_MIN <= 16
+            FCS_WIDE(16)
+#endif
+#if FCS_WIDE_MID_WD_MIN <= 18
+            FCS_WIDE(18)
+#endif
+#if FCS_WIDE_MID_WD_MIN <= 19
+            FCS_WIDE(19)
+#endif
             FCS_WIDE(20) FCS_WIDE(22) FCS_WIDE(23) FCS_WIDE(24) FCS_WIDE(26) FCS_WIDE(30)
             default: hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
         }

@@ -181,13 +181,14 @@ inline bool fixed_segil(const KParams &p) {
 #endif
 constexpr uint32_t kWideMinLen = FCS_WIDE_MIN;
 __host__ __device__ constexpr int wide_threads(int wd) { return wd == 32 ? 768 : (wd > 24 ? 832 : 1024); }   // 12 / 13 / 16 waves
-// Mid-length band (round 4): fixed lengths kWideMidMinLen..wide_cover(kWideMidMax) (1157..1476 B)
+// Mid-length band (round 4): fixed lengths kWideMidMinLen..wide_cover(kWideMidMax) (870..1476 B)
 // take the narrowest bank-safe width whose 16 windows cover the frame (wide_mid_ok), 6 KiB slots,
-// 16 waves, instead of the flat kernel: tools/ab.py, one process per length,
-// 1160 B +4.3 %, 1250 B +4.2 %, 1300 B +4.3 %, 1350 B +7.2 %, 1413 B +5.6 %, 1476 B +7.7 %; the
-// narrower widths lost to the flat kernel (700 B -7.4 %, 1000 B -2.9 %, 1100 B -0.5 %).
+// 16 waves, instead of the flat kernel. tools/ab.py, one process per length, with the one-AND front
+// masks: 870 B +5.8 %, 880 B +3.9 %, 900 B +5.7 %, 965 B +4.4 %, 1000 B +1.8 %,
+// 1093 B +7.1 %, 1157 B +10.5 %, 1300 B +7.7 %; below the band 837 B -2.3 %, 860 B -1.0 %, and
+// WD 14 at 720 B -9 %.
 #ifndef FCS_WIDE_MID_MIN   // measurement-only override of the band's lower end (0: no mid band)
-#define FCS_WIDE_MID_MIN 1157
+#define FCS_WIDE_MID_MIN 870
 #endif
 constexpr uint32_t kWideMidMinLen = FCS_WIDE_MID_MIN;
 __host__ __device__ constexpr int wide_mid_wd(uint32_t len) {

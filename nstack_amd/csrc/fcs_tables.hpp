@@ -91,12 +91,16 @@ __host__ __device__ constexpr uint32_t wide_win(int wd) { return 4u * (uint32_t)
 __host__ __device__ constexpr uint32_t wide_step(int wd) { return 4u * (uint32_t)wd - 4u; }
 __host__ __device__ constexpr uint32_t wide_cover(int wd) { return 15u * wide_step(wd) + wide_win(wd); }
 __host__ __device__ constexpr uint32_t wide_slot(int wd) { return wd == 32 ? 8192u : (wd > 24 ? 7168u : 6144u); }
-// Mid-length windows (round 4): WD = kWideMidMin..kWideMidMax dwords (cover 1157..1476 B), 6 KiB
+// Mid-length windows (round 4): WD = kWideMidMin..kWideMidMax dwords (cover 900..1476 B), 6 KiB
 // slots (four frames), 16 waves. Only widths whose 16 window starts fall on 16 distinct dword banks
-// are used: (WD - 1) c mod 32 must differ for c = 0..15, so WD - 1 must not be a multiple of 4 (WD 21
-// is skipped). Narrower widths (581..1156 B) measured slower than the flat kernel and are not used
+// are used: (WD - 1) c mod 32 must differ for c = 0..15, so WD - 1 must not be a multiple of 4 (WD 17
+// and 21 are skipped). Narrower widths (below 870 B) measured no faster than the flat kernel
 // (DESIGN.md §3.2d).
-constexpr int kWideMidMin = 20, kWideMidMax = 24;
+#ifndef FCS_WIDE_MID_WD_MIN   // the narrowest mid-length width (11..14: measurement builds)
+#define FCS_WIDE_MID_WD_MIN 15
+#endif
+constexpr int kWideMidMin = FCS_WIDE_MID_WD_MIN, kWideMidMax = 24;
+static_assert(kWideMidMin >= 11 && kWideMidMin <= 20, "mid-length widths the launch switch instantiates");
 __host__ __device__ constexpr bool wide_mid_ok(int wd) { return wd >= kWideMidMin && wd <= kWideMidMax && (wd - 1) % 4 != 0; }
 constexpr uint32_t kWideCover = wide_cover(32);                  // 1988
 constexpr uint32_t kWideCover26 = wide_cover(26);                // 1604

@@ -326,8 +326,8 @@ BLOB_INV_WIDE = BLOB_LANE_WIDE30 + 8 * 16 * 32
 WIDE_WIN, WIDE_SLOT = 128, 8192
 WIDE_COVER = 124 * 15 + WIDE_WIN   # 1988
 WIDE_MERGE_HOLE, WIDE_INV_HOLE = 128, 132
-WIDE_MID = [wd for wd in range(20, 25) if (wd - 1) % 4]   # mid-length widths (fcs_tables.hpp wide_mid_ok)
-BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 20..24
+WIDE_MID = [wd for wd in range(15, 25) if (wd - 1) % 4]   # mid-length widths (fcs_tables.hpp wide_mid_ok)
+BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 15..24
 WIDE_CL0 = {32: 16, 30: 14, 26: 12, **{wd: wd - 2 * (wd // 4) for wd in WIDE_MID}}   # chain 0's words
 
 

@@ -579,10 +579,10 @@ def test_var_batches_fuzz(dev, batch, kernel):
 
 
 # Fixed-length batches above the small-batch threshold with frames of at most 1503 B take the flat
-# kernel (len array absent: the length is the batch's) unless a slot kernel takes them (1157..1503 B
+# kernel (len array absent: the length is the batch's) unless a slot kernel takes them (870..1503 B
 # with strides whose four frames fit its slot); lengths and strides the route covers.
 @pytest.mark.parametrize("L,stride", [(0, 4), (1, 1), (13, 17), (60, 60), (64, 64), (70, 72),
-                                      (96, 96), (97, 101), (576, 576), (1000, 1003), (1156, 1156),
+                                      (96, 96), (97, 101), (576, 576), (1000, 1003), (869, 869), (1156, 2100),
                                       (1157, 2100), (1476, 2049), (1490, 1900), (1503, 2100)])
 def test_fixed_short_frames_flat_route(dev, oracle, L, stride):
     n = 20000   # > the 16384-frame small-batch threshold

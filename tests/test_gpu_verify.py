@@ -150,9 +150,9 @@ def test_verify_fixed_single_and_multi_segment(dev, oracle, L):
     assert int(bad.item()) == int((exp == 0).sum())
 
 
-@pytest.mark.parametrize("L", [64, 576, 1156])
+@pytest.mark.parametrize("L", [64, 576, 869])
 def test_verify_fixed_flat_route(dev, oracle, L):
-    """Fixed frames of <= 1156 B (packed; longer ones take the slot kernels, up to 1503 B with
+    """Fixed frames of <= 869 B (packed; longer ones take the slot kernels, up to 1503 B with
     strides those do not take) in batches of > 16384 take the flat chunk-stream kernel with no
     length array (p.len == null) and the fused ok/bad epilogue: corrupted frames
     included, ok[] and the bad count against the oracle."""

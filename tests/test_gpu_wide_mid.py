@@ -1,12 +1,12 @@
-"""GPU parity of the mid-length wide kernels (fcs_wide_kernel<WD>, WD = 20, 22, 23, 24).
+"""GPU parity of the mid-length wide kernels (fcs_wide_kernel<WD>, WD = 15 .. 24).
 
-Fixed-length frames of 1157..1476 B whose four consecutive frames fit a 6 KiB slot take the narrowest
+Fixed-length frames of 870..1476 B whose four consecutive frames fit a 6 KiB slot take the narrowest
 bank-safe window width whose 16 windows cover the frame (fcs_launch.hpp wide_mid_wd: WD - 1 not a
-multiple of 4, so WD 21 is skipped): windows of 4 WD bytes every 4 WD - 4 bytes, 16 waves. Before
-round 4 these lengths took the flat chunk stream (which keeps 581..1156 B: the narrower widths
-measured slower). Every case is checked bit-exact against the oracle (the CPU restatement of
-src/ether_fcs.c:4-19): both ends of every width's band, the band's own ends and the lengths just
-outside it (1156 / 1157, 1476 / 1477), strides from no gap to the largest
+multiple of 4, so WD 17 and 21 are skipped): windows of 4 WD bytes every 4 WD - 4 bytes, 16 waves.
+Before round 4 these lengths took the flat chunk stream, which keeps the shorter ones. Every case is
+checked bit-exact against the oracle (the CPU restatement of src/ether_fcs.c:4-19): both ends of
+every width's band, the band's own ends and the lengths just outside it (869 / 870, 1476 / 1477),
+strides from no gap to the largest
 a 6 KiB slot takes (3 stride + len = 6126) and one past it, all base alignments, partial items, the
 arena-end slot clamp, batches large enough for the dynamic schedule, verify mode, and a fuzz over
 the band. The CPU model of the same decomposition: tests/test_kernel_model.py::test_wide_kernel_model.
@@ -23,7 +23,7 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-WIDTHS = [wd for wd in range(20, 25) if (wd - 1) % 4]
+WIDTHS = [wd for wd in range(15, 25) if (wd - 1) % 4]
 
 
 def cover(wd):
@@ -53,8 +53,8 @@ def run(dev, d, lead, stride, L, n):
 
 
 # each width's narrowest and widest frame, and the band's ends with the lengths just outside
-LENS = sorted({700, 1000, 1156, 1157, 1476, 1477, 1500} | {cover(wd) for wd in WIDTHS} |
-              {cover(prev) + 1 for prev, wd in zip([19] + WIDTHS[:-1], WIDTHS)})
+LENS = sorted({700, 837, 869, 870, 1000, 1156, 1157, 1476, 1477, 1500} | {cover(wd) for wd in WIDTHS} |
+              {cover(prev) + 1 for prev, wd in zip(WIDTHS[:-1], WIDTHS[1:])})
 
 
 @pytest.mark.parametrize("L", LENS)
@@ -72,7 +72,7 @@ def test_mid_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(1000, 1000), (1157, 1157), (1200, 1200), (1220, 1300), (1221, 1221),
+@pytest.mark.parametrize("L,stride", [(870, 870), (900, 964), (1000, 1000), (1092, 1092), (1157, 1157), (1200, 1200), (1220, 1300), (1221, 1221),
                                       (1300, 1300), (1400, 1400), (1476, 1476), (1476, 1550)])
 def test_mid_many_items(dev, oracle, L, stride):
     """More items than the grid's waves (the dynamic schedule) and a second launch reusing the
@@ -86,7 +86,7 @@ def test_mid_many_items(dev, oracle, L, stride):
         assert np.array_equal(got, exp), int(np.argmax(got != exp))
 
 
-@pytest.mark.parametrize("L", [1157, 1220, 1221, 1349, 1412, 1413, 1476])
+@pytest.mark.parametrize("L", [870, 900, 964, 965, 1093, 1157, 1220, 1221, 1349, 1412, 1413, 1476])
 def test_mid_verify_mode(dev, L):
     """RX residue check through the mid-length kernels: frames of L bytes carrying their FCS, a few
     corrupted; ok[] and the bad count against zlib."""
@@ -115,7 +115,7 @@ from hypothesis import given, settings, strategies as hst  # noqa: E402
 
 
 @settings(max_examples=40, deadline=None, derandomize=True)
-@given(hst.integers(1100, 1500), hst.integers(0, 400), hst.integers(1, 3000), hst.integers(0, 15))
+@given(hst.integers(800, 1500), hst.integers(0, 400), hst.integers(1, 3000), hst.integers(0, 15))
 def test_mid_fuzz(dev, oracle, L, gap, n, lead):
     """Random lengths across the band and just outside it, gaps, frame counts and base alignments
     against the oracle (the mid-length kernels where a 6 KiB slot takes the item, others elsewhere)."""

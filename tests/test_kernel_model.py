@@ -191,7 +191,7 @@ def lds_wide():
                          # mid-length widths (6 KiB slots): each width's narrowest and widest frame,
                          # a gap, and the largest stride a 6 KiB slot takes (3 stride + len = 6126)
                          [(L, x, wd) for wd in km.WIDE_MID
-                          for L in sorted({km.wide_cover(wd), max(1157, km.wide_cover(wd) - 63)})
+                          for L in sorted({km.wide_cover(wd), max(870, km.wide_cover(wd) - 63)})
                           if km.wide_mid_wd(L) == wd
                           for x in (0, 5, (6126 - L) // 3 - L)])
 def test_wide_kernel_model(lds_wide, flen, extra, wd):

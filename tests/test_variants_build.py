@@ -31,9 +31,11 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_NO_SEGIL -DFCS_SEGIL_TAIL_AUX=2 -DFCS_SEGIL_SKEW=0"),
     ("fcs_kernel.hip", "-DFCS_SEGIL_NOCRC -DFCS_SEGIL_ANY"),
     ("fcs_kernel.hip", "-DFCS_NO_WIDE"),
+    ("fcs_kernel.hip", "-DFCS_WIDE_OLD_MASK"),
     ("fcs_kernel.hip", "-DFCS_WIDE_NO26 -DFCS_WIDE_NO30"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1537"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MID_MIN=0"),
+    ("fcs_kernel.hip", "-DFCS_WIDE_MID_WD_MIN=11"),
     ("fcs_engine.cpp", "-DFCS_WIDE_NO_PRE"),
     ("fcs_kernel.hip", "-DFCS_SEGIL_CMAX_ITEMS=100000"),
     ("fcs_engine.cpp", "-DFCS_SEGIL_ANY"),

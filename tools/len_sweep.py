@@ -15,15 +15,15 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
-DEFAULT_LENS = [64, 128, 256, 512, 576, 768, 1000, 1156, 1157, 1250, 1350, 1476, 1477, 1490, 1500, 1514, 1518,
+DEFAULT_LENS = [64, 128, 256, 512, 576, 768, 869, 870, 1000, 1156, 1157, 1250, 1350, 1476, 1477, 1490, 1500, 1514, 1518,
                 1524, 1525, 1536, 1600, 1787, 1900, 1988, 2500, 3000, 4096, 6000, 9000, 9216, 16384, 65536]
 
 
 def family(L):
     """The kernel family a large packed batch of L-byte frames takes (as selected in the library)."""
-    if 1157 <= L <= 1476:
+    if 870 <= L <= 1476:
         return "wide (mid, 6 KiB slots)"
-    if L <= 1156:
+    if L <= 869:
         return "flat"
     if L <= 1495:
         return "wide WD26"
