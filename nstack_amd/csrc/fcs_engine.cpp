@@ -443,6 +443,19 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
     p.zmax = mask_bound(len);
     p.blob = ds->d_blob;
     p.dbg = g_dbg;
+    if (n > g_var_threshold.load(std::memory_order_relaxed) && fcs::fixed_short(p)) {
+        // short frames: one lane per frame, its window in registers (fcs_short_kernel)
+#ifndef FCS_SHORT_WG_PER_CU   // measurement-only: workgroups per CU (2: -6 to -8 %)
+#define FCS_SHORT_WG_PER_CU 1
+#endif
+        const int sgrid = FCS_SHORT_WG_PER_CU * grid_for(ds, (n + 15) / 16, fcs::kWgThreads);
+        if ((n + 63) / 64 >= fcs::kDmaDynMinItemsPerWave * (uint64_t)sgrid * (fcs::kWgThreads / 64)) {
+            const int rc = take_counter(ds, st, p, lease);
+            if (rc) return rc;
+        }
+        HIPTRY(fcs::launch_short(p, sgrid, st), "launching fcs_short_kernel");
+        return 0;
+    }
     if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed) &&
         !(!fcs::fixed_tiny(p) && (fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {   // (slot kernels first)
         // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame

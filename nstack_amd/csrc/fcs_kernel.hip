@@ -1868,6 +1868,105 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 
 
 // ---------------------------------------------------------------------------------------------
+// Short fixed-length frames, one lane per frame (fcs_short_kernel<W>; host-selected by
+// short_wd(): frames of 1..64 B on W = 16 and 97..128 B on W = 32, large batches, any stride).
+// The flat chunk stream (fcs_flat_kernel) spends a 96-B chunk on a 64-B frame: a 24-word chain of
+// which 8 words are masked, the dealing of chunks to lanes, a chunk shift and an LDS atomic. With
+// the length fixed none of that is needed: lane l of a wave's item takes frame 64 item + l, loads
+// the W dwords ending at the frame end (plus the realignment dword) straight into registers, masks
+// the zc = 4 W - len bytes before the frame start (zc is a launch constant: scalar masks) and runs
+// two chains of W / 2 words from INV[zc], merged with A_{2 W}. Its FCS leaves in one coalesced
+// 256-B store per item. Items come from the dispenser (dynamic for large batches).
+// LDS: the 64 KiB table image of fcs_wide_kernel (slice tables; holes 128..131 the merge A_{2 W},
+// 132..135 INV[0..127]); no slots. CPU model: tests/kernel_model.py model_short_frame.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kShortLdsBytes = kDmaRing;   // the table image only
+template <int W>
+__global__ __launch_bounds__(kWgThreads, 1) void fcs_short_kernel(KParams p) {
+    static_assert(W % 8 == 0 && W >= 8 && W <= 32, "two chains of an even word count; merge A_{2 W} = A_{8 (W / 4)}");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kShortLdsBytes];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 2048; i += kWgThreads) {   // slice tables as fcs_dma_kernel
+        const uint32_t v = p.blob[kBlobSlice + 256 * (3 - ((i & 7) >> 1)) + (i >> 3)];
+        u32x4 vv = {v, v, v, v};
+        *reinterpret_cast<u32x4 *>(lds + (uint32_t)(i >> 3) * 256u + (uint32_t)(i & 7) * 16u) = vv;
+    }
+    for (int i = tid; i < 128; i += kWgThreads) {   // the chain merge A_{2 W}
+        const int t = (i >> 4) & 7, e = i & 15;
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kWideMergeHole + (uint32_t)(t >> 1)) + 64u * (uint32_t)(t & 1) +
+                                      4u * (uint32_t)e) = p.blob[kBlobMerge + (W / 4 - 1) * 128 + i];
+    }
+    for (int i = tid; i < (int)kWideWin; i += kWgThreads)
+        *reinterpret_cast<uint32_t *>(lds + dma_hole(kWideInvHole + (uint32_t)i / 32u) + (uint32_t)(i % 32) * 4u) =
+            p.blob[kBlobInvWide + i];
+    init_bad<kWideBad>(lds);
+    __syncthreads();
+
+    const int lane = tid & 63;
+    const uint32_t wave = (uint32_t)__builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    // launch constants: the masked bytes before the frame start and the chain's start value
+    const uint32_t zc = 4u * (uint32_t)W - p.flen;   // 0 .. 4 W - 1 (host: 1 <= len <= 4 W)
+    const uint32_t x0 = lds_rd(lds, dma_hole(kWideInvHole + zc / 32u) + (zc % 32u) * 4u);
+
+    constexpr uint64_t kEnd = Dispenser::kEnd;
+    constexpr int kWaves = kWgThreads / 64;
+    const uint64_t n = p.n;
+    Dispenser D(p.ctr, (n + 63) >> 6, (uint64_t)gridDim.x * kWaves, (uint64_t)blockIdx.x * kWaves + wave, lane,
+                100, 1, 16);
+    for (uint64_t it = D.first(); it != kEnd; it = D.next(it)) {
+        const uint64_t f = 64 * it + (uint64_t)lane;
+        const bool act = f < n;
+        // the window [E - 4 W, E) of this lane's frame; lanes past n read the first frame's
+        const uint64_t E = p.base + (act ? f : 0ull) * p.stride + p.flen;
+        const uint64_t cs = E - 4u * (uint32_t)W;   // may lie before the frame (masked) and before lo4
+        const uint32_t r = (uint32_t)E & 3u;
+        const uint64_t a = cs & ~3ull;
+        uint32_t d[W + 1];
+        if (__any(a < p.lo4)) {   // a window reaching before the arena's first dword: guarded loads
+#pragma unroll
+            for (int q = 0; q <= W; q++) {
+                const uint64_t ad = a + 4u * (uint32_t)q;
+                d[q] = (ad >= p.lo4 && ad + 4 <= p.hi4) ? gload<uint32_t>(ad) : 0u;
+            }
+        } else {
+            LoadPriority lp;
+#pragma unroll
+            for (int q = 0; q < W / 4; q++) {
+                const u32x4a4 x = gload<u32x4a4>(a + 16u * (uint32_t)q);
+                d[4 * q] = x.x;
+                d[4 * q + 1] = x.y;
+                d[4 * q + 2] = x.z;
+                d[4 * q + 3] = x.w;
+            }
+            // dword W matters only when r != 0; then it ends at ceil4(E) <= hi4 (else re-read W - 1)
+            d[W] = gload<uint32_t>(a + (r ? 4u * (uint32_t)W : 4u * (uint32_t)(W - 1)));
+        }
+        uint32_t w[W];
+#pragma unroll
+        for (int i = 0; i < W; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+#pragma unroll
+        for (int i = 0; i < W; i++) {   // the zc bytes before the frame start go (scalar masks)
+            const int t = (int)zc - 4 * i;
+            w[i] &= t >= 4 ? 0u : (t <= 0 ? 0xFFFFFFFFu : (uint32_t)(0xFFFFFFFFull << (8 * t)));
+        }
+        constexpr int CL = W / 2;
+        uint32_t xa = w[0] ^ x0, xb = w[CL];
+#pragma unroll
+        for (int i = 0; i < CL; i++) {
+            xa = step4_l8(lds, xa, i < CL - 1 ? w[i + 1] : 0u, B, SEL);
+            xb = step4_l8(lds, xb, i < CL - 1 ? w[CL + i + 1] : 0u, B, SEL);
+        }
+        const uint32_t v = merge_shift_dma(lds, 0, xa, xb);
+        emit<kWideBad>(p, lds, act, f, ~v);
+    }
+    flush_bad<kWideBad>(p, lds);
+}
+
+// ---------------------------------------------------------------------------------------------
 // Variable-length frames, arena stream (fcs_stream_kernel): batches with offsets, windowed size.
 // CPU model of the decomposition: tests/stream_model.py.
 // The dispenser hands out units of kStUnitFrames frames. A unit whose frames are packed
@@ -2698,6 +2797,16 @@ hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hip
 hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
     hipLaunchKernelGGL((fcs_dma_kernel<2, true>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
+    return hipGetLastError();
+}
+
+hipError_t launch_short(const KParams &p, int grid, hipStream_t st) {
+    (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    switch (short_wd(p.flen)) {
+        case 16: hipLaunchKernelGGL(fcs_short_kernel<16>, dim3(grid), dim3(kWgThreads), 0, st, p); break;
+        case 32: hipLaunchKernelGGL(fcs_short_kernel<32>, dim3(grid), dim3(kWgThreads), 0, st, p); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

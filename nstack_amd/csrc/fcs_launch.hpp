@@ -232,6 +232,19 @@ inline int wide_wd(const KParams &p) {
 #endif
 }
 inline bool fixed_wide(const KParams &p) { return wide_wd(p) != 0; }
+// Short-frame kernel (fcs_short_kernel<W>): fixed lengths of 1..64 and 97..kShortMaxLen bytes, one
+// lane per frame, the W-dword window ending at the frame end loaded into registers (any stride).
+// Against the flat chunk stream (tools/ab.py, one process per length): 60 B +7.6
+// to +8.1 %, 64 B +5.7 to +6.7 %, 100 B +27 %, 128 B +1.6 to +10 %; 65..96 B stay on the flat kernel
+// (74 B +3.9 %, 96 B +-0: one 96-B chunk per frame there is the same work).
+#ifndef FCS_SHORT_MAX   // measurement-only override (0: no short-frame kernel)
+#define FCS_SHORT_MAX 128
+#endif
+constexpr uint32_t kShortMaxLen = FCS_SHORT_MAX;
+__host__ __device__ constexpr int short_wd(uint32_t len) { return len <= 64 ? 16 : (len <= 96 ? 0 : (len <= 128 ? 32 : 0)); }
+inline bool fixed_short(const KParams &p) {
+    return p.flen >= 1 && p.flen <= kShortMaxLen && short_wd(p.flen) != 0 && !fixed_tiny(p);
+}
 inline int fixed_threads(const KParams &p) {
     if (!fixed_tiny(p) && fixed_wide(p)) return wide_threads(wide_wd(p));
     if (fixed_segil(p)) return kSegilWgThreads;
@@ -249,6 +262,7 @@ hipError_t launch_read_stream(const void *p, uint64_t bytes, uint32_t *sink, hip
 hipError_t launch_dma_stream(const KParams &p, int grid, hipStream_t st);
 // load_only: fcs_stream_kernel<true>, the measurement form behind fcs_stream_load_dev
 hipError_t launch_stream(const KParams &p, int grid, hipStream_t st, bool load_only = false);
+hipError_t launch_short(const KParams &p, int grid, hipStream_t st);
 hipError_t launch_tx_store(uint8_t *base, uint64_t stride, const uint32_t *len, const uint32_t *crc,
                            uint64_t n, hipStream_t st);
 
