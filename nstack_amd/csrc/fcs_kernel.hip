@@ -1917,37 +1917,42 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_short_kernel(KParams p) {
     const uint64_t n = p.n;
     Dispenser D(p.ctr, (n + 63) >> 6, (uint64_t)gridDim.x * kWaves, (uint64_t)blockIdx.x * kWaves + wave, lane,
                 100, 1, 16);
-    for (uint64_t it = D.first(); it != kEnd; it = D.next(it)) {
-        const uint64_t f = 64 * it + (uint64_t)lane;
-        const bool act = f < n;
-        // the window [E - 4 W, E) of this lane's frame; lanes past n read the first frame's
-        const uint64_t E = p.base + (act ? f : 0ull) * p.stride + p.flen;
-        const uint64_t cs = E - 4u * (uint32_t)W;   // may lie before the frame (masked) and before lo4
-        const uint32_t r = (uint32_t)E & 3u;
-        const uint64_t a = cs & ~3ull;
+    // one item's window loads (issued one item ahead of its CRC work: two register sets, ping-pong)
+    struct Win {
         uint32_t d[W + 1];
+        uint32_t r;
+    };
+    auto load = [&](uint64_t it, Win &x) {
+        const uint64_t f = 64 * it + (uint64_t)lane;
+        // the window [E - 4 W, E) of this lane's frame; lanes past n read the first frame's
+        const uint64_t E = p.base + (f < n ? f : 0ull) * p.stride + p.flen;
+        const uint64_t a = (E - 4u * (uint32_t)W) & ~3ull;   // may lie before the frame (masked) and before lo4
+        x.r = (uint32_t)E & 3u;
         if (__any(a < p.lo4)) {   // a window reaching before the arena's first dword: guarded loads
 #pragma unroll
             for (int q = 0; q <= W; q++) {
                 const uint64_t ad = a + 4u * (uint32_t)q;
-                d[q] = (ad >= p.lo4 && ad + 4 <= p.hi4) ? gload<uint32_t>(ad) : 0u;
+                x.d[q] = (ad >= p.lo4 && ad + 4 <= p.hi4) ? gload<uint32_t>(ad) : 0u;
             }
         } else {
             LoadPriority lp;
 #pragma unroll
             for (int q = 0; q < W / 4; q++) {
-                const u32x4a4 x = gload<u32x4a4>(a + 16u * (uint32_t)q);
-                d[4 * q] = x.x;
-                d[4 * q + 1] = x.y;
-                d[4 * q + 2] = x.z;
-                d[4 * q + 3] = x.w;
+                const u32x4a4 v = gload<u32x4a4>(a + 16u * (uint32_t)q);
+                x.d[4 * q] = v.x;
+                x.d[4 * q + 1] = v.y;
+                x.d[4 * q + 2] = v.z;
+                x.d[4 * q + 3] = v.w;
             }
             // dword W matters only when r != 0; then it ends at ceil4(E) <= hi4 (else re-read W - 1)
-            d[W] = gload<uint32_t>(a + (r ? 4u * (uint32_t)W : 4u * (uint32_t)(W - 1)));
+            x.d[W] = gload<uint32_t>(a + (x.r ? 4u * (uint32_t)W : 4u * (uint32_t)(W - 1)));
         }
+    };
+    auto crc = [&](uint64_t it, const Win &x) {
+        const uint64_t f = 64 * it + (uint64_t)lane;
         uint32_t w[W];
 #pragma unroll
-        for (int i = 0; i < W; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], r);
+        for (int i = 0; i < W; i++) w[i] = __builtin_amdgcn_alignbyte(x.d[i + 1], x.d[i], x.r);
 #pragma unroll
         for (int i = 0; i < W; i++) {   // the zc bytes before the frame start go (scalar masks)
             const int t = (int)zc - 4 * i;
@@ -1961,7 +1966,33 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_short_kernel(KParams p) {
             xb = step4_l8(lds, xb, i < CL - 1 ? w[CL + i + 1] : 0u, B, SEL);
         }
         const uint32_t v = merge_shift_dma(lds, 0, xa, xb);
-        emit<kWideBad>(p, lds, act, f, ~v);
+        emit<kWideBad>(p, lds, f < n, f, ~v);
+    };
+#ifdef FCS_SHORT_NO_PIPE   // measurement-only: each item's loads right before its CRC work
+    constexpr bool kPipe = false;
+#else
+    constexpr bool kPipe = W <= 16;   // two 33-dword register sets at W = 32 spill
+#endif
+    if constexpr (!kPipe) {
+        for (uint64_t it = D.first(); it != kEnd; it = D.next(it)) {
+            Win x;
+            load(it, x);
+            crc(it, x);
+        }
+    } else {
+    Win xa, xb;
+    uint64_t it = D.first();
+    if (it != kEnd) load(it, xa);
+    while (it != kEnd) {   // wave-uniform
+        const uint64_t i1 = D.next(it);
+        if (i1 != kEnd) load(i1, xb);
+        crc(it, xa);
+        if (i1 == kEnd) break;
+        const uint64_t i2 = D.next(i1);
+        if (i2 != kEnd) load(i2, xa);
+        crc(i1, xb);
+        it = i2;
+    }
     }
     flush_bad<kWideBad>(p, lds);
 }

@@ -234,9 +234,10 @@ inline int wide_wd(const KParams &p) {
 inline bool fixed_wide(const KParams &p) { return wide_wd(p) != 0; }
 // Short-frame kernel (fcs_short_kernel<W>): fixed lengths of 1..64 and 97..kShortMaxLen bytes, one
 // lane per frame, the W-dword window ending at the frame end loaded into registers (any stride).
-// Against the flat chunk stream (tools/ab.py, one process per length): 60 B +7.6
-// to +8.1 %, 64 B +5.7 to +6.7 %, 100 B +27 %, 128 B +1.6 to +10 %; 65..96 B stay on the flat kernel
-// (74 B +3.9 %, 96 B +-0: one 96-B chunk per frame there is the same work).
+// Against the flat chunk stream (tools/ab.py, one process per length): 60 B
+// +11.5 %, 64 B +10.4 %, 32 B +10.2 % (with the loads one item ahead), 100 B +27 %, 128 B +1.6 to
+// +10 %; 65..96 B stay on the flat kernel (74 B +3.9 %, 96 B +-0: one 96-B chunk per frame there is
+// the same work).
 #ifndef FCS_SHORT_MAX   // measurement-only override (0: no short-frame kernel)
 #define FCS_SHORT_MAX 128
 #endif

@@ -36,6 +36,7 @@ VARIANTS = [
     ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1537"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MID_MIN=0"),
     ("fcs_engine.cpp", "-DFCS_SHORT_MAX=0 -DFCS_SHORT_WG_PER_CU=2"),
+    ("fcs_kernel.hip", "-DFCS_SHORT_NO_PIPE"),
     ("fcs_kernel.hip", "-DFCS_WIDE_MID_WD_MIN=11"),
     ("fcs_engine.cpp", "-DFCS_WIDE_NO_PRE"),
     ("fcs_kernel.hip", "-DFCS_SEGIL_CMAX_ITEMS=100000"),
