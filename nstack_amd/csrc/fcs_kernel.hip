@@ -1158,11 +1158,12 @@ __host__ __device__ constexpr int wide_cl0(int wd) {
     return wd == 32 ? 16 : (wd == 30 ? 14 : (wd == 26 ? 12 : wd - 2 * (wd / 4)));
 }
 
-template <int WD>
+template <int WD, int G>
 __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds, int tid) {
     constexpr int NT = wide_threads(WD);
-    static_assert(WD == 26 || WD == 30 || WD == 32 || wide_mid_ok(WD), "window width");
-    constexpr uint32_t kLane = WD == 32 ? kBlobLaneWide
+    static_assert(G == 16 ? (WD == 26 || WD == 30 || WD == 32 || wide_mid_ok(WD)) : (G == 8 && wide8_ok(WD)), "window width");
+    constexpr uint32_t kLane = G == 8 ? kBlobLane8 + (uint32_t)(WD - kWide8Min) * 4096u
+                             : WD == 32 ? kBlobLaneWide
                                         : (WD == 30 ? kBlobLaneWide30
                                                     : (WD == 26 ? kBlobLaneWide26 : kBlobLaneMid + (uint32_t)(WD - kWideMidMin) * 4096u));
     constexpr int kMergeK = 2 * (WD - wide_cl0(WD)) / 4;   // A_{8 k} with 8 k = 4 (WD - CL0)
@@ -1211,20 +1212,23 @@ __device__ __forceinline__ void wide_dma_item(const uint8_t *slot, uint64_t src,
     }
 }
 
-template <int WD>
+// G: lanes per frame (16: four frames per item; 8: eight frames per item, eight windows each).
+template <int WD, int G = 16>
 __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p) {
     constexpr uint32_t kWin = wide_win(WD), kStep = wide_step(WD), kSlot = wide_slot(WD);
     constexpr uint32_t kLdsB = wide_lds_bytes(WD);
     constexpr int kWaves = wide_threads(WD) / 64, CL0 = wide_cl0(WD);
+    static_assert(G == 16 || G == 8, "lanes per frame");
+    constexpr int kFr = 64 / G;   // frames per item
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsB];
     const int tid = threadIdx.x;
-    stage_wide_tables<WD>(p, lds, tid);
+    stage_wide_tables<WD, G>(p, lds, tid);
     init_bad<kWideBad>(lds);
     __syncthreads();
 
     const int lane = tid & 63;
-    const int c = lane & (kGroup - 1);     // window index back from the frame end
-    const int g = lane >> 4;               // frame of the item
+    const int c = lane & (G - 1);          // window index back from the frame end
+    const int g = lane / G;                // frame of the item
     const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kSlot;
     const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
@@ -1234,7 +1238,7 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
     const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
 
     // launch constants: the front lane, its leading bytes, the words they reach (scalars)
-    const int cf = (int)((p.flen - 1u) / kStep) < 15 ? (int)((p.flen - 1u) / kStep) : 15;
+    const int cf = (int)((p.flen - 1u) / kStep) < G - 1 ? (int)((p.flen - 1u) / kStep) : G - 1;
     const uint32_t zc = kStep * (uint32_t)cf + kWin - p.flen;   // 0 .. kWin - 1
     const uint32_t mwords = (zc + 3u) / 4u;
     const bool live = c <= cf, front = c == cf;
@@ -1251,23 +1255,23 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
         const uint64_t a = S & ~15ull;
         return a < lo16 ? lo16 : (a > smax ? smax : a);
     };
-    auto item_start = [&](uint64_t i) { return p.base + 4 * i * p.stride; };
+    auto item_start = [&](uint64_t i) { return p.base + (uint64_t)kFr * i * p.stride; };
     auto dma_of = [&](uint64_t i) {
         const uint64_t S = item_start(i), src = slot_src(S);
-        const uint64_t e = S + 3 * p.stride + p.flen + 4 - src;
+        const uint64_t e = S + (uint64_t)(kFr - 1) * p.stride + p.flen + 4 - src;
         wide_dma_item<WD>(slot, src, lane, (uint32_t)(e < (uint64_t)kSlot ? e : (uint64_t)kSlot));
     };
 
     constexpr uint64_t kEnd = Dispenser::kEnd;
-    Dispenser D(p.ctr, (p.n + 3) >> 2, (uint64_t)gridDim.x * kWaves,
+    Dispenser D(p.ctr, (p.n + kFr - 1) / kFr, (uint64_t)gridDim.x * kWaves,
                 (uint64_t)blockIdx.x * kWaves + (uint64_t)wave, lane, FCS_DMA_DYN_PCT, 4, FCS_DMA_CHUNK_MAX);
-    D.align = 16;   // chunks start on 16-item groups: whole 256-B result runs
+    D.align = G;   // chunks start on G-item groups: whole 256-B result runs
     uint64_t it = D.first();
     if (it != kEnd) dma_of(it);
-    uint32_t cbuf = 0;    // FCSs of the current run of items, lane 4 (item & 15) + frame
+    uint32_t cbuf = 0;    // FCSs of the current run of items, lane kFr (item mod G) + frame
     uint64_t cmask = 0;   // lanes of cbuf that hold one (wave-uniform)
     while (it != kEnd) {   // wave-uniform
-        const uint64_t f = 4 * it;
+        const uint64_t f = (uint64_t)kFr * it;
         const uint64_t S = item_start(it);
         const uint64_t src = slot_src(S);
         __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot DMA has landed
@@ -1327,15 +1331,22 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
         }
         const uint32_t mv = merge_shift_dma(lds, 0, xa, xb);
         uint32_t v = live ? lane_shift_dma(lds, mv, lanebase) : 0u;
-        v = row_xor(v);
+        if constexpr (G == 16) {
+            v = row_xor(v);
+        } else {   // the eight-lane half-row sums (row_xor's first three steps)
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
+            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+        }
         {
-            const uint32_t k = (uint32_t)(it & 15u);
-            const uint32_t vq = (uint32_t)__shfl((int)~v, (lane & 3) * kGroup);   // frame (lane & 3)'s FCS
-            if ((uint32_t)(lane >> 2) == k) cbuf = vq;
-            const uint64_t livem = f + 4 <= p.n ? 0xFull : ((1ull << (p.n - f)) - 1ull);
-            cmask |= livem << (4 * k);
-            if (k == 15 || nxt != it + 1) {
-                emit<kWideBad>(p, lds, (cmask >> lane) & 1ull, 4 * (it & ~15ull) + (uint64_t)lane, cbuf);
+            const uint32_t k = (uint32_t)(it & (uint64_t)(G - 1));
+            const uint32_t vq = (uint32_t)__shfl((int)~v, (lane % kFr) * G);   // frame (lane mod kFr)'s FCS
+            if ((uint32_t)(lane / kFr) == k) cbuf = vq;
+            constexpr uint64_t kAll = (1ull << kFr) - 1ull;
+            const uint64_t livem = f + kFr <= p.n ? kAll : ((1ull << (p.n - f)) - 1ull);
+            cmask |= livem << (kFr * k);
+            if (k == (uint32_t)(G - 1) || nxt != it + 1) {
+                emit<kWideBad>(p, lds, (cmask >> lane) & 1ull, (uint64_t)kFr * (it & ~(uint64_t)(G - 1)) + (uint64_t)lane, cbuf);
                 cmask = 0;
             }
         }
@@ -2750,6 +2761,15 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
         } else {
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
         }
+    } else if (!tiny && fixed_wide8(p)) {
+#define FCS_WIDE8(W) \
+    case W: hipLaunchKernelGGL((fcs_wide_kernel<W, 8>), dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
+        switch (wide8_wd(p)) {
+            FCS_WIDE8(11) FCS_WIDE8(12) FCS_WIDE8(14) FCS_WIDE8(15) FCS_WIDE8(16) FCS_WIDE8(18) FCS_WIDE8(19)
+            FCS_WIDE8(20) FCS_WIDE8(22) FCS_WIDE8(23) FCS_WIDE8(24) FCS_WIDE8(26) FCS_WIDE8(27)
+            default: hipLaunchKernelGGL((fcs_wide_kernel<28, 8>), dim3(grid), dim3(wide_threads(28)), 0, st, p);
+        }
+#undef FCS_WIDE8
     } else if (!tiny && fixed_wide(p)) {
         const int wd = wide_wd(p);
 #define FCS_WIDE(W) \

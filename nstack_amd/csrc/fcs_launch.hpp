@@ -232,6 +232,41 @@ inline int wide_wd(const KParams &p) {
 #endif
 }
 inline bool fixed_wide(const KParams &p) { return wide_wd(p) != 0; }
+// Eight-lane groups (fcs_wide_kernel<WD, 8>): fixed lengths kWide8MinLen..wide8_cover(28) bytes,
+// eight frames per item, the narrowest bank-safe WD (11..28) whose eight windows cover the frame,
+// when the item's eight frames fit the width's slot.
+#ifndef FCS_WIDE8_MIN   // measurement-only override of the band's lower end (0: no eight-lane groups)
+#define FCS_WIDE8_MIN 400
+#endif
+constexpr uint32_t kWide8MinLen = FCS_WIDE8_MIN;
+// The windows' LDS reads: the most live lanes of one 32-lane half on one dword bank (every window
+// word shifts all lanes' banks alike, so word 0 stands for all). Four frames share a half; strides
+// that put them on the same bank phase (e.g. 512 or 768 B) give 4-way conflicts, which measured
+// slower than the flat kernel (512 B -4.6 %, 768 B -3.6 %; 741 B, 3-way, -1.6 %).
+inline int wide8_bank_load(const KParams &p, int wd) {
+    const uint32_t step = wide_step(wd);
+    const uint32_t cf = (p.flen - 1u) / step < 7u ? (p.flen - 1u) / step : 7u;
+    int worst = 0;
+    for (int half = 0; half < 2; half++) {
+        int cnt[32] = {0};
+        for (int l = 32 * half; l < 32 * half + 32; l++) {
+            const uint32_t c = (uint32_t)l & 7u, g = (uint32_t)l >> 3;
+            if (c > cf) continue;
+            const uint64_t x = p.base + g * p.stride + p.flen - step * c - wide_win(wd);
+            const int b = (int)((x >> 2) & 31u);
+            if (++cnt[b] > worst) worst = cnt[b];
+        }
+    }
+    return worst;
+}
+inline int wide8_wd(const KParams &p) {
+    if (!kWide8MinLen || p.flen < kWide8MinLen || p.flen > wide8_cover(28) || p.stride > 2048) return 0;
+    int wd = kWide8Min;
+    while (!wide8_ok(wd) || wide8_cover(wd) < p.flen) wd++;
+    return (7 * p.stride + p.flen <= wide_slot(wd) - 18 && p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(wd) &&
+            wide8_bank_load(p, wd) <= 2) ? wd : 0;
+}
+inline bool fixed_wide8(const KParams &p) { return wide8_wd(p) != 0; }
 // Short-frame kernel (fcs_short_kernel<W>): fixed lengths of 1..64 and 97..kShortMaxLen bytes, one
 // lane per frame, the W-dword window ending at the frame end loaded into registers (any stride).
 // Against the flat chunk stream (tools/ab.py, one process per length): 60 B
@@ -247,6 +282,7 @@ inline bool fixed_short(const KParams &p) {
     return p.flen >= 1 && p.flen <= kShortMaxLen && short_wd(p.flen) != 0 && !fixed_tiny(p);
 }
 inline int fixed_threads(const KParams &p) {
+    if (!fixed_tiny(p) && fixed_wide8(p)) return wide_threads(wide8_wd(p));
     if (!fixed_tiny(p) && fixed_wide(p)) return wide_threads(wide_wd(p));
     if (fixed_segil(p)) return kSegilWgThreads;
     if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;

@@ -102,6 +102,12 @@ __host__ __device__ constexpr uint32_t wide_slot(int wd) { return wd == 32 ? 819
 constexpr int kWideMidMin = FCS_WIDE_MID_WD_MIN, kWideMidMax = 24;
 static_assert(kWideMidMin >= 11 && kWideMidMin <= 20, "mid-length widths the launch switch instantiates");
 __host__ __device__ constexpr bool wide_mid_ok(int wd) { return wd >= kWideMidMin && wd <= kWideMidMax && (wd - 1) % 4 != 0; }
+// Eight-lane groups (round 4): eight frames per wave item, eight windows per frame, the bank-safe
+// WD = 11 .. 28 dwords (cover 32 WD - 28 = 324 .. 868 B); 6 KiB slots up to WD 24, 7 KiB (13 waves)
+// above.
+constexpr int kWide8Min = 11, kWide8Max = 28;
+__host__ __device__ constexpr uint32_t wide8_cover(int wd) { return 7u * wide_step(wd) + wide_win(wd); }
+__host__ __device__ constexpr bool wide8_ok(int wd) { return wd >= kWide8Min && wd <= kWide8Max && (wd - 1) % 4 != 0; }
 constexpr uint32_t kWideCover = wide_cover(32);                  // 1988
 constexpr uint32_t kWideCover26 = wide_cover(26);                // 1604
 constexpr uint32_t kWideCover30 = wide_cover(30);                // 1860
@@ -132,7 +138,10 @@ constexpr uint32_t kBlobInvWide = kBlobLaneWide30 + 8 * 16 * 32;
 // Mid-length wide kernels: lane tables A_{(4 WD - 4) c} for WD = kWideMidMin..kWideMidMax in the
 // LDS-DMA layout [8][16][32] (one set per width, unused widths included so the offsets stay simple).
 constexpr uint32_t kBlobLaneMid = kBlobInvWide + kWideWin;
-constexpr uint32_t kBlobWords = kBlobLaneMid + (kWideMidMax - kWideMidMin + 1) * 8 * 16 * 32;
+// Eight-lane groups: lane tables A_{(4 WD - 4) (slot mod 8)} for WD = kWide8Min..kWide8Max (one set
+// per width, unused widths included).
+constexpr uint32_t kBlobLane8 = kBlobLaneMid + (kWideMidMax - kWideMidMin + 1) * 8 * 16 * 32;
+constexpr uint32_t kBlobWords = kBlobLane8 + (kWide8Max - kWide8Min + 1) * 8 * 16 * 32;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -242,6 +251,12 @@ struct Tables {
                 for (int t = 0; t < 8; t++)
                     for (int e = 0; e < 16; e++)
                         b[kBlobLaneMid + (wd - kWideMidMin) * 4096 + (t * 16 + e) * 32 + slot] = nt[t][e];
+            }
+        for (int wd = kWide8Min; wd <= kWide8Max; wd++)   // eight-lane groups
+            for (int slot = 0; slot < 32; slot++) {
+                nibble_table((long)wide_step(wd) * (slot % 8), nt);
+                for (int t = 0; t < 8; t++)
+                    for (int e = 0; e < 16; e++) b[kBlobLane8 + (wd - kWide8Min) * 4096 + (t * 16 + e) * 32 + slot] = nt[t][e];
             }
         return b;
     }

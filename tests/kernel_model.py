@@ -328,7 +328,9 @@ WIDE_COVER = 124 * 15 + WIDE_WIN   # 1988
 WIDE_MERGE_HOLE, WIDE_INV_HOLE = 128, 132
 WIDE_MID = [wd for wd in range(15, 25) if (wd - 1) % 4]   # mid-length widths (fcs_tables.hpp wide_mid_ok)
 BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 15..24
-WIDE_CL0 = {32: 16, 30: 14, 26: 12, **{wd: wd - 2 * (wd // 4) for wd in WIDE_MID}}   # chain 0's words
+WIDE8 = [wd for wd in range(11, 29) if (wd - 1) % 4]    # eight-lane group widths (fcs_tables.hpp wide8_ok)
+BLOB_LANE8 = BLOB_LANE_MID + (24 - WIDE_MID[0] + 1) * 4096   # kBlobLane8: one set per WD 11..28
+WIDE_CL0 = {**{wd: wd - 2 * (wd // 4) for wd in WIDE_MID + WIDE8}, 32: 16, 30: 14, 26: 12}   # chain 0's words
 
 
 def wide_end_off(c, wd=32):
@@ -343,17 +345,28 @@ def wide_cover(wd):
     return 15 * (4 * wd - 4) + 4 * wd
 
 
+def wide8_cover(wd):
+    return 7 * (4 * wd - 4) + 4 * wd
+
+
+def wide8_wd(flen):
+    """The width the host picks for an eight-lane-group frame (fcs_launch.hpp wide8_wd)."""
+    return next(wd for wd in WIDE8 if wide8_cover(wd) >= flen)
+
+
 def wide_mid_wd(flen):
     """The width the host picks for a mid-length frame (fcs_launch.hpp wide_mid_wd)."""
     return next(wd for wd in WIDE_MID if wide_cover(wd) >= flen)
 
 
-def build_lds_wide(blob, wd=32):
+def build_lds_wide(blob, wd=32, G=16):
     """fcs_wide_kernel<WD>'s 64 KiB table image: the slice tables as fcs_dma_kernel's; holes 16t+n
     the lane tables A_{(4 WD - 4) c}; holes 128..131 the chain merge A_{4 (WD - CL0)}; holes
     132..135 INV[0..127]."""
     lane_blob = {32: BLOB_LANE_WIDE, 30: BLOB_LANE_WIDE30, 26: BLOB_LANE_WIDE26}.get(wd)
-    if lane_blob is None:
+    if G == 8:
+        lane_blob = BLOB_LANE8 + (wd - 11) * 4096
+    elif lane_blob is None:
         lane_blob = BLOB_LANE_MID + (wd - WIDE_MID[0]) * 4096
     k = (4 * (wd - WIDE_CL0[wd])) // 8
     lds = np.zeros(65536 // 4, dtype=np.uint32)
@@ -370,14 +383,14 @@ def build_lds_wide(blob, wd=32):
     return lds
 
 
-def wide_front(flen, wd=32):
+def wide_front(flen, wd=32, G=16):
     """Front lane cf (the last lane whose window reaches into the frame) and its leading bytes zc."""
     step = 4 * wd - 4
-    cf = min(15, (flen - 1) // step)
+    cf = min(G - 1, (flen - 1) // step)
     return cf, step * cf + 4 * wd - flen
 
 
-def model_wide_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f: int, garbage: bytes, wd=32):
+def model_wide_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, f: int, garbage: bytes, wd=32, G=16):
     """The four FCS values fcs_wide_kernel computes for the wave item whose first frame is f: lanes
     c <= cf are live; each masks its first word (its neighbour's last) except the front lane, which
     masks its zc leading bytes and starts from INV[zc]; two 16-word chains merged with A_64; lane
@@ -393,12 +406,12 @@ def model_wide_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, 
     img = bytearray(garbage[:pad]) + bytearray(slot) + bytearray(garbage[pad:pad + 64])
     chunk = mem[src:src + slot]
     img[pad:pad + len(chunk)] = chunk
-    cf, zc = wide_front(flen, wd)
+    cf, zc = wide_front(flen, wd, G)
     out = []
-    for g in range(4):
+    for g in range(64 // G):
         v = 0
         for c in range(cf + 1):
-            lane = 16 * g + c
+            lane = G * g + c
             x = (S - src) + g * stride + flen - wide_end_off(c, wd) - win
             r = x & 3
             a = pad + (x & ~3)

@@ -176,7 +176,8 @@ def test_segil_decomposition_model(lds_dma, L):
 @pytest.fixture(scope="module")
 def lds_wide():
     blob = na.tables_blob()
-    return {wd: km.build_lds_wide(blob, wd) for wd in (26, 30, 32, *km.WIDE_MID)}
+    return {**{wd: km.build_lds_wide(blob, wd) for wd in (26, 30, 32, *km.WIDE_MID)},
+            **{(wd, 8): km.build_lds_wide(blob, wd, 8) for wd in km.WIDE8}}
 
 
 @pytest.mark.parametrize("flen,extra,wd", [(1525, 0, 32), (1530, 3, 32), (1536, 0, 32), (1537, 1, 32), (1600, 0, 32),
@@ -212,6 +213,37 @@ def test_wide_kernel_model(lds_wide, flen, extra, wd):
                 if f + g < n:
                     S = b0 + (f + g) * stride
                     assert got[g] == zlib.crc32(mem[S:S + flen]), (flen, extra, b0, f + g)
+
+
+@pytest.mark.parametrize("flen,extra", [(300, 0), (324, 1), (325, 0), (356, 0), (400, 0), (421, 3), (452, 0),
+                                        (484, 0), (485, 1), (548, 0), (580, 2), (612, 2), (613, 0), (676, 0),
+                                        (700, 5), (708, 0), (740, 0), (741, 0), (800, 7), (836, 0), (868, 0),
+                                        (740, (6126 - 740) // 7 - 740), (868, (7150 - 868) // 7 - 868)])
+def test_wide8_kernel_model(lds_wide, flen, extra):
+    """fcs_wide_kernel<WD, 8>: eight frames per item, eight windows per frame (front lane
+    cf = min(7, (len - 1) / (4 WD - 4))), the lane tables A_{(4 WD - 4) (slot mod 8)}, the
+    eight-lane sums; replayed on the CPU for every item of small batches at four base alignments
+    (the last cases: the largest stride a 6 KiB / 7 KiB slot takes), against zlib."""
+    wd = km.wide8_wd(flen)
+    stride = flen + extra
+    rng = random.Random(flen * 41 + extra)
+    garbage = bytes(rng.randrange(256) for _ in range(2048 + 64))
+    for b0 in (0, 1, 2, 3):
+        n = max(19, 2 * km.wide_slot(wd) // stride + 3)   # the host takes arenas of two slots or more
+        mem = bytes(rng.randrange(256) for _ in range(b0 + n * stride + 64))
+        for f in range(0, n, 8):
+            got = km.model_wide_item(lds_wide[(wd, 8)], mem, b0, stride, flen, n, f, garbage, wd, 8)
+            for g in range(8):
+                if f + g < n:
+                    S = b0 + (f + g) * stride
+                    assert got[g] == zlib.crc32(mem[S:S + flen]), (flen, extra, b0, f + g)
+
+
+def test_wide8_windows_bank_distinct():
+    """The eight windows of a frame in fcs_wide_kernel<WD, 8> start on eight distinct dword banks."""
+    for wd in km.WIDE8:
+        for E in range(0, 64, 4):
+            assert len({((E - km.wide_end_off(c, wd) - 4 * wd) // 4) % 32 for c in range(8)}) == 8
 
 
 def test_wide_windows_bank_distinct():
