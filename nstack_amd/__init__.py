@@ -349,7 +349,7 @@ def shard_plan(n: int, parts: int, lengths=None):
 
 def tables_blob():
     import numpy as np
-    buf = np.zeros(1 << 18, dtype=np.uint32)   # the blob is kBlobWords (about 130 k) words
+    buf = np.zeros(1 << 19, dtype=np.uint32)   # the blob is kBlobWords (about 261 k) words
     n = _check(load().fcs_tables_blob(buf.ctypes.data, buf.size), "fcs_tables_blob")
     return buf[:n].copy()
 

@@ -457,7 +457,7 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         return 0;
     }
     if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed) &&
-        !(!fcs::fixed_tiny(p) && (fcs::fixed_wide8(p) || fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {   // (slot kernels first)
+        !(!fcs::fixed_tiny(p) && (fcs::fixed_wide4(p) || fcs::fixed_wide8(p) || fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {
         // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame
         // instead of a 16-lane quarter-wave (len == null tells it the length is p.flen)
         p.zmax = fcs::kChunkBytes;
@@ -470,8 +470,8 @@ int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, 
         return 0;
     }
     const int grid = grid_for(ds, n, fcs::fixed_threads(p));
-    if (!fcs::fixed_tiny(p) && (fcs::fixed_wide8(p) || fcs::fixed_wide(p))) {   // wide LDS-DMA kernels
-        const uint64_t fr = fcs::fixed_wide8(p) ? 8 : 4;   // frames per item
+    if (!fcs::fixed_tiny(p) && (fcs::fixed_wide4(p) || fcs::fixed_wide8(p) || fcs::fixed_wide(p))) {   // wide LDS-DMA kernels
+        const uint64_t fr = fcs::fixed_wide4(p) ? 16 : (fcs::fixed_wide8(p) ? 8 : 4);   // frames per item
         const uint64_t items = (n + fr - 1) / fr, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);
         if (items >= fcs::kDmaDynMinItemsPerWave * waves) {
             const int rc = take_counter(ds, st, p, lease);
@@ -1488,7 +1488,7 @@ const char *fcs_last_error(void) { return g_last_error.c_str(); }
 const char *fcs_engine_version(void) {
     return "nstack-fcs 0.6 gfx950: quarter-wave/frame, 96B lane windows as 2 slice-by-4 chains, v_perm "
            "addressing, DPP reduce; 1496-1524B: LDS-DMA (nt global_load_lds) 6KiB slot/wave, 16 waves/CU, "
-           "32KiB 8-replica tables, guided dynamic items; 400-868B: 8 lanes x 44-112B windows/frame, 870-1476B: 16 lanes x 60-96B windows, 6-7KiB LDS-DMA slots; <=64B, 97-128B: lane/frame; 1477-1495B, 1525-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
+           "32KiB 8-replica tables, guided dynamic items; 130-399B: 4 lanes x 36-104B, 400-868B: 8 lanes x 44-112B windows/frame, 870-1476B: 16 lanes x 60-96B windows, 6-7KiB LDS-DMA slots; <=64B, 97-128B: lane/frame; 1477-1495B, 1525-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
            ">1524B otherwise: frame-interleaved LDS-DMA segments; var: "
            "packed 64-1536B units as an arena stream (4KiB LDS-DMA items, taps at frame boundaries, XOR "
            "scan), other units as a flat chunk stream per 64-frame window";

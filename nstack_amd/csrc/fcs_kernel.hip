@@ -1161,8 +1161,10 @@ __host__ __device__ constexpr int wide_cl0(int wd) {
 template <int WD, int G>
 __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds, int tid) {
     constexpr int NT = wide_threads(WD);
-    static_assert(G == 16 ? (WD == 26 || WD == 30 || WD == 32 || wide_mid_ok(WD)) : (G == 8 && wide8_ok(WD)), "window width");
-    constexpr uint32_t kLane = G == 8 ? kBlobLane8 + (uint32_t)(WD - kWide8Min) * 4096u
+    static_assert(G == 16 ? (WD == 26 || WD == 30 || WD == 32 || wide_mid_ok(WD))
+                          : (G == 8 ? wide8_ok(WD) : (G == 4 && wide4_ok(WD))), "window width");
+    constexpr uint32_t kLane = G == 4 ? kBlobLane4 + (uint32_t)(WD - kWide4Min) * 4096u
+                             : G == 8 ? kBlobLane8 + (uint32_t)(WD - kWide8Min) * 4096u
                              : WD == 32 ? kBlobLaneWide
                                         : (WD == 30 ? kBlobLaneWide30
                                                     : (WD == 26 ? kBlobLaneWide26 : kBlobLaneMid + (uint32_t)(WD - kWideMidMin) * 4096u));
@@ -1218,7 +1220,7 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
     constexpr uint32_t kWin = wide_win(WD), kStep = wide_step(WD), kSlot = wide_slot(WD);
     constexpr uint32_t kLdsB = wide_lds_bytes(WD);
     constexpr int kWaves = wide_threads(WD) / 64, CL0 = wide_cl0(WD);
-    static_assert(G == 16 || G == 8, "lanes per frame");
+    static_assert(G == 16 || G == 8 || G == 4, "lanes per frame");
     constexpr int kFr = 64 / G;   // frames per item
     __shared__ __attribute__((aligned(16))) uint8_t lds[kLdsB];
     const int tid = threadIdx.x;
@@ -1333,10 +1335,11 @@ __global__ __launch_bounds__(wide_threads(WD), 1) void fcs_wide_kernel(KParams p
         uint32_t v = live ? lane_shift_dma(lds, mv, lanebase) : 0u;
         if constexpr (G == 16) {
             v = row_xor(v);
-        } else {   // the eight-lane half-row sums (row_xor's first three steps)
+        } else {   // the eight-lane half-row (or four-lane quad) sums: row_xor's first steps
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad [1,0,3,2]
             v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   // quad [2,3,0,1]
-            v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
+            if constexpr (G == 8)
+                v ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x141, 0xF, 0xF, false);  // row_half_mirror
         }
         {
             const uint32_t k = (uint32_t)(it & (uint64_t)(G - 1));
@@ -2761,6 +2764,16 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
         } else {
             hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
         }
+    } else if (!tiny && fixed_wide4(p)) {
+#define FCS_WIDE4(W) \
+    case W: hipLaunchKernelGGL((fcs_wide_kernel<W, 4>), dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
+        switch (wide4_wd(p)) {
+            FCS_WIDE4(9) FCS_WIDE4(10) FCS_WIDE4(11) FCS_WIDE4(12) FCS_WIDE4(13) FCS_WIDE4(14) FCS_WIDE4(15)
+            FCS_WIDE4(16) FCS_WIDE4(18) FCS_WIDE4(19) FCS_WIDE4(20) FCS_WIDE4(21) FCS_WIDE4(22) FCS_WIDE4(23)
+            FCS_WIDE4(24) FCS_WIDE4(25)
+            default: hipLaunchKernelGGL((fcs_wide_kernel<26, 4>), dim3(grid), dim3(wide_threads(26)), 0, st, p);
+        }
+#undef FCS_WIDE4
     } else if (!tiny && fixed_wide8(p)) {
 #define FCS_WIDE8(W) \
     case W: hipLaunchKernelGGL((fcs_wide_kernel<W, 8>), dim3(grid), dim3(wide_threads(W)), 0, st, p); break;

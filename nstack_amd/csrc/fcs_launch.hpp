@@ -243,14 +243,14 @@ constexpr uint32_t kWide8MinLen = FCS_WIDE8_MIN;
 // word shifts all lanes' banks alike, so word 0 stands for all). Four frames share a half; strides
 // that put them on the same bank phase (e.g. 512 or 768 B) give 4-way conflicts, which measured
 // slower than the flat kernel (512 B -4.6 %, 768 B -3.6 %; 741 B, 3-way, -1.6 %).
-inline int wide8_bank_load(const KParams &p, int wd) {
+inline int wide_bank_load(const KParams &p, int wd, uint32_t G) {
     const uint32_t step = wide_step(wd);
-    const uint32_t cf = (p.flen - 1u) / step < 7u ? (p.flen - 1u) / step : 7u;
+    const uint32_t cf = (p.flen - 1u) / step < G - 1u ? (p.flen - 1u) / step : G - 1u;
     int worst = 0;
     for (int half = 0; half < 2; half++) {
         int cnt[32] = {0};
         for (int l = 32 * half; l < 32 * half + 32; l++) {
-            const uint32_t c = (uint32_t)l & 7u, g = (uint32_t)l >> 3;
+            const uint32_t c = (uint32_t)l % G, g = (uint32_t)l / G;
             if (c > cf) continue;
             const uint64_t x = p.base + g * p.stride + p.flen - step * c - wide_win(wd);
             const int b = (int)((x >> 2) & 31u);
@@ -264,9 +264,26 @@ inline int wide8_wd(const KParams &p) {
     int wd = kWide8Min;
     while (!wide8_ok(wd) || wide8_cover(wd) < p.flen) wd++;
     return (7 * p.stride + p.flen <= wide_slot(wd) - 18 && p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(wd) &&
-            wide8_bank_load(p, wd) <= 2) ? wd : 0;
+            wide_bank_load(p, wd, 8) <= 2) ? wd : 0;
 }
 inline bool fixed_wide8(const KParams &p) { return wide8_wd(p) != 0; }
+// Four-lane groups (fcs_wide_kernel<WD, 4>): fixed lengths kWide4MinLen..kWide8MinLen - 1, sixteen
+// frames per item, the narrowest width (9..26, not 17) whose four windows cover the frame, when the
+// item's sixteen frames fit the width's slot and the 32-lane halves' bank load is at most 2.
+#ifndef FCS_WIDE4_MIN   // measurement-only override of the band's lower end (0: no four-lane groups)
+#define FCS_WIDE4_MIN 130
+#endif
+constexpr uint32_t kWide4MinLen = FCS_WIDE4_MIN;
+inline int wide4_wd(const KParams &p) {
+    if (!kWide4MinLen || p.flen < kWide4MinLen || p.flen > wide4_cover(kWide4Max) || p.stride > 2048 ||
+        (kWide8MinLen && p.flen >= kWide8MinLen))
+        return 0;
+    int wd = kWide4Min;
+    while (!wide4_ok(wd) || wide4_cover(wd) < p.flen) wd++;
+    return (15 * p.stride + p.flen <= wide_slot(wd) - 18 && p.hi4 - p.lo4 >= 2 * (uint64_t)wide_slot(wd) &&
+            wide_bank_load(p, wd, 4) <= 2) ? wd : 0;
+}
+inline bool fixed_wide4(const KParams &p) { return wide4_wd(p) != 0; }
 // Short-frame kernel (fcs_short_kernel<W>): fixed lengths of 1..64 and 97..kShortMaxLen bytes, one
 // lane per frame, the W-dword window ending at the frame end loaded into registers (any stride).
 // Against the flat chunk stream (tools/ab.py, one process per length): 60 B
@@ -282,6 +299,7 @@ inline bool fixed_short(const KParams &p) {
     return p.flen >= 1 && p.flen <= kShortMaxLen && short_wd(p.flen) != 0 && !fixed_tiny(p);
 }
 inline int fixed_threads(const KParams &p) {
+    if (!fixed_tiny(p) && fixed_wide4(p)) return wide_threads(wide4_wd(p));
     if (!fixed_tiny(p) && fixed_wide8(p)) return wide_threads(wide8_wd(p));
     if (!fixed_tiny(p) && fixed_wide(p)) return wide_threads(wide_wd(p));
     if (fixed_segil(p)) return kSegilWgThreads;

@@ -108,6 +108,11 @@ __host__ __device__ constexpr bool wide_mid_ok(int wd) { return wd >= kWideMidMi
 constexpr int kWide8Min = 11, kWide8Max = 28;
 __host__ __device__ constexpr uint32_t wide8_cover(int wd) { return 7u * wide_step(wd) + wide_win(wd); }
 __host__ __device__ constexpr bool wide8_ok(int wd) { return wd >= kWide8Min && wd <= kWide8Max && (wd - 1) % 4 != 0; }
+// Four-lane groups (round 4): sixteen frames per wave item, four windows per frame, WD = 9 .. 26
+// (cover 16 WD - 12 = 132 .. 404 B), WD 17 skipped (windows 0 and 2 on one bank).
+constexpr int kWide4Min = 9, kWide4Max = 26;
+__host__ __device__ constexpr uint32_t wide4_cover(int wd) { return 3u * wide_step(wd) + wide_win(wd); }
+__host__ __device__ constexpr bool wide4_ok(int wd) { return wd >= kWide4Min && wd <= kWide4Max && (wd - 1) % 16 != 0; }
 constexpr uint32_t kWideCover = wide_cover(32);                  // 1988
 constexpr uint32_t kWideCover26 = wide_cover(26);                // 1604
 constexpr uint32_t kWideCover30 = wide_cover(30);                // 1860
@@ -141,7 +146,8 @@ constexpr uint32_t kBlobLaneMid = kBlobInvWide + kWideWin;
 // Eight-lane groups: lane tables A_{(4 WD - 4) (slot mod 8)} for WD = kWide8Min..kWide8Max (one set
 // per width, unused widths included).
 constexpr uint32_t kBlobLane8 = kBlobLaneMid + (kWideMidMax - kWideMidMin + 1) * 8 * 16 * 32;
-constexpr uint32_t kBlobWords = kBlobLane8 + (kWide8Max - kWide8Min + 1) * 8 * 16 * 32;
+constexpr uint32_t kBlobLane4 = kBlobLane8 + (kWide8Max - kWide8Min + 1) * 8 * 16 * 32;   // (slot mod 4)
+constexpr uint32_t kBlobWords = kBlobLane4 + (kWide4Max - kWide4Min + 1) * 8 * 16 * 32;
 static_assert((kLdsInv - kLdsLane) / 4 == kBlobInv - kBlobLane, "blob/LDS order");
 static_assert((kLdsM768 - kLdsLane) / 4 == kBlobM768 - kBlobLane, "blob/LDS order");
 
@@ -257,6 +263,12 @@ struct Tables {
                 nibble_table((long)wide_step(wd) * (slot % 8), nt);
                 for (int t = 0; t < 8; t++)
                     for (int e = 0; e < 16; e++) b[kBlobLane8 + (wd - kWide8Min) * 4096 + (t * 16 + e) * 32 + slot] = nt[t][e];
+            }
+        for (int wd = kWide4Min; wd <= kWide4Max; wd++)   // four-lane groups
+            for (int slot = 0; slot < 32; slot++) {
+                nibble_table((long)wide_step(wd) * (slot % 4), nt);
+                for (int t = 0; t < 8; t++)
+                    for (int e = 0; e < 16; e++) b[kBlobLane4 + (wd - kWide4Min) * 4096 + (t * 16 + e) * 32 + slot] = nt[t][e];
             }
         return b;
     }

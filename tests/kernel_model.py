@@ -330,7 +330,9 @@ WIDE_MID = [wd for wd in range(15, 25) if (wd - 1) % 4]   # mid-length widths (f
 BLOB_LANE_MID = BLOB_INV_WIDE + WIDE_WIN                  # kBlobLaneMid: one [8][16][32] set per WD 15..24
 WIDE8 = [wd for wd in range(11, 29) if (wd - 1) % 4]    # eight-lane group widths (fcs_tables.hpp wide8_ok)
 BLOB_LANE8 = BLOB_LANE_MID + (24 - WIDE_MID[0] + 1) * 4096   # kBlobLane8: one set per WD 11..28
-WIDE_CL0 = {**{wd: wd - 2 * (wd // 4) for wd in WIDE_MID + WIDE8}, 32: 16, 30: 14, 26: 12}   # chain 0's words
+WIDE4 = [wd for wd in range(9, 27) if (wd - 1) % 16]     # four-lane group widths (fcs_tables.hpp wide4_ok)
+BLOB_LANE4 = BLOB_LANE8 + (28 - 11 + 1) * 4096            # kBlobLane4: one set per WD 9..26
+WIDE_CL0 = {**{wd: wd - 2 * (wd // 4) for wd in WIDE_MID + WIDE8 + WIDE4}, 32: 16, 30: 14, 26: 12}   # chain 0's words
 
 
 def wide_end_off(c, wd=32):
@@ -349,6 +351,15 @@ def wide8_cover(wd):
     return 7 * (4 * wd - 4) + 4 * wd
 
 
+def wide4_cover(wd):
+    return 3 * (4 * wd - 4) + 4 * wd
+
+
+def wide4_wd(flen):
+    """The width the host picks for a four-lane-group frame (fcs_launch.hpp wide4_wd)."""
+    return next(wd for wd in WIDE4 if wide4_cover(wd) >= flen)
+
+
 def wide8_wd(flen):
     """The width the host picks for an eight-lane-group frame (fcs_launch.hpp wide8_wd)."""
     return next(wd for wd in WIDE8 if wide8_cover(wd) >= flen)
@@ -364,7 +375,9 @@ def build_lds_wide(blob, wd=32, G=16):
     the lane tables A_{(4 WD - 4) c}; holes 128..131 the chain merge A_{4 (WD - CL0)}; holes
     132..135 INV[0..127]."""
     lane_blob = {32: BLOB_LANE_WIDE, 30: BLOB_LANE_WIDE30, 26: BLOB_LANE_WIDE26}.get(wd)
-    if G == 8:
+    if G == 4:
+        lane_blob = BLOB_LANE4 + (wd - 9) * 4096
+    elif G == 8:
         lane_blob = BLOB_LANE8 + (wd - 11) * 4096
     elif lane_blob is None:
         lane_blob = BLOB_LANE_MID + (wd - WIDE_MID[0]) * 4096

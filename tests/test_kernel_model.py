@@ -177,7 +177,8 @@ def test_segil_decomposition_model(lds_dma, L):
 def lds_wide():
     blob = na.tables_blob()
     return {**{wd: km.build_lds_wide(blob, wd) for wd in (26, 30, 32, *km.WIDE_MID)},
-            **{(wd, 8): km.build_lds_wide(blob, wd, 8) for wd in km.WIDE8}}
+            **{(wd, 8): km.build_lds_wide(blob, wd, 8) for wd in km.WIDE8},
+            **{(wd, 4): km.build_lds_wide(blob, wd, 4) for wd in km.WIDE4}}
 
 
 @pytest.mark.parametrize("flen,extra,wd", [(1525, 0, 32), (1530, 3, 32), (1536, 0, 32), (1537, 1, 32), (1600, 0, 32),
@@ -234,6 +235,29 @@ def test_wide8_kernel_model(lds_wide, flen, extra):
         for f in range(0, n, 8):
             got = km.model_wide_item(lds_wide[(wd, 8)], mem, b0, stride, flen, n, f, garbage, wd, 8)
             for g in range(8):
+                if f + g < n:
+                    S = b0 + (f + g) * stride
+                    assert got[g] == zlib.crc32(mem[S:S + flen]), (flen, extra, b0, f + g)
+
+
+@pytest.mark.parametrize("flen,extra", [(130, 0), (132, 1), (133, 0), (148, 0), (180, 3), (200, 0), (244, 0),
+                                        (245, 2), (256, 0), (300, 5), (324, 0), (340, 0), (356, 1), (388, 0),
+                                        (399, 0), (404, 0), (372, (6126 - 372) // 15 - 372),
+                                        (399, (7150 - 399) // 15 - 399)])
+def test_wide4_kernel_model(lds_wide, flen, extra):
+    """fcs_wide_kernel<WD, 4>: sixteen frames per item, four windows per frame (front lane
+    cf = min(3, (len - 1) / (4 WD - 4))), lane tables A_{(4 WD - 4) (slot mod 4)}, the quad sums;
+    replayed on the CPU for every item at four base alignments, against zlib."""
+    wd = km.wide4_wd(flen)
+    stride = flen + extra
+    rng = random.Random(flen * 43 + extra)
+    garbage = bytes(rng.randrange(256) for _ in range(2048 + 64))
+    for b0 in (0, 1, 2, 3):
+        n = max(35, 2 * km.wide_slot(wd) // stride + 3)   # the host takes arenas of two slots or more
+        mem = bytes(rng.randrange(256) for _ in range(b0 + n * stride + 64))
+        for f in range(0, n, 16):
+            got = km.model_wide_item(lds_wide[(wd, 4)], mem, b0, stride, flen, n, f, garbage, wd, 4)
+            for g in range(16):
                 if f + g < n:
                     S = b0 + (f + g) * stride
                     assert got[g] == zlib.crc32(mem[S:S + flen]), (flen, extra, b0, f + g)

@@ -35,7 +35,7 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_WIDE_NO26 -DFCS_WIDE_NO30"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MIN=1537"),
     ("fcs_engine.cpp", "-DFCS_WIDE_MID_MIN=0"),
-    ("fcs_engine.cpp", "-DFCS_WIDE8_MIN=0"),
+    ("fcs_engine.cpp", "-DFCS_WIDE8_MIN=0 -DFCS_WIDE4_MIN=0"),
     ("fcs_engine.cpp", "-DFCS_SHORT_MAX=0 -DFCS_SHORT_WG_PER_CU=2"),
     ("fcs_kernel.hip", "-DFCS_SHORT_NO_PIPE"),
     ("fcs_kernel.hip", "-DFCS_WIDE_MID_WD_MIN=11"),

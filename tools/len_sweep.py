@@ -23,6 +23,8 @@ def family(L):
     """The kernel family a large packed batch of L-byte frames takes (as selected in the library)."""
     if L <= 64 or 97 <= L <= 128:
         return "short (lane per frame)"
+    if 130 <= L <= 399:
+        return "wide, 4 lanes (flat if bank-phased)"
     if 400 <= L <= 868:
         return "wide, 8 lanes (flat if bank-phased)"
     if 870 <= L <= 1476:
