@@ -84,11 +84,22 @@ def splitmix_bytes(seed: int, byte_off: int, n: int):
     return b[s:s + n]
 
 
+def _traffic_key(p):
+    """Sort key of a PMC summary: round, then a round's first bundle (profiles/rNN_pmc_traffic*.json)
+    before its tagged re-runs (profiles/rNN_<tag>/rNN_<tag>_pmc_traffic*.json), as _profile_bundles."""
+    import re
+    m = re.match(r"r(\d+)(?:_([a-z0-9]+))?_pmc_traffic", os.path.basename(p))
+    tagged = m is not None and m.group(2) is not None and os.path.dirname(p) != os.path.join(ROOT, "profiles")
+    return (int(m.group(1)) if m else -1, 1 if tagged else 0, m.group(2) or "" if m else "", os.path.basename(p))
+
+
 def _load_pmc_traffic(frames: int, L, kernel: str = None):
     """HBM bytes per launch from the newest committed rocprofv3 PMC summary of this workload
-    (profiles/rNN_pmc_traffic*.json; later rounds sort later), if one matches."""
+    (profiles/rNN_pmc_traffic*.json and tagged bundles under profiles/rNN_<tag>/; later rounds and
+    later bundles of a round sort later), if one matches."""
     best = None
-    for p in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic*.json"))):
+    paths = glob.glob(os.path.join(ROOT, "profiles", "**", "*pmc_traffic*.json"), recursive=True)
+    for p in sorted(paths, key=_traffic_key):
         try:
             d = json.load(open(p))
         except Exception:
