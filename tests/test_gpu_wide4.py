@@ -54,7 +54,7 @@ def run(dev, d, lead, stride, L, n):
     return out.cpu().numpy().view(np.uint32)
 
 
-LENS = sorted({128, 129, 130, 131, 150, 200, 256, 300, 333, 380, 399, 400} | {cover(wd) for wd in WIDTHS if cover(wd) >= 130} |
+LENS = sorted({128, 129, 130, 131, 150, 192, 200, 256, 300, 320, 333, 384, 380, 399, 400} | {cover(wd) for wd in WIDTHS if cover(wd) >= 130} |
               {cover(wd) + 1 for wd in WIDTHS if 130 <= cover(wd) < 399})
 
 
@@ -74,8 +74,8 @@ def test_wide4_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(130, 130), (150, 150), (200, 200), (256, 256), (300, 300), (333, 333),
-                                      (372, 372), (399, 399), (399, 440)])
+@pytest.mark.parametrize("L,stride", [(130, 130), (150, 150), (200, 200), (256, 256), (300, 300), (320, 320),
+                                      (333, 333), (372, 372), (384, 384), (399, 399), (399, 440)])
 def test_wide4_many_items(dev, oracle, L, stride):
     """More items than the grid's waves (the dynamic schedule) and a second launch reusing the
     counter ring; the last items' slots clamped at the arena end."""

@@ -55,7 +55,7 @@ def run(dev, d, lead, stride, L, n):
     return out.cpu().numpy().view(np.uint32)
 
 
-LENS = sorted({300, 399, 400, 401, 460, 500, 560, 640, 700, 768, 800, 868, 869, 870} | {cover(wd) for wd in WIDTHS} |
+LENS = sorted({300, 399, 400, 401, 460, 500, 512, 560, 640, 700, 768, 800, 832, 868, 869, 870} | {cover(wd) for wd in WIDTHS} |
               {cover(wd) + 1 for wd in WIDTHS})
 
 
@@ -75,8 +75,8 @@ def test_wide8_lengths(dev, oracle, L):
                 assert np.array_equal(got, exp), (L, stride, n, lead, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("L,stride", [(400, 400), (484, 484), (512, 512), (612, 640), (700, 700), (740, 740),
-                                      (741, 741), (868, 868), (868, 1000)])
+@pytest.mark.parametrize("L,stride", [(400, 400), (484, 484), (512, 512), (612, 640), (640, 640), (700, 700),
+                                      (740, 740), (741, 741), (768, 768), (868, 868), (868, 1000)])
 def test_wide8_many_items(dev, oracle, L, stride):
     """More items than the grid's waves (the dynamic schedule) and a second launch reusing the
     counter ring; the last items' slots clamped at the arena end."""
