@@ -1883,7 +1883,8 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
 
 // ---------------------------------------------------------------------------------------------
 // Short fixed-length frames, one lane per frame (fcs_short_kernel<W>; host-selected by
-// short_wd(): frames of 1..64 B on W = 16 and 97..128 B on W = 32, large batches, any stride).
+// short_wd(): frames of 1..64 B on W = 16, 65..96 B on W = 24, 97..128 B on W = 32, large batches,
+// any stride).
 // The flat chunk stream (fcs_flat_kernel) spends a 96-B chunk on a 64-B frame: a 24-word chain of
 // which 8 words are masked, the dealing of chunks to lanes, a chunk shift and an LDS atomic. With
 // the length fixed none of that is needed: lane l of a wave's item takes frame 64 item + l, loads
@@ -1985,7 +1986,7 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_short_kernel(KParams p) {
 #ifdef FCS_SHORT_NO_PIPE   // measurement-only: each item's loads right before its CRC work
     constexpr bool kPipe = false;
 #else
-    constexpr bool kPipe = W <= 16;   // two 33-dword register sets at W = 32 spill
+    constexpr bool kPipe = W <= 24;   // two 33-dword register sets at W = 32 spill (W = 24: 103 VGPRs)
 #endif
     if constexpr (!kPipe) {
         for (uint64_t it = D.first(); it != kEnd; it = D.next(it)) {
@@ -2868,6 +2869,7 @@ hipError_t launch_short(const KParams &p, int grid, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
     switch (short_wd(p.flen)) {
         case 16: hipLaunchKernelGGL(fcs_short_kernel<16>, dim3(grid), dim3(kWgThreads), 0, st, p); break;
+        case 24: hipLaunchKernelGGL(fcs_short_kernel<24>, dim3(grid), dim3(kWgThreads), 0, st, p); break;
         case 32: hipLaunchKernelGGL(fcs_short_kernel<32>, dim3(grid), dim3(kWgThreads), 0, st, p); break;
         default: return hipErrorInvalidValue;
     }

@@ -284,17 +284,17 @@ inline int wide4_wd(const KParams &p) {
             wide_bank_load(p, wd, 4) <= 2) ? wd : 0;
 }
 inline bool fixed_wide4(const KParams &p) { return wide4_wd(p) != 0; }
-// Short-frame kernel (fcs_short_kernel<W>): fixed lengths of 1..64 and 97..kShortMaxLen bytes, one
-// lane per frame, the W-dword window ending at the frame end loaded into registers (any stride).
-// Against the flat chunk stream (tools/ab.py, one process per length): 60 B
-// +11.5 %, 64 B +10.4 %, 32 B +10.2 % (with the loads one item ahead), 100 B +27 %, 128 B +1.6 to
-// +10 %; 65..96 B stay on the flat kernel (74 B +3.9 %, 96 B +-0: one 96-B chunk per frame there is
-// the same work).
+// Short-frame kernel (fcs_short_kernel<W>): fixed lengths of 1..kShortMaxLen bytes, one lane per
+// frame, the W-dword window ending at the frame end loaded into registers (any stride). Against the
+// flat chunk stream (tools/ab.py, one process per length): 60 B +11.5 %, 64 B
+// +10.4 %, 32 B +10.2 %, 66..74 B +6.0 to +6.7 %, 80..96 B +1.7 to +3.6 % (W = 16 and 24 with the
+// loads one item ahead), 100 B +27 %, 128 B +1.6 to +10 %.
 #ifndef FCS_SHORT_MAX   // measurement-only override (0: no short-frame kernel)
 #define FCS_SHORT_MAX 128
 #endif
 constexpr uint32_t kShortMaxLen = FCS_SHORT_MAX;
-__host__ __device__ constexpr int short_wd(uint32_t len) { return len <= 64 ? 16 : (len <= 96 ? 0 : (len <= 128 ? 32 : 0)); }
+__host__ __device__ constexpr int short_wd(uint32_t len) { return len <= 64 ? 16 : (len <= 96 ? 24 : (len <= 128 ? 32 : 0)); }
+static_assert(short_wd(1) == 16 && short_wd(65) == 24 && short_wd(97) == 32 && short_wd(129) == 0, "short-frame widths");
 inline bool fixed_short(const KParams &p) {
     return p.flen >= 1 && p.flen <= kShortMaxLen && short_wd(p.flen) != 0 && !fixed_tiny(p);
 }

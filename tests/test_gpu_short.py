@@ -1,9 +1,9 @@
 """GPU parity of the short-frame kernel (fcs_short_kernel<W>).
 
-Fixed-length batches of more than 16384 frames of 1..64 and 97..128 B take one lane per frame
-(fcs_launch.hpp fixed_short / short_wd): the W-dword window ending at the frame end (W = 16 up to
-64 B, 32 from 97 to 128 B; 65..96 B keep the flat kernel) in registers, the zc = 4 W - len bytes
-before the frame start masked, two chains from INV[zc] merged with A_{2 W}. Every case is checked bit-exact against the oracle (the CPU
+Fixed-length batches of more than 16384 frames of 1..128 B take one lane per frame (fcs_launch.hpp
+fixed_short / short_wd): the W-dword window ending at the frame end (W = 16 up to 64 B, 24 up to
+96 B, 32 up to 128 B) in registers, the zc = 4 W - len bytes before the frame start masked, two
+chains from INV[zc] merged with A_{2 W}. Every case is checked bit-exact against the oracle (the CPU
 restatement of src/ether_fcs.c:4-19): every window width's shortest and longest frame and the
 lengths just outside the kernel (129 B takes the flat kernel), the minimum Ethernet sizes (60/64 B,
 and 70/74 B, the smallest frame ether_send builds, src/linux/ether.c:222-224), strides from packed

@@ -21,7 +21,7 @@ DEFAULT_LENS = [64, 128, 256, 512, 576, 768, 869, 870, 1000, 1156, 1157, 1250, 1
 
 def family(L):
     """The kernel family a large packed batch of L-byte frames takes (as selected in the library)."""
-    if L <= 64 or 97 <= L <= 128:
+    if L <= 128:
         return "short (lane per frame)"
     if 130 <= L <= 399:
         return "wide, 4 lanes (flat if bank-phased)"
