@@ -165,6 +165,12 @@ int fcs_timed_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_
  * the device. */
 int64_t fcs_debug_stream_listed(void);
 uint32_t fcs_debug_stream_unit_frames(void);
+/* Test introspection: the kernel a fixed-length batch (frames of len bytes every stride bytes from
+ * base, n frames) would take, as ether_fcs_fixed_dev picks it: "short:W", "flat", "wide4:WD",
+ * "wide8:WD", "wide16:WD", "segment", "lds-dma", "tiny", "single" or "generic" (DESIGN.md §3.2,
+ * §3.3c). Host arithmetic only: no device call, base is not read. Writes a NUL-terminated name
+ * into out (cap bytes); returns its length or -errno. */
+int fcs_debug_fixed_route(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, char *out, uint64_t cap);
 /* Test introspection: copy the constant tables the kernel stages into LDS (GF(2) operators of
  * the CRC, built on the host once; no frame data involved). Returns words written or -errno. */
 int fcs_tables_blob(uint32_t *out, uint64_t words);

@@ -22,7 +22,7 @@ __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fi
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "fcs_debug_fixed_route", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
@@ -120,6 +120,7 @@ def _bind(path: str) -> ctypes.CDLL:
         "fcs_engine_host_batches": (u64, []),
         "fcs_debug_stream_listed": (c.c_int64, []),
         "fcs_debug_stream_unit_frames": (u32, []),
+        "fcs_debug_fixed_route": (i32, [u64, u64, u32, u64, c.c_char_p, u64]),
         "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
@@ -316,6 +317,14 @@ def engine_stats() -> dict:
     d["host_fallbacks"] = int(L.fcs_engine_host_fallbacks())   # drop-in calls the host CRC answered
     d["host_batches"] = int(L.fcs_engine_host_batches())       # TX/RX queue batches the host CRC answered
     return d
+
+
+def fixed_route(base: int, stride: int, length: int, n: int) -> str:
+    """The kernel a fixed-length batch would take (fcs_debug_fixed_route; host arithmetic only)."""
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    _check(load().fcs_debug_fixed_route(base, stride, length, n, buf, 64), "fcs_debug_fixed_route")
+    return buf.value.decode()
 
 
 def stream_listed() -> int:

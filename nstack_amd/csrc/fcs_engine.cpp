@@ -1715,6 +1715,50 @@ uint64_t fcs_engine_host_fallbacks(void) { return g_host_fallbacks.load(std::mem
 
 uint32_t fcs_debug_stream_unit_frames(void) { return fcs::kStUnitFrames; }
 
+// The same decisions as launch_fixed and fcs::launch_fcs, named (no device call).
+int fcs_debug_fixed_route(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, char *out, uint64_t cap) {
+    if (!out || cap == 0) return -EINVAL;
+    std::string r;
+    if (n == 0) {
+        r = "none";
+    } else {
+        fcs::KParams p{};
+        p.base = base;
+        p.stride = stride;
+        p.n = n;
+        p.lo4 = floor4(base);
+        p.hi4 = ceil4(base + (n - 1) * stride + len);
+        p.flen = len;
+        p.fseg = segments(len);
+        p.zmax = mask_bound(len);
+        const bool big = n > g_var_threshold.load(std::memory_order_relaxed), tiny = fcs::fixed_tiny(p);
+        if (big && fcs::fixed_short(p)) {
+            r = "short:" + std::to_string(fcs::short_wd(len));
+        } else if (len <= kFixedFlatMaxLen && big &&
+                   !(!tiny && (fcs::fixed_wide4(p) || fcs::fixed_wide8(p) || fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {
+            r = "flat";
+        } else if (!tiny && fcs::fixed_wide4(p)) {
+            r = "wide4:" + std::to_string(fcs::wide4_wd(p));
+        } else if (!tiny && fcs::fixed_wide8(p)) {
+            r = "wide8:" + std::to_string(fcs::wide8_wd(p));
+        } else if (!tiny && fcs::fixed_wide(p)) {
+            r = "wide16:" + std::to_string(fcs::wide_wd(p));
+        } else if (fcs::fixed_segil(p)) {
+            r = "segment";
+        } else if (!tiny && fcs::fixed_dma(p)) {
+            r = "lds-dma";
+        } else if (tiny) {
+            r = "tiny";
+        } else {
+            r = fcs::fixed_single(p) ? "single" : "generic";
+        }
+    }
+    const uint64_t k = std::min<uint64_t>(r.size(), cap - 1);
+    std::memcpy(out, r.data(), k);
+    out[k] = 0;
+    return (int)k;
+}
+
 int64_t fcs_debug_stream_listed(void) {
     DevState *ds = g_last_stream_dev.load(std::memory_order_relaxed);
     if (!ds) return -1;
