@@ -21,19 +21,35 @@
  * Semantics (all entry points): out[i] == ether_fcs(frame_i, len_i) of the reference, i.e.
  * CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init/final complement), bit-exact; len 0 -> 0.
  *
- * Errors: the batch/device entry points return 0 on success or a negative errno
- * (-EINVAL bad arguments, -ENODEV no usable GPU / HIP code object missing, -ENOMEM,
- * -EIO a HIP runtime error; fcs_last_error() has the text). These entry points have NO CPU
- * fallback: without a GPU they fail loudly. ether_fcs() has no error channel in the reference
- * (it cannot fail there): a failed attempt (HIP error, lost completion, timeout)
- * quarantines that lane's stream and result word and is retried once on a fresh lane; if the
- * retry fails too, or bsize >= 4 GiB (the kernels take 32-bit lengths), the call is answered by
- * the library's own host CRC instead of aborting, so the result never differs from the
- * reference. Each such call is counted (fcs_engine_host_fallbacks) and the first one is reported
- * on stderr; fcs_engine_stats counts calls, retries and recoveries. The TX/RX call-site queues
- * (nstack_txq.h, nstack_rxq.h) keep ether_send's / ether_receive's contract the same way: a batch
- * whose GPU step fails is answered by that host CRC (fcs_engine_host_batches), never failed or
- * dropped for FCS reasons.
+ * Errors (the reference's ether_fcs cannot fail). Every entry point returns 0 on
+ * success or a negative errno; fcs_last_error() has the text.
+ *   -EINVAL   bad arguments: nothing has been written. Never answered by the host CRC.
+ *   -ENODEV   no usable gfx950 GPU or HIP code object at all: the batch and device forms fail
+ *             loudly then (they never turn into a CPU library). The drop-in ether_fcs is the
+ *             exception below.
+ *   device forms (*_dev): any other HIP error is returned (-EIO, -ENOMEM, ...): the frames are in
+ *             device memory, so there is no host answer to give.
+ *   host forms (ether_fcs_batch_host, _fixed_host, _tx_host, _tx_batch_host, _verify_host): any
+ *             other failure of the GPU step (a HIP error, a lost completion, the 10 s timeout, an
+ *             allocation failure) is answered by the library's own host CRC (fcs_host_crc.cpp,
+ *             slice-by-16, not a test oracle), so the results are the reference's and the call
+ *             returns 0 (verify: the bad count). Each such call is counted in
+ *             fcs_engine_host_batches(), the first is reported on stderr, and fcs_last_error() says
+ *             "<form> answered by the host CRC after: <the GPU error>". A failed GPU step never leaves
+ *             a kernel that can write into the caller's memory: results travel through the library's
+ *             own staging and mapped arrays, which are set aside (never reused or freed before
+ *             fcs_engine_fini) when a kernel may still be in flight. After 16 such set-asides the
+ *             host forms stop calling the GPU and answer from the host CRC (counted) until
+ *             fcs_engine_fini. fcs_host_free waits up to 10 s for set-aside kernels before it frees
+ *             pinned memory, and keeps the memory if one is still running.
+ *   ether_fcs (drop-in): a failed attempt (HIP error, lost completion, timeout) quarantines that
+ *             lane's stream and result word and is retried once on a fresh lane; if the retry fails
+ *             too, or there is no GPU, or bsize >= 4 GiB (the kernels take 32-bit lengths), the call
+ *             is answered by the same host CRC instead of aborting. Counted in
+ *             fcs_engine_host_fallbacks, first reported on stderr; fcs_engine_stats counts calls,
+ *             retries and recoveries.
+ * The TX/RX call-site queues (nstack_txq.h, nstack_rxq.h) go through the host forms, so they keep
+ * ether_send's / ether_receive's contract: never failed or dropped for FCS reasons.
  *
  * Threading: every entry point is thread-safe and may be called concurrently (the reference
  * calls ether_fcs from the main, ingress, egress and TCP-timer threads: SURVEY.md §8b).
@@ -73,10 +89,10 @@ void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t
 /* Drop-in calls answered by the host CRC because the GPU path failed twice or bsize >= 4 GiB
  * (0 on a healthy GPU: the GPU test suite asserts it). */
 uint64_t fcs_engine_host_fallbacks(void);
-/* Batches of the TX/RX call-site queues (nstack_txq.h, nstack_rxq.h) whose GPU step failed and
- * whose FCSs were therefore computed or checked by the same host CRC, so that ether_send's and
- * ether_receive's per-call results never depend on the GPU (0 on a healthy GPU: the GPU test
- * suite asserts it). */
+/* Host batch calls (ether_fcs_*_host, including the TX/RX call-site queues' batches, nstack_txq.h,
+ * nstack_rxq.h) whose GPU step failed and whose results were therefore computed or checked by the
+ * same host CRC, so that their results, and ether_send's and ether_receive's per-call results,
+ * never depend on the GPU (0 on a healthy GPU: the GPU test suite asserts it). */
 uint64_t fcs_engine_host_batches(void);
 /* Host batch paths: calls that were split over more than one engine device, and the shard jobs
  * those calls ran (one host thread and pipeline each). Any pointer may be NULL. */
@@ -166,11 +182,14 @@ int fcs_timed_fixed_dev(const void *base, uint64_t stride, uint32_t len, uint64_
 int64_t fcs_debug_stream_listed(void);
 uint32_t fcs_debug_stream_unit_frames(void);
 /* Test introspection: the kernel a fixed-length batch (frames of len bytes every stride bytes from
- * base, n frames) would take, as ether_fcs_fixed_dev picks it: "short:W", "flat", "wide4:WD",
- * "wide8:WD", "wide16:WD", "segment", "lds-dma", "tiny", "single" or "generic" (DESIGN.md §3.2,
- * §3.3c). Host arithmetic only: no device call, base is not read. Writes a NUL-terminated name
- * into out (cap bytes); returns its length or -errno. */
+ * base, n frames) would take, as ether_fcs_fixed_dev picks it (fcs::route_fixed, the one function
+ * that decides it): "short:W", "flat", "wide4:WD", "wide8:WD", "wide16:WD", "segment", "lds-dma",
+ * "tiny", "single" or "generic" (DESIGN.md §3.2). Host arithmetic only: no device call, base is not
+ * read. Writes a NUL-terminated name into out (cap bytes); returns its length or -errno. */
 int fcs_debug_fixed_route(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, char *out, uint64_t cap);
+/* Test introspection: the kernel the process's last fixed-length launch actually launched, recorded
+ * by the launcher in the branch that launches it: "<name as above>/<workgroup threads>", or "none". */
+int fcs_debug_last_fixed_launch(char *out, uint64_t cap);
 /* Test introspection: copy the constant tables the kernel stages into LDS (GF(2) operators of
  * the CRC, built on the host once; no frame data involved). Returns words written or -errno. */
 int fcs_tables_blob(uint32_t *out, uint64_t words);

@@ -22,7 +22,7 @@ __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fi
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "fcs_debug_fixed_route", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "fcs_debug_fixed_route", "fcs_debug_last_fixed_launch", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
@@ -69,8 +69,10 @@ _faults = None
 
 def load_faults() -> ctypes.CDLL:
     """The TEST-ONLY fault-hook build (-DFCS_FAULT_HOOK), bound like the product library plus its
-    fcs_debug_fail_next / fcs_debug_timeout_next / fcs_debug_fail_batches hooks. Its engine state
-    is separate from the product library's. Nothing in the product loads it."""
+    fcs_debug_fail_next / fcs_debug_timeout_next (drop-in) and fcs_debug_fail_batches /
+    fcs_debug_late_batches (host batch calls: fail before the launch / give up after it with the
+    kernel in flight) hooks. Its engine state is separate from the product library's. Nothing in the
+    product loads it."""
     global _faults
     if _faults is None:
         L = _bind(FAULTS_PATH)
@@ -78,8 +80,12 @@ def load_faults() -> ctypes.CDLL:
             f = getattr(L, name)
             f.restype = None
             f.argtypes = [ctypes.c_int]
-        L.fcs_debug_fail_batches.restype = None
-        L.fcs_debug_fail_batches.argtypes = [ctypes.c_int, ctypes.c_int]
+        for name in ("fcs_debug_fail_batches", "fcs_debug_late_batches"):
+            f = getattr(L, name)
+            f.restype = None
+            f.argtypes = [ctypes.c_int, ctypes.c_int]
+        L.fcs_debug_retired.restype = ctypes.c_uint32
+        L.fcs_debug_retired.argtypes = []
         L.fcs_debug_batch_faults_left.restype = ctypes.c_int
         L.fcs_debug_batch_faults_left.argtypes = []
         _faults = L
@@ -121,6 +127,7 @@ def _bind(path: str) -> ctypes.CDLL:
         "fcs_debug_stream_listed": (c.c_int64, []),
         "fcs_debug_stream_unit_frames": (u32, []),
         "fcs_debug_fixed_route": (i32, [u64, u64, u32, u64, c.c_char_p, u64]),
+        "fcs_debug_last_fixed_launch": (i32, [c.c_char_p, u64]),
         "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
@@ -324,6 +331,14 @@ def fixed_route(base: int, stride: int, length: int, n: int) -> str:
     import ctypes
     buf = ctypes.create_string_buffer(64)
     _check(load().fcs_debug_fixed_route(base, stride, length, n, buf, 64), "fcs_debug_fixed_route")
+    return buf.value.decode()
+
+
+def last_fixed_launch() -> str:
+    """"<route>/<threads>" of the kernel the last fixed-length launch actually launched."""
+    import ctypes
+    buf = ctypes.create_string_buffer(64)
+    _check(load().fcs_debug_last_fixed_launch(buf, 64), "fcs_debug_last_fixed_launch")
     return buf.value.decode()
 
 

@@ -100,30 +100,58 @@ bool injected_timeout() {
     g_inject_timeouts--;
     return true;
 }
-// ... and of the batch calls the TX/RX queues make (ether_fcs_tx_batch_host,
-// ether_fcs_verify_host, and the mapped-list submit and wait), whichever thread makes them (the TX
-// queue's GPU step runs on its flusher thread), the next `skip` run normally and the `calls` after
-// them fail. A failed wait leaves its kernel in flight.
-std::mutex g_inject_batch_mu;
-int g_inject_batch_skip = 0, g_inject_batch_calls = 0;
-bool injected_batch_fault() {
-    std::lock_guard<std::mutex> lk(g_inject_batch_mu);
-    if (g_inject_batch_skip > 0) {
-        g_inject_batch_skip--;
-        return false;
+// ... and of the host batch calls (the five ether_fcs_*_host forms, which the TX/RX queues use, and
+// the mapped-list submit and wait of the RX queue), whichever thread makes them (the TX queue's GPU
+// step runs on its flusher thread), the next `skip` run normally and the `calls` after them fail:
+// at entry, before anything is launched (fcs_debug_fail_batches; a failed mapped-list wait leaves
+// its kernel in flight), or at the call's first wait after a launch, giving up with the kernel
+// still in flight as a timeout would (fcs_debug_late_batches).
+struct Injector {
+    std::mutex mu;
+    int skip = 0, calls = 0;
+    bool take() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (skip > 0) {
+            skip--;
+            return false;
+        }
+        if (calls <= 0) return false;
+        calls--;
+        return true;
     }
-    if (g_inject_batch_calls <= 0) return false;
-    g_inject_batch_calls--;
-    return true;
-}
+    void arm(int s, int c) {
+        std::lock_guard<std::mutex> lk(mu);
+        skip = s;
+        calls = c;
+    }
+    int left() {
+        std::lock_guard<std::mutex> lk(mu);
+        return skip + calls;
+    }
+};
+Injector g_inject_batch, g_inject_late;
+bool injected_batch_fault() { return g_inject_batch.take(); }
+bool injected_late_fault() { return g_inject_late.take(); }
 #else
 inline bool injected_fault() { return false; }
 inline bool injected_timeout() { return false; }
 inline bool injected_batch_fault() { return false; }
+inline bool injected_late_fault() { return false; }
 #endif
 
-// Queue batches (TX/RX call sites) answered by the host CRC because their GPU step failed.
+// Host batch calls (ether_fcs_*_host, and the TX/RX queues' batches, which go through them)
+// answered by the host CRC because their GPU step failed.
 std::atomic<uint64_t> g_host_batches{0};
+// Set when the calling thread's last host batch call was answered by the host CRC (the queues read
+// it to count their own batches: fcs::last_call_host_answered).
+thread_local bool t_host_answered = false;
+// Failed host batch calls that may have left a kernel in flight retire the resources that kernel
+// can still write (pipeline staging, the small-batch stream, its mapped words and counters): they
+// are set aside until fcs_engine_fini, never reused. After kMaxRetired such calls the host batch
+// forms stop calling the GPU and answer from the host CRC (counted, reported once).
+constexpr uint32_t kMaxRetired = 16;
+std::atomic<uint32_t> g_retired{0};
+bool host_only() { return g_retired.load(std::memory_order_relaxed) >= kMaxRetired; }
 
 // Host pipeline resources of one device: kDepth chunks in flight (double-buffered by default).
 #ifndef FCS_PIPE_DEPTH   // measurement-only override (chunks in flight per device)
@@ -172,6 +200,7 @@ struct DevState {
     std::mutex q_mu;
     std::vector<hipStream_t> q_streams;
     std::vector<void *> q_host;
+    std::vector<void *> q_dev;   // device buffers of retired resources (hipFree at fini)
     std::mutex pipe_mu;      // one host pipeline at a time per device
     Pipe pipe;
     std::mutex tx_mu;        // small-batch zero-copy TX (ether_fcs_tx_host on pinned frames)
@@ -181,6 +210,14 @@ struct DevState {
     uint64_t *tx_off = nullptr, *tx_doff = nullptr;  // frame offsets (ether_fcs_tx_batch_host)
     uint64_t *tx_flag = nullptr, *tx_dflag = nullptr; // completion word (signal_kernel), mapped
     uint64_t tx_seq = 0;
+    uint64_t tx_first_seq = 1;   // first completion number of the current tx_stream (earlier ones
+                                 // belong to a retired stream: retire_small)
+    struct OldGen {              // a retired small-batch stream: completions [first, last] were
+        uint64_t first, last;    // issued on it; its stream and word are quarantined, not freed, so
+        hipStream_t st;          // a batch issued before the retirement can still be waited for
+        const uint64_t *flag;
+    };
+    std::vector<OldGen> tx_old;
     unsigned long long *tx_dcount = nullptr;        // small-batch kernel: frames done (device memory)
     uint64_t tx_count = 0;                           //   ... its value once every launch so far is done
     uint64_t *vz_off = nullptr, *vz_doff = nullptr;  // small RX verify batches (same stream and lock):
@@ -345,18 +382,6 @@ std::atomic<uint64_t> g_var_threshold{16384};
 // (fcs_debug_stream_listed). DevStates live until fcs_engine_fini, so the pointer stays valid.
 std::atomic<DevState *> g_last_stream_dev{nullptr};
 
-// Fixed-length batches of frames up to this length (and more than g_var_threshold frames) take the
-// flat variable-length kernel: a 64-B frame then costs one lane instead of a quarter-wave. Measured
-// against the quarter-wave kernel (tools/ab.py): 64 B 11x, 576 B 2.1x, 1300 B
-// +6.5 %; 1504..1536 B stay on the single kernel (the flat kernel is 9 % slower at 1518 B). The
-// slot kernels go first where their slots take the batch: the mid-length and 104-B-window wide
-// kernels (870..1495 B) and the LDS-DMA kernel (1496..1503 B: +10 % against the flat kernel,
-// tools/ab.py, round 4).
-#ifndef FCS_FIXED_FLAT_MAX   // measurement-only override (0 = never)
-#define FCS_FIXED_FLAT_MAX 1503
-#endif
-constexpr uint32_t kFixedFlatMaxLen = FCS_FIXED_FLAT_MAX;
-
 // A zeroed work counter for one launch (Dispenser in fcs_kernel.hip): the next slot of the
 // device's ring, cleared on the launch's own stream just before the kernel, after the slot's
 // previous kernel (on any stream) has finished. The lease holds the slot until the new launch's
@@ -412,93 +437,42 @@ int take_counter(DevState *ds, hipStream_t st, fcs::KParams &p, CounterLease &le
     return 0;
 }
 
-// The flat kernel hands its 64-frame windows out dynamically once there are at least this many
-// windows per wave of the grid.
-#ifndef FCS_FLAT_DYN_MIN   // measurement-only override (a huge value keeps the flat kernel static)
-#define FCS_FLAT_DYN_MIN 4
-#endif
-constexpr uint64_t kFlatDynMinWindowsPerWave = FCS_FLAT_DYN_MIN;
-
-// The generic fixed-length kernel hands its 4-frame units out dynamically from this many units per
-// wave of the grid.
-#ifndef FCS_FIXED_DYN_MIN   // measurement-only override (a huge value keeps the kernel static)
-#define FCS_FIXED_DYN_MIN 4
-#endif
-constexpr uint64_t kFixedDynMinUnitsPerWave = FCS_FIXED_DYN_MIN;
-
-int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
-                 uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
-    CounterLease lease;   // declared first: released (event recorded) after the launch below
+// The fixed-length route (fcs::route_fixed, the one place that decides it), its grid, its work
+// counter, and the launch of exactly that kernel (fcs::launch_fixed_route).
+fcs::KParams fixed_params(const DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n) {
     fcs::KParams p{};
-    p.ok = ok;
-    p.bad = bad;
     p.base = (uint64_t)base;
     p.stride = stride;
-    p.out = out;
     p.n = n;
     p.lo4 = floor4((uint64_t)base);
     p.hi4 = ceil4((uint64_t)base + (n - 1) * stride + len);
     p.flen = len;
     p.fseg = segments(len);
     p.zmax = mask_bound(len);
-    p.blob = ds->d_blob;
+    p.blob = ds ? ds->d_blob : nullptr;
+    return p;
+}
+
+int launch_fixed(DevState *ds, const void *base, uint64_t stride, uint32_t len, uint64_t n,
+                 uint32_t *out, hipStream_t st, uint8_t *ok = nullptr, unsigned long long *bad = nullptr) {
+    CounterLease lease;   // declared first: released (event recorded) after the launch below
+    fcs::KParams p = fixed_params(ds, base, stride, len, n);
+    p.ok = ok;
+    p.bad = bad;
+    p.out = out;
     p.dbg = g_dbg;
-    if (n > g_var_threshold.load(std::memory_order_relaxed) && fcs::fixed_short(p)) {
-        // short frames: one lane per frame, its window in registers (fcs_short_kernel)
-#ifndef FCS_SHORT_WG_PER_CU   // measurement-only: workgroups per CU (2: -6 to -8 %)
-#define FCS_SHORT_WG_PER_CU 1
-#endif
-        const int sgrid = FCS_SHORT_WG_PER_CU * grid_for(ds, (n + 15) / 16, fcs::kWgThreads);
-        if ((n + 63) / 64 >= fcs::kDmaDynMinItemsPerWave * (uint64_t)sgrid * (fcs::kWgThreads / 64)) {
-            const int rc = take_counter(ds, st, p, lease);
-            if (rc) return rc;
-        }
-        HIPTRY(fcs::launch_short(p, sgrid, st), "launching fcs_short_kernel");
-        return 0;
+    const fcs::FixedRoute r = fcs::route_fixed(p, n > g_var_threshold.load(std::memory_order_relaxed));
+    p.zmax = r.zmax;
+    // short frames: one lane per frame, 64 frames per wave item; the others: the route's slots
+    const int grid = r.kernel == fcs::FixedKernel::kShort
+                         ? FCS_SHORT_WG_PER_CU * grid_for(ds, (n + 15) / 16, r.threads)
+                         : grid_for(ds, n, r.threads);
+    const uint64_t items = (n + r.item_frames - 1) / r.item_frames, waves = (uint64_t)grid * (r.threads / 64);
+    if (r.dyn_min && items >= r.dyn_min * waves) {   // large batch: dynamic schedule
+        const int rc = take_counter(ds, st, p, lease);
+        if (rc) return rc;
     }
-    if (len <= kFixedFlatMaxLen && n > g_var_threshold.load(std::memory_order_relaxed) &&
-        !(!fcs::fixed_tiny(p) && (fcs::fixed_wide4(p) || fcs::fixed_wide8(p) || fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {
-        // short fixed-length frames: the flat chunk stream packs ceil(len / 96) lanes per frame
-        // instead of a 16-lane quarter-wave (len == null tells it the length is p.flen)
-        p.zmax = fcs::kChunkBytes;
-        const int fgrid = grid_for(ds, n, fcs::kWgThreads);
-        if ((n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)fgrid * (fcs::kWgThreads / 64)) {
-            const int rc = take_counter(ds, st, p, lease);
-            if (rc) return rc;
-        }
-        HIPTRY(fcs::launch_fcs(true, true, p, fgrid, st), "launching fcs_flat_kernel<fixed>");
-        return 0;
-    }
-    const int grid = grid_for(ds, n, fcs::fixed_threads(p));
-    if (!fcs::fixed_tiny(p) && (fcs::fixed_wide4(p) || fcs::fixed_wide8(p) || fcs::fixed_wide(p))) {   // wide LDS-DMA kernels
-        const uint64_t fr = fcs::fixed_wide4(p) ? 16 : (fcs::fixed_wide8(p) ? 8 : 4);   // frames per item
-        const uint64_t items = (n + fr - 1) / fr, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);
-        if (items >= fcs::kDmaDynMinItemsPerWave * waves) {
-            const int rc = take_counter(ds, st, p, lease);
-            if (rc) return rc;
-        }
-    } else if (fcs::fixed_dma(p)) {   // LDS-DMA kernel: the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
-        p.zmax = std::max<uint32_t>(4u, fcs::kDmaCover - len);
-        const uint64_t items = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kDmaWgThreads / 64);
-        if (items >= fcs::kDmaDynMinItemsPerWave * waves) {   // large batch: dynamic schedule
-            const int rc = take_counter(ds, st, p, lease);
-            if (rc) return rc;
-        }
-    } else if (fcs::fixed_segil(p)) {   // frame-interleaved segments: units of 4 frames
-        const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::kSegilWgThreads / 64);
-        if (units >= kFixedDynMinUnitsPerWave * waves) {
-            const int rc = take_counter(ds, st, p, lease);
-            if (rc) return rc;
-        }
-    } else if (!fcs::fixed_tiny(p) && !fcs::fixed_single(p)) {
-        // generic kernel: units of 4 frames (one per quarter-wave), dynamic for large batches
-        const uint64_t units = (n + 3) / 4, waves = (uint64_t)grid * (fcs::fixed_threads(p) / 64);
-        if (units >= kFixedDynMinUnitsPerWave * waves) {
-            const int rc = take_counter(ds, st, p, lease);
-            if (rc) return rc;
-        }
-    }
-    HIPTRY(fcs::launch_fcs(false, false, p, grid, st), "launching fcs_kernel<fixed>");
+    HIPTRY(fcs::launch_fixed_route(r, p, grid, st), "launching a fixed-length FCS kernel");
     return 0;
 }
 
@@ -551,12 +525,41 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
         return 0;
     }
 #endif
-    if (windowed && (n + 63) / 64 >= kFlatDynMinWindowsPerWave * (uint64_t)grid * (fcs::kWgThreads / 64)) {
+    if (windowed && (n + 63) / 64 >= fcs::kFlatDynMinWindowsPerWave * (uint64_t)grid * (fcs::kWgThreads / 64)) {
         const int rc = take_counter(ds, st, p, lease);
         if (rc) return rc;
     }
     HIPTRY(fcs::launch_fcs(true, windowed, p, grid, st), "launching fcs_kernel<var>");
     return 0;
+}
+
+// Set aside a stream and pinned words that a kernel may still use: neither destroyed nor freed
+// (hipHostFree could block behind a hung kernel, and a late kernel must not write into a word that
+// serves another call by then) until fcs_engine_fini.
+void quarantine(DevState *ds, hipStream_t st, std::initializer_list<void *> host,
+                std::initializer_list<void *> dev = {}) {
+    std::lock_guard<std::mutex> lk(ds->q_mu);
+    if (st) ds->q_streams.push_back(st);
+    for (void *h : host)
+        if (h) ds->q_host.push_back(h);
+    for (void *d : dev)
+        if (d) ds->q_dev.push_back(d);
+}
+
+// A host batch call failed after launching on the pipeline (a chunk's kernel or copies may still
+// run): its streams, events and staging are set aside and recreated on next use, so a late kernel or
+// D2H copy cannot write into staging that serves a later call. Caller holds pipe_mu.
+void retire_pipe(DevState *ds) {
+    Pipe &pp = ds->pipe;
+    quarantine(ds, pp.stream, {}, {});
+    quarantine(ds, pp.cstream, {}, {});
+    for (int b = 0; b < Pipe::kDepth; b++) {
+        quarantine(ds, nullptr, {pp.h_in[b], pp.h_off[b], pp.h_out[b]}, {pp.d_in[b], pp.d_off[b], pp.d_out[b]});
+        // events are only recorded and waited on; a fresh pipe creates its own
+    }
+    ds->pipe = Pipe{};
+    (void)hipGetLastError();
+    g_retired.fetch_add(1, std::memory_order_relaxed);
 }
 
 int ensure_pipe(DevState *ds, uint64_t bytes, uint64_t frames) {
@@ -676,11 +679,21 @@ constexpr uint32_t kResidue = 0x2144DF1Cu;   // ether_fcs(frame || LE32(ether_fc
 constexpr uint64_t kChunkBytesHost = 128ull << 20;   // per pipeline slot
 constexpr uint64_t kChunkFramesMax = 1ull << 20;
 
-// Runs the chunked H2D -> kernel -> D2H pipeline of one device over frames [i0, i1).
+int run_host_job_body(DevState *ds, const HostJob &job, bool &launched);
+
+// Runs the chunked H2D -> kernel -> D2H pipeline of one device over frames [i0, i1). A failure after
+// anything was enqueued retires the pipeline (retire_pipe): a chunk's kernel or copy may still run.
 int run_host_job(DevState *ds, const HostJob &job) {
     std::lock_guard<std::mutex> lk(ds->pipe_mu);
     DeviceGuard dg(ds->dev);
     HIPTRY(dg.err, "hipSetDevice");
+    bool launched = false;
+    const int rc = run_host_job_body(ds, job, launched);
+    if (rc && launched) retire_pipe(ds);
+    return rc;
+}
+
+int run_host_job_body(DevState *ds, const HostJob &job, bool &launched) {
     int rc = ensure_pipe(ds, kChunkBytesHost + 2 * fcs::kSegBytes, kChunkFramesMax);
     if (rc) return rc;
     Pipe &pp = ds->pipe;
@@ -690,6 +703,7 @@ int run_host_job(DevState *ds, const HostJob &job) {
     struct Pending { bool live = false; uint64_t i0 = 0, n = 0; } pend[Pipe::kDepth];
     auto drain = [&](int b) -> int {
         if (!pend[b].live) return 0;
+        if (injected_late_fault()) return fail(ETIMEDOUT, "host pipeline: injected late fault (FCS_FAULT_HOOK build)");
         HIPTRY(hipEventSynchronize(pp.done[b]), "hipEventSynchronize");
         if (job.out && !job.ok && !job.tx_base) {   // plain CRCs: one copy
             std::memcpy(job.out + pend[b].i0, pp.h_out[b], pend[b].n * 4);
@@ -829,6 +843,7 @@ int run_host_job(DevState *ds, const HostJob &job) {
         }
         FCS_TR(2, tc);
         FCS_TR_AT(td);
+        launched = true;
         HIPTRY(hipMemcpyAsync(pp.d_in[b], src, span, hipMemcpyHostToDevice, pp.stream), "H2D frames");
         if (var) {
             HIPTRY(hipMemcpyAsync(pp.d_off[b], ho, n * 12, hipMemcpyHostToDevice, pp.stream), "H2D off, len");
@@ -888,18 +903,40 @@ int ensure_small(DevState *ds) {
     return 0;
 }
 
+// A call on the small-batch stream failed after its launch (a timeout, a lost completion): the
+// kernel may still run and write the stream's mapped results (tx_out, vz_ok), its completion word
+// and the frame counter whose value later launches' completion test relies on. All of them are set
+// aside and recreated on next use; completions numbered before the new stream's first one
+// (tx_first_seq) are waited for on the retired stream's own word (tx_old). Caller holds tx_mu.
+void retire_small(DevState *ds) {
+    if (ds->tx_stream && ds->tx_seq >= ds->tx_first_seq)
+        ds->tx_old.push_back({ds->tx_first_seq, ds->tx_seq, ds->tx_stream, ds->tx_flag});
+    quarantine(ds, ds->tx_stream, {ds->tx_flag, ds->tx_len, ds->tx_out, ds->tx_off, ds->vz_off, ds->vz_len, ds->vz_ok},
+               {ds->tx_dcount, ds->vz_dbad});
+    ds->tx_stream = nullptr;
+    ds->tx_flag = ds->tx_dflag = nullptr;
+    ds->tx_len = ds->tx_out = ds->tx_dlen = ds->tx_dout = nullptr;
+    ds->tx_off = ds->tx_doff = nullptr;
+    ds->vz_off = ds->vz_doff = nullptr;
+    ds->vz_len = ds->vz_dlen = nullptr;
+    ds->vz_ok = ds->vz_dok = nullptr;
+    ds->vz_dbad = nullptr;
+    ds->tx_dcount = nullptr;
+    ds->tx_count = 0;
+    ds->tx_cap = ds->vz_cap = 0;
+    ds->tx_first_seq = ds->tx_seq + 1;
+    (void)hipGetLastError();
+    g_retired.fetch_add(1, std::memory_order_relaxed);
+}
+
 
 int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t stride, const uint64_t *off,
                      const uint32_t *len, uint64_t n) {
     std::lock_guard<std::mutex> lk(ds->tx_mu);
     DeviceGuard dg(ds->dev);
     HIPTRY(dg.err, "hipSetDevice");
-    if (!ds->tx_stream) {
-        HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
-        HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
-        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dflag, ds->tx_flag, 0), "hipHostGetDevicePointer(flag)");
-        *ds->tx_flag = 0;
-    }
+    int rc = ensure_small(ds);
+    if (rc) return rc;
     if (n > ds->tx_cap) {
         if (ds->tx_len) HIPTRY(hipHostFree(ds->tx_len), "hipHostFree(tx len)");
         if (ds->tx_out) HIPTRY(hipHostFree(ds->tx_out), "hipHostFree(tx out)");
@@ -923,20 +960,18 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
     }
     bool small = n <= fcs::kTxSmallMax;
     for (uint64_t i = 0; small && i < n; i++) small = len[i] <= fcs::kOneBytes;
-    if (small) {
-        const int e = ensure_small(ds);
-        if (e) return e;
-    }
-    if (small) {   // everything the kernel needs rides in its arguments; it writes the FCSs itself
+    uint64_t v = 0;
+    if (small) {   // everything the kernel needs rides in its arguments; it writes the FCSs to tx_out
         const std::vector<uint32_t> &kinit = kinit_table();
         fcs::TxSmallArgs a;
         a.flag = ds->tx_dflag;
         a.ok = nullptr;
+        a.out = ds->tx_dout;
         a.count = ds->tx_dcount;
         a.count_base = ds->tx_count;
         a.blob = ds->d_one_blob;
         a.base = (uint8_t *)dbase;
-        a.seq = ++ds->tx_seq;
+        a.seq = v = ++ds->tx_seq;
         a.n = (uint32_t)n;
         a.pad = 0;
         for (uint64_t i = 0; i < n; i++) {
@@ -946,16 +981,28 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
         }
         HIPTRY(fcs::launch_tx_small(a, ds->tx_stream), "launching the small TX kernel");
         ds->tx_count += n;
-        return wait_flag(ds->tx_stream, ds->tx_flag, a.seq, "small TX batch");
+    } else {
+        std::memcpy(ds->tx_len, len, n * 4);
+        if (off) std::memcpy(ds->tx_off, off, n * 8);
+        if ((rc = launch_var(ds, dbase, bytes, off ? ds->tx_doff : nullptr, ds->tx_dlen, ds->tx_dout, n, ds->tx_stream,
+                             nullptr, nullptr, off ? 0 : stride))) {
+            retire_small(ds);   // the arena-stream kernel may have started before a later launch failed
+            return rc;
+        }
+        v = ++ds->tx_seq;
+        if (const hipError_t e = fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream); e != hipSuccess) {
+            rc = hip_fail(e, "launching signal");
+            retire_small(ds);   // the FCS kernel is in flight
+            return rc;
+        }
     }
-    std::memcpy(ds->tx_len, len, n * 4);
-    if (off) std::memcpy(ds->tx_off, off, n * 8);
-    int rc = launch_var(ds, dbase, bytes, off ? ds->tx_doff : nullptr, ds->tx_dlen, ds->tx_dout, n, ds->tx_stream,
-                        nullptr, nullptr, off ? 0 : stride);
-    if (rc) return rc;
-    const uint64_t v = ++ds->tx_seq;
-    HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
-    if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small TX batch"))) return rc;
+    // the kernel is in flight: a failed wait leaves it so, and it may still write tx_out
+    rc = injected_late_fault() ? fail(ETIMEDOUT, "small TX batch: injected late fault (FCS_FAULT_HOOK build)")
+                               : wait_flag(ds->tx_stream, ds->tx_flag, v, "small TX batch");
+    if (rc) {
+        retire_small(ds);
+        return rc;
+    }
     for (uint64_t i = 0; i < n; i++) std::memcpy(base + (off ? off[i] : i * stride) + len[i], &ds->tx_out[i], 4);
     return 0;
 }
@@ -966,16 +1013,6 @@ uint32_t my_lane() {
     static std::atomic<uint32_t> next_thread{0};
     thread_local const uint32_t me = next_thread.fetch_add(1, std::memory_order_relaxed);
     return me % DevState::kOneLanes;
-}
-
-// Set aside a stream and pinned words that a kernel may still use: neither destroyed nor freed
-// (hipHostFree could block behind a hung kernel, and a late kernel must not write into a word that
-// serves another call by then) until fcs_engine_fini.
-void quarantine(DevState *ds, hipStream_t st, std::initializer_list<void *> host) {
-    std::lock_guard<std::mutex> lk(ds->q_mu);
-    if (st) ds->q_streams.push_back(st);
-    for (void *h : host)
-        if (h) ds->q_host.push_back(h);
 }
 
 // Drop a lane whose last call failed: its stream and result word are recreated on next use, so a
@@ -989,7 +1026,7 @@ void reset_lane(DevState *ds, DevState::OneLane &L) {
     g_lane_resets.fetch_add(1, std::memory_order_relaxed);
 }
 
-int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc, uint32_t lane) {
+int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc, uint32_t lane, bool batch = false) {
     DevState::OneLane &L = ds->one_lane[lane % DevState::kOneLanes];
     std::lock_guard<std::mutex> lk(L.mu);
     DeviceGuard dg(ds->dev);
@@ -1025,7 +1062,8 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc, uint32_
             *crc = (uint32_t)v;
             return 0;
         }
-        if (i == 1 && injected_timeout()) {   // FCS_FAULT_HOOK builds only: give up with the kernel in flight
+        // FCS_FAULT_HOOK builds only: give up with the kernel in flight (drop-in, or a one-frame host batch)
+        if (i == 1 && (injected_timeout() || (batch && injected_late_fault()))) {
             reset_lane(ds, L);
             return fail(ETIMEDOUT, "single-frame kernel: injected timeout (FCS_FAULT_HOOK build)");
         }
@@ -1057,17 +1095,12 @@ int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena
     std::lock_guard<std::mutex> lk(ds->tx_mu);
     DeviceGuard dg(ds->dev);
     HIPTRY(dg.err, "hipSetDevice");
-    if (!ds->tx_stream) {
-        HIPTRY(hipStreamCreateWithFlags(&ds->tx_stream, hipStreamNonBlocking), "hipStreamCreate");
-        HIPTRY(hipHostMalloc(&ds->tx_flag, 64, hipHostMallocMapped), "hipHostMalloc(tx flag)");
-        HIPTRY(hipHostGetDevicePointer((void **)&ds->tx_dflag, ds->tx_flag, 0), "hipHostGetDevicePointer(flag)");
-        *ds->tx_flag = 0;
-    }
+    int rc = ensure_small(ds);
+    if (rc) return rc;
     if (n > ds->vz_cap) {
         if (ds->vz_off) HIPTRY(hipHostFree(ds->vz_off), "hipHostFree(verify off)");
         if (ds->vz_len) HIPTRY(hipHostFree(ds->vz_len), "hipHostFree(verify len)");
         if (ds->vz_ok) HIPTRY(hipHostFree(ds->vz_ok), "hipHostFree(verify ok)");
-        if (!ds->vz_dbad) HIPTRY(hipMalloc(&ds->vz_dbad, 64), "hipMalloc(verify bad scratch)");
         ds->vz_off = nullptr;
         ds->vz_len = nullptr;
         ds->vz_ok = nullptr;
@@ -1081,20 +1114,21 @@ int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena
         HIPTRY(hipHostGetDevicePointer((void **)&ds->vz_dok, ds->vz_ok, 0), "hipHostGetDevicePointer(ok)");
         ds->vz_cap = cap;
     }
+    if (!ds->vz_dbad) HIPTRY(hipMalloc(&ds->vz_dbad, 64), "hipMalloc(verify bad scratch)");
     bool small = n <= fcs::kTxSmallMax;
     for (uint64_t i = 0; small && i < n; i++) small = len[i] <= fcs::kOneBytes;
-    int rc = 0;
+    uint64_t v = 0;
     if (small) {   // the small-batch kernel in verify mode: frame list in its arguments
-        if ((rc = ensure_small(ds))) return rc;
         const std::vector<uint32_t> &kinit = kinit_table();
         fcs::TxSmallArgs a;
         a.flag = ds->tx_dflag;
         a.blob = ds->d_one_blob;
         a.base = (uint8_t *)darena;
         a.ok = ds->vz_dok;
+        a.out = nullptr;
         a.count = ds->tx_dcount;
         a.count_base = ds->tx_count;
-        a.seq = ++ds->tx_seq;
+        a.seq = v = ++ds->tx_seq;
         a.n = (uint32_t)n;
         a.pad = 0;
         for (uint64_t i = 0; i < n; i++) {
@@ -1104,16 +1138,27 @@ int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena
         }
         HIPTRY(fcs::launch_tx_small(a, ds->tx_stream), "launching the small verify kernel");
         ds->tx_count += n;
-        if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, a.seq, "small verify batch"))) return rc;
     } else {
         std::memcpy(ds->vz_off, off, n * 8);
         std::memcpy(ds->vz_len, len, n * 4);
-        rc = launch_var(ds, darena, arena_bytes, ds->vz_doff, ds->vz_dlen, nullptr, n, ds->tx_stream, ds->vz_dok,
-                        ds->vz_dbad);
-        if (rc) return rc;
-        const uint64_t v = ++ds->tx_seq;
-        HIPTRY(fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream), "launching signal");
-        if ((rc = wait_flag(ds->tx_stream, ds->tx_flag, v, "small verify batch"))) return rc;
+        if ((rc = launch_var(ds, darena, arena_bytes, ds->vz_doff, ds->vz_dlen, nullptr, n, ds->tx_stream, ds->vz_dok,
+                             ds->vz_dbad))) {
+            retire_small(ds);   // the arena-stream kernel may have started before a later launch failed
+            return rc;
+        }
+        v = ++ds->tx_seq;
+        if (const hipError_t e = fcs::launch_signal(ds->tx_dflag, v, ds->tx_stream); e != hipSuccess) {
+            rc = hip_fail(e, "launching signal");
+            retire_small(ds);   // the verify kernel is in flight
+            return rc;
+        }
+    }
+    // the kernel is in flight: a failed wait leaves it so, and it may still write vz_ok
+    rc = injected_late_fault() ? fail(ETIMEDOUT, "small verify batch: injected late fault (FCS_FAULT_HOOK build)")
+                               : wait_flag(ds->tx_stream, ds->tx_flag, v, "small verify batch");
+    if (rc) {
+        retire_small(ds);
+        return rc;
     }
     std::memcpy(ok, ds->vz_ok, n);
     int64_t bad = 0;
@@ -1156,7 +1201,7 @@ int tx_one(uint8_t *frame, uint32_t len) {
     int rc = engine_devices(&devs);
     if (rc) return rc;
     uint32_t c = 0;
-    if ((rc = run_one(devs[0], frame, len, &c, my_lane()))) return rc;
+    if ((rc = run_one(devs[0], frame, len, &c, my_lane(), true))) return rc;
     std::memcpy(frame + len, &c, 4);
     return 0;
 }
@@ -1239,6 +1284,65 @@ int run_host_sharded(HostJob job, uint64_t n) {
     return 0;
 }
 
+// The host CRC's answer to a host batch call ("on any HIP error, fall back to the CPU
+// path so results never differ"): fcs_host_crc.cpp, the product's own slice-by-16 (never the oracle).
+// Plain CRCs, TX mode (the FCS stored little-endian after each frame, src/linux/ether.c:263) or RX
+// verify (ok[i]; returns the count of failing frames). Large batches are split over 8 threads.
+int64_t host_answer(const HostJob &job, uint64_t n) {
+    auto part = [&job](uint64_t a, uint64_t z) -> uint64_t {
+        uint64_t bad = 0;
+        for (uint64_t i = a; i < z; i++) {
+            const uint64_t o = job.off ? job.off[i] : i * job.stride;
+            const uint32_t L = job.len ? job.len[i] : job.flen;
+            const uint32_t c = fcs::host_crc32(job.arena + o, L);
+            if (job.out) job.out[i] = c;
+            if (job.ok) {
+                job.ok[i] = c == kResidue;   // no input of 0..3 bytes has the residue as its CRC
+                bad += c != kResidue;
+            }
+            if (job.tx_base) std::memcpy(job.tx_base + o + L, &c, 4);
+        }
+        return bad;
+    };
+    constexpr uint64_t kSplit = 1ull << 16;
+    constexpr int kThreads = 8;
+    if (n < kSplit) return (int64_t)part(0, n);
+    uint64_t bad[kThreads] = {};
+    std::thread th[kThreads - 1];
+    const uint64_t per = (n + kThreads - 1) / kThreads;
+    for (int t = 1; t < kThreads; t++)
+        th[t - 1] = std::thread([&, t] { bad[t] = part(std::min(n, per * t), std::min(n, per * (t + 1))); });
+    bad[0] = part(0, std::min(n, per));
+    uint64_t sum = 0;
+    for (auto &x : th) x.join();
+    for (uint64_t b : bad) sum += b;
+    return (int64_t)sum;
+}
+
+// A host batch form's GPU step, answered by the host CRC when it fails with a runtime error: -EIO,
+// -ETIMEDOUT, -ENOMEM or any other errno but -EINVAL (bad arguments, nothing written) and -ENODEV
+// (no usable gfx950 GPU or code object at all: the batch forms fail loudly then, they never turn
+// into a CPU library). Such calls are counted in fcs_engine_host_batches, the first is reported on
+// stderr, and fcs_last_error() keeps the GPU step's error. A failed GPU step never leaves a kernel
+// that can still write into the caller's memory: results go through the library's own staging or
+// mapped arrays, which are retired on such a failure (retire_pipe, retire_small). After kMaxRetired
+// retirements the forms answer from the host CRC without calling the GPU (host_only).
+template <class F>
+int64_t with_host_answer(const char *site, const HostJob &job, uint64_t n, F gpu) {
+    t_host_answered = false;
+    int64_t rc;
+    if (injected_batch_fault()) rc = fail(EIO, "%s: injected fault (FCS_FAULT_HOOK build)", site);
+    else if (host_only()) rc = fail(EIO, "%s: the host batch forms stopped using the GPU after %u failed calls", site, kMaxRetired);
+    else rc = gpu();
+    if (rc >= 0 || rc == -EINVAL || rc == -ENODEV) return rc;
+    const std::string why = g_last_error;
+    fcs::host_batch_answered(site, why.c_str());
+    t_host_answered = true;
+    const int64_t r = host_answer(job, n);
+    g_last_error = std::string(site) + " answered by the host CRC after: " + why;
+    return job.ok ? r : 0;
+}
+
 // Frames over kOneBytes (no Ethernet frame is): copied into pinned, device-mapped staging and run
 // through the fixed-length kernels on the device's staging stream. On an error the staging stream
 // and words are dropped, so a retry starts from fresh ones.
@@ -1310,16 +1414,16 @@ int dropin_attempt(const void *data, size_t bsize, uint32_t lane, uint32_t *crc)
 // ~28 GB/s, below PCIe Gen5 x16, so large spans are split over a few threads.
 int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len, uint8_t *ok,
                        uint64_t n, uint64_t *ticket) {
-    if (!arena || !off || !len || !ticket || n == 0) return fail(EINVAL, "mapped_submit: bad arguments");
-    const uint64_t tail = ok ? 0 : 4;   // TX writes the FCS after each frame
+    if (!arena || !off || !len || !ok || !ticket || n == 0) return fail(EINVAL, "mapped_submit: bad arguments");
     for (uint64_t i = 0; i < n; i++)
-        if (len[i] > fcs::kOneBytes || off[i] > arena_bytes || len[i] + tail > arena_bytes - off[i])
+        if (len[i] > fcs::kOneBytes || off[i] > arena_bytes || len[i] > arena_bytes - off[i])
             return fail(EINVAL, "mapped_submit: frame %llu out of range", (unsigned long long)i);
     const uint8_t *da = pinned_dev_ptr(arena, arena_bytes);
     const uint8_t *doff = pinned_dev_ptr(off, n * 8), *dlen = pinned_dev_ptr(len, n * 4);
-    uint8_t *dok = ok ? pinned_dev_ptr(ok, n) : nullptr;
-    if (!da || !doff || !dlen || (ok && !dok)) return fail(EINVAL, "mapped_submit: buffers not from fcs_host_alloc");
+    uint8_t *dok = pinned_dev_ptr(ok, n);
+    if (!da || !doff || !dlen || !dok) return fail(EINVAL, "mapped_submit: buffers not from fcs_host_alloc");
     if (injected_batch_fault()) return fail(EIO, "mapped_submit: injected fault (FCS_FAULT_HOOK build)");
+    if (host_only()) return fail(EIO, "mapped_submit: the host batch forms stopped using the GPU after %u failed calls", kMaxRetired);
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
     if (rc) return rc;
@@ -1335,6 +1439,7 @@ int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off
         a.blob = ds->d_one_blob;
         a.base = (uint8_t *)da;
         a.ok = dok;
+        a.out = nullptr;
         a.count = ds->tx_dcount;
         a.count_base = ds->tx_count;
         a.seq = ds->tx_seq + 1;
@@ -1359,6 +1464,7 @@ int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off
     a.off = (const uint64_t *)doff;
     a.len = (const uint32_t *)dlen;
     a.ok = dok;
+    a.out = nullptr;
     a.count = ds->tx_dcount;
     a.count_base = ds->tx_count;
     a.seq = ds->tx_seq + 1;
@@ -1372,12 +1478,34 @@ int fcs::mapped_submit(uint8_t *arena, uint64_t arena_bytes, const uint64_t *off
 }
 
 int fcs::mapped_wait(uint64_t ticket) {
-    // injected: give up at once, as if the wait had timed out, with the kernel still in flight
-    if (injected_batch_fault()) return fail(ETIMEDOUT, "mapped_wait: injected fault (FCS_FAULT_HOOK build)");
     std::vector<DevState *> devs;
     int rc = engine_devices(&devs);
     if (rc) return rc;
-    return wait_flag(devs[0]->tx_stream, devs[0]->tx_flag, ticket, "mapped-list batch");
+    DevState *ds = devs[0];
+    hipStream_t st = nullptr;
+    const uint64_t *flag = nullptr;
+    {
+        std::lock_guard<std::mutex> lk(ds->tx_mu);
+        if (ticket >= ds->tx_first_seq && ds->tx_stream) {
+            st = ds->tx_stream;
+            flag = ds->tx_flag;
+        } else {   // issued on a stream retired since (another batch's wait failed): wait on its word
+            for (const DevState::OldGen &g : ds->tx_old)
+                if (g.first <= ticket && ticket <= g.last) {
+                    st = g.st;
+                    flag = g.flag;
+                }
+            if (!st) return fail(EIO, "mapped_wait: no small-batch stream issued batch %llu", (unsigned long long)ticket);
+        }
+    }
+    // injected: give up at once, as if the wait had timed out, with the kernel still in flight
+    rc = injected_batch_fault() ? fail(ETIMEDOUT, "mapped_wait: injected fault (FCS_FAULT_HOOK build)")
+                                : wait_flag(st, flag, ticket, "mapped-list batch");
+    if (rc) {
+        std::lock_guard<std::mutex> lk(ds->tx_mu);
+        if (ds->tx_stream == st) retire_small(ds);   // not retired by another failed call meanwhile
+    }
+    return rc;
 }
 
 void fcs::host_batch_answered(const char *site, const char *why) {
@@ -1387,6 +1515,8 @@ void fcs::host_batch_answered(const char *site, const char *why) {
                              "(counted in fcs_engine_host_batches; reported once)\n", site, why ? why : "");
     g_host_batches.fetch_add(1, std::memory_order_relaxed);
 }
+
+bool fcs::last_call_host_answered() { return t_host_answered; }
 
 void fcs::staging_copy(uint8_t *dst, const uint8_t *src, uint64_t bytes) {
     constexpr uint64_t kCopySplitBytes = 16ull << 20;
@@ -1468,9 +1598,10 @@ static void destroy_state(DevState *ds) {
         if (L.st) hipStreamDestroy(L.st);
         if (L.flag) hipHostFree(L.flag);
     }
-    if (!ds->q_streams.empty() || !ds->q_host.empty()) (void)hipDeviceSynchronize();
+    if (!ds->q_streams.empty() || !ds->q_host.empty() || !ds->q_dev.empty()) (void)hipDeviceSynchronize();
     for (hipStream_t q : ds->q_streams) hipStreamDestroy(q);
     for (void *h : ds->q_host) hipHostFree(h);
+    for (void *d : ds->q_dev) hipFree(d);
     for (hipEvent_t ev : ds->ctr_done)
         if (ev) hipEventDestroy(ev);
     if (ds->d_blob) hipFree(ds->d_blob);
@@ -1536,6 +1667,7 @@ void fcs_engine_fini(void) {
     g_alias.clear();
     g_alias_retired.clear();
     g_engine_devs.clear();
+    g_retired.store(0, std::memory_order_relaxed);   // the retired resources are freed with their states
     hipSetDevice(cur);
 }
 
@@ -1578,7 +1710,7 @@ int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t
     if (!arena || !off || !len || !out) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
     HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, out, nullptr, 0, n, nullptr, nullptr};
-    return run_host_sharded(job, n);
+    return (int)with_host_answer(__func__, job, n, [&] { return (int64_t)run_host_sharded(job, n); });
 }
 
 int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64_t n,
@@ -1588,7 +1720,7 @@ int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64
     if (n > 1 && stride < len) return fail(EINVAL, "stride %llu < len %u", (unsigned long long)stride, len);
     HostJob job{(const uint8_t *)base, (n - 1) * stride + len, nullptr, nullptr, n > 1 ? stride : len, len,
                 out, nullptr, 0, n, nullptr, nullptr};
-    return run_host_sharded(job, n);
+    return (int)with_host_answer(__func__, job, n, [&] { return (int64_t)run_host_sharded(job, n); });
 }
 
 int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n) {
@@ -1598,17 +1730,19 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
         if ((uint64_t)len[i] + 4 > stride)
             return fail(EINVAL, "frame %llu: len %u + FCS does not fit stride %llu", (unsigned long long)i,
                         len[i], (unsigned long long)stride);
-    if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)base, len[0]);
-    if (n * stride <= kZeroCopyMaxBytes && (pinned_dev_ptr(base, n * stride) || is_pinned(base))) {
-        std::vector<DevState *> devs;
-        int rc = engine_devices(&devs);
-        if (rc) return rc;
-        rc = run_tx_zero_copy(devs[0], (uint8_t *)base, n * stride, stride, nullptr, len, n);
-        if (rc <= 0) return rc;   // 1: the frames are not device-mapped; take the staged pipeline
-    }
     HostJob job{(const uint8_t *)base, n * stride, nullptr, len, stride, 0, nullptr, (uint8_t *)base, 0, n,
                 nullptr, nullptr};
-    return run_host_sharded(job, n);
+    return (int)with_host_answer(__func__, job, n, [&]() -> int64_t {
+        if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)base, len[0]);
+        if (n * stride <= kZeroCopyMaxBytes && (pinned_dev_ptr(base, n * stride) || is_pinned(base))) {
+            std::vector<DevState *> devs;
+            int rc = engine_devices(&devs);
+            if (rc) return rc;
+            rc = run_tx_zero_copy(devs[0], (uint8_t *)base, n * stride, stride, nullptr, len, n);
+            if (rc <= 0) return rc;   // 1: the frames are not device-mapped; take the staged pipeline
+        }
+        return run_host_sharded(job, n);
+    });
 }
 
 int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
@@ -1616,18 +1750,19 @@ int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *o
     if (n == 0) return 0;
     if (!arena || !off || !len) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 4, __func__)) return rc;
-    if (injected_batch_fault()) return fail(EIO, "ether_fcs_tx_batch_host: injected fault (FCS_FAULT_HOOK build)");
-    if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)arena + off[0], len[0]);
-    if (arena_bytes <= kZeroCopyMaxBytes && (pinned_dev_ptr(arena, arena_bytes) || is_pinned(arena))) {
-        std::vector<DevState *> devs;
-        int rc = engine_devices(&devs);
-        if (rc) return rc;
-        rc = run_tx_zero_copy(devs[0], (uint8_t *)arena, arena_bytes, 0, off, len, n);
-        if (rc <= 0) return rc;
-    }
     HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, nullptr, (uint8_t *)arena, 0, n, nullptr,
                 nullptr};
-    return run_host_sharded(job, n);
+    return (int)with_host_answer(__func__, job, n, [&]() -> int64_t {
+        if (n == 1 && len[0] <= fcs::kOneBytes) return tx_one((uint8_t *)arena + off[0], len[0]);
+        if (arena_bytes <= kZeroCopyMaxBytes && (pinned_dev_ptr(arena, arena_bytes) || is_pinned(arena))) {
+            std::vector<DevState *> devs;
+            int rc = engine_devices(&devs);
+            if (rc) return rc;
+            rc = run_tx_zero_copy(devs[0], (uint8_t *)arena, arena_bytes, 0, off, len, n);
+            if (rc <= 0) return rc;
+        }
+        return run_host_sharded(job, n);
+    });
 }
 
 // ---- RX verification: frames that carry their FCS trailer ----
@@ -1662,19 +1797,22 @@ int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uin
     if (n == 0) return 0;
     if (!arena || !off || !len || !ok) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
-    if (injected_batch_fault()) return fail(EIO, "ether_fcs_verify_host: injected fault (FCS_FAULT_HOOK build)");
-    if (arena_bytes <= kZeroCopyMaxBytes) {
-        if (const uint8_t *darena = pinned_dev_ptr(arena, arena_bytes)) {   // the RX queue's arena
-            std::vector<DevState *> devs;
-            const int rc = engine_devices(&devs);
-            if (rc) return rc;
-            return run_verify_zero_copy(devs[0], darena, arena_bytes, off, len, ok, n);
+    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, nullptr, nullptr, 0, n, ok, nullptr};
+    return with_host_answer(__func__, job, n, [&]() -> int64_t {
+        if (arena_bytes <= kZeroCopyMaxBytes) {
+            if (const uint8_t *darena = pinned_dev_ptr(arena, arena_bytes)) {   // the RX queue's arena
+                std::vector<DevState *> devs;
+                const int rc = engine_devices(&devs);
+                if (rc) return rc;
+                return run_verify_zero_copy(devs[0], darena, arena_bytes, off, len, ok, n);
+            }
         }
-    }
-    std::atomic<uint64_t> bad{0};
-    HostJob job{(const uint8_t *)arena, arena_bytes, off, len, 0, 0, nullptr, nullptr, 0, n, ok, &bad};
-    const int rc = run_host_sharded(job, n);
-    return rc ? rc : (int64_t)bad.load();
+        std::atomic<uint64_t> bad{0};
+        HostJob jb = job;
+        jb.bad = &bad;
+        const int rc = run_host_sharded(jb, n);
+        return rc ? rc : (int64_t)bad.load();
+    });
 }
 
 // Drop-in for src/ether_fcs.c:4. Synchronous, reentrant. The reference cannot fail and has no
@@ -1715,48 +1853,44 @@ uint64_t fcs_engine_host_fallbacks(void) { return g_host_fallbacks.load(std::mem
 
 uint32_t fcs_debug_stream_unit_frames(void) { return fcs::kStUnitFrames; }
 
-// The same decisions as launch_fixed and fcs::launch_fcs, named (no device call).
-int fcs_debug_fixed_route(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, char *out, uint64_t cap) {
-    if (!out || cap == 0) return -EINVAL;
-    std::string r;
-    if (n == 0) {
-        r = "none";
-    } else {
-        fcs::KParams p{};
-        p.base = base;
-        p.stride = stride;
-        p.n = n;
-        p.lo4 = floor4(base);
-        p.hi4 = ceil4(base + (n - 1) * stride + len);
-        p.flen = len;
-        p.fseg = segments(len);
-        p.zmax = mask_bound(len);
-        const bool big = n > g_var_threshold.load(std::memory_order_relaxed), tiny = fcs::fixed_tiny(p);
-        if (big && fcs::fixed_short(p)) {
-            r = "short:" + std::to_string(fcs::short_wd(len));
-        } else if (len <= kFixedFlatMaxLen && big &&
-                   !(!tiny && (fcs::fixed_wide4(p) || fcs::fixed_wide8(p) || fcs::fixed_wide(p) || fcs::fixed_dma(p)))) {
-            r = "flat";
-        } else if (!tiny && fcs::fixed_wide4(p)) {
-            r = "wide4:" + std::to_string(fcs::wide4_wd(p));
-        } else if (!tiny && fcs::fixed_wide8(p)) {
-            r = "wide8:" + std::to_string(fcs::wide8_wd(p));
-        } else if (!tiny && fcs::fixed_wide(p)) {
-            r = "wide16:" + std::to_string(fcs::wide_wd(p));
-        } else if (fcs::fixed_segil(p)) {
-            r = "segment";
-        } else if (!tiny && fcs::fixed_dma(p)) {
-            r = "lds-dma";
-        } else if (tiny) {
-            r = "tiny";
-        } else {
-            r = fcs::fixed_single(p) ? "single" : "generic";
-        }
+// The name of a fixed-length route (fcs_debug_fixed_route, fcs_debug_last_fixed_launch).
+static std::string route_name(const fcs::FixedRoute &r) {
+    switch (r.kernel) {
+        case fcs::FixedKernel::kShort: return "short:" + std::to_string(r.wd);
+        case fcs::FixedKernel::kFlat: return "flat";
+        case fcs::FixedKernel::kWide4: return "wide4:" + std::to_string(r.wd);
+        case fcs::FixedKernel::kWide8: return "wide8:" + std::to_string(r.wd);
+        case fcs::FixedKernel::kWide16: return "wide16:" + std::to_string(r.wd);
+        case fcs::FixedKernel::kSegment: return "segment";
+        case fcs::FixedKernel::kDma: return "lds-dma";
+        case fcs::FixedKernel::kTiny: return "tiny";
+        case fcs::FixedKernel::kSingle: return "single";
+        case fcs::FixedKernel::kGeneric: return "generic";
     }
+    return "?";
+}
+
+static int copy_name(const std::string &r, char *out, uint64_t cap) {
+    if (!out || cap == 0) return -EINVAL;
     const uint64_t k = std::min<uint64_t>(r.size(), cap - 1);
     std::memcpy(out, r.data(), k);
     out[k] = 0;
     return (int)k;
+}
+
+// fcs::route_fixed's decision for a batch, named (no device call).
+int fcs_debug_fixed_route(uint64_t base, uint64_t stride, uint32_t len, uint64_t n, char *out, uint64_t cap) {
+    if (n == 0) return copy_name("none", out, cap);
+    const fcs::KParams p = fixed_params(nullptr, (const void *)base, stride, len, n);
+    return copy_name(route_name(fcs::route_fixed(p, n > g_var_threshold.load(std::memory_order_relaxed))), out, cap);
+}
+
+// The kernel the last fixed-length launch of this process actually launched (launch_fixed_route
+// records it in the case that launches), with its workgroup size: "<route name>/<threads>".
+int fcs_debug_last_fixed_launch(char *out, uint64_t cap) {
+    const fcs::FixedRoute r = fcs::last_fixed_launch();
+    if (r.threads == 0) return copy_name("none", out, cap);
+    return copy_name(route_name(r) + "/" + std::to_string(r.threads), out, cap);
 }
 
 int64_t fcs_debug_stream_listed(void) {
@@ -1788,15 +1922,11 @@ uint64_t fcs_engine_host_batches(void) { return g_host_batches.load(std::memory_
 #ifdef FCS_FAULT_HOOK
 void fcs_debug_fail_next(int attempts) { g_inject_faults = attempts; }
 void fcs_debug_timeout_next(int attempts) { g_inject_timeouts = attempts; }
-void fcs_debug_fail_batches(int skip, int calls) {
-    std::lock_guard<std::mutex> lk(g_inject_batch_mu);
-    g_inject_batch_skip = skip;
-    g_inject_batch_calls = calls;
-}
-int fcs_debug_batch_faults_left(void) {
-    std::lock_guard<std::mutex> lk(g_inject_batch_mu);
-    return g_inject_batch_skip + g_inject_batch_calls;
-}
+void fcs_debug_fail_batches(int skip, int calls) { g_inject_batch.arm(skip, calls); }
+void fcs_debug_late_batches(int skip, int calls) { g_inject_late.arm(skip, calls); }
+int fcs_debug_batch_faults_left(void) { return g_inject_batch.left() + g_inject_late.left(); }
+// Resources retired after failed host batch calls so far (host-only from kMaxRetired on).
+uint32_t fcs_debug_retired(void) { return g_retired.load(std::memory_order_relaxed); }
 #endif
 
 int fcs_shard_plan(const uint32_t *len, uint64_t n, uint32_t parts, uint64_t *cut) {
@@ -1835,8 +1965,33 @@ void *fcs_host_alloc(uint64_t bytes) {
     return p;
 }
 
+// A kernel set aside by a failed call (quarantined stream) may still read pinned memory the caller
+// now frees: wait for the quarantined streams to drain, at most 10 s, and keep the memory mapped (a
+// leak, never a GPU page fault) if one is still busy.
 void fcs_host_free(void *p) {
     if (!p) return;
+    std::vector<hipStream_t> busy;
+    {
+        std::lock_guard<std::mutex> lk(g_mu);
+        auto take = [&busy](DevState *ds) {
+            std::lock_guard<std::mutex> ql(ds->q_mu);
+            busy.insert(busy.end(), ds->q_streams.begin(), ds->q_streams.end());
+        };
+        for (auto &up : g_dev)
+            if (up) take(up.get());
+        for (auto &kv : g_alias)
+            if (kv.second) take(kv.second.get());
+    }
+    const auto t0 = std::chrono::steady_clock::now();
+    for (hipStream_t st : busy)
+        while (hipStreamQuery(st) == hipErrorNotReady) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+                (void)hipGetLastError();
+                return;   // kept: a kernel of a failed call may still read it
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
+    (void)hipGetLastError();
     {
         std::lock_guard<std::mutex> lk(g_pin_mu);
         g_pinned.erase((uintptr_t)p);

@@ -24,6 +24,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
 #include "fcs_launch.hpp"
 #include "fcs_tables.hpp"
 #include "wave_sync.hpp"
@@ -2078,6 +2080,13 @@ static_assert(kStUnitFrames * kStMaxLen + 16 < (1u << (32 - kStLenBits)) && kStM
 #ifndef FCS_ST_AUX   // cache policy of the item DMA's middle rows (measurement-only override)
 #define FCS_ST_AUX 2
 #endif
+// Items at 128-B line boundaries (measurement-only FCS_ST_ALIGN128): a unit's first item starts at
+// the line below its first frame (not past the arena's first 16-B piece), so consecutive items share
+// no line and the first and last rows can be non-temporal too (FCS_ST_EDGE_AUX, default: the
+// default policy, which keeps a line the neighbouring item shares in L2).
+#ifndef FCS_ST_EDGE_AUX
+#define FCS_ST_EDGE_AUX 0
+#endif
 
 // A_n(s) ^ extra from the nibble table at holes h .. h + 3 (h = 4 q for table q; h may differ per
 // lane). Nibble t sits in hole h + t / 2, in the half (t + q) & 1 of its 32 banks: lanes shifting by
@@ -2200,15 +2209,15 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         lds_void *ls = (lds_void *)slot;
         if (X + kStItem <= hi16) {   // wave-uniform: the whole item lies inside the arena's 16-B pieces
             // first and last rows at the default policy (lines shared with the neighbouring items)
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 0, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 0, FCS_ST_EDGE_AUX);
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 1024, FCS_ST_AUX);
             __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 2048, FCS_ST_AUX);
-            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 3072, 0);
+            __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 3072, FCS_ST_EDGE_AUX);
         } else {
-            if (a < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 0, 0);
+            if (a < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 0, FCS_ST_EDGE_AUX);
             if (a + 1024 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 1024, FCS_ST_AUX);
             if (a + 2048 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 2048, FCS_ST_AUX);
-            if (a + 3072 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 3072, 0);
+            if (a + 3072 < hi16) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), ls, 16, 3072, FCS_ST_EDGE_AUX);
         }
     };
     // piece m of this lane's chunk in the slot (loop invariants)
@@ -2246,7 +2255,12 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         // ---- geometry, relative to X0 (the first item's start) ----
         const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
+#ifdef FCS_ST_ALIGN128
+        const uint64_t lo16 = p.lo4 & ~15ull;
+        const uint64_t X0 = (s0 & ~127ull) > lo16 ? (s0 & ~127ull) : lo16;
+#else
         const uint64_t X0 = s0 & ~15ull;
+#endif
         dma_item(X0);
         const uint64_t o0 = X0 - p.base;   // arena offset of X0
         const uint32_t last = nf - 1;
@@ -2383,6 +2397,17 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             }
             const uint32_t c0 = x;
             x = hole_shift(lds, c0, kStHoleWord + 4u * 8u, y);
+#elif defined(FCS_ST_SMASK)
+            // measurement-only: the state before word k picked by lane masks built with scalar ops from
+            // the four bit planes of k (a v_cndmask on an SGPR mask per word, no per-word v_cmp)
+            const uint64_t kb0 = __ballot(k & 1u), kb1 = __ballot(k & 2u), kb2 = __ballot(k & 4u), kb3 = __ballot(k & 8u);
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                const uint64_t mi = ((i & 1) ? kb0 : ~kb0) & ((i & 2) ? kb1 : ~kb1) & ((i & 4) ? kb2 : ~kb2) &
+                                    ((i & 8) ? kb3 : ~kb3);
+                if (__builtin_amdgcn_inverse_ballot_w64(mi)) xk = x;
+                x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
+            }
 #else
 #pragma unroll
             for (int i = 0; i < 16; i++) {
@@ -2682,15 +2707,15 @@ __device__ __forceinline__ uint32_t one_frame_reg(uint32_t *t, const uint32_t *b
 }
 
 // A small-batch frame's result: RX verify writes ok[f] (the frame carries its trailer; it checks
-// iff the residue shows), TX writes the FCS little-endian right after the frame
-// (src/linux/ether.c:263). Then the frame counts itself done; the batch's last frame stores seq.
-__device__ __forceinline__ void small_finish(uint32_t fcs, uint8_t *ok, uint32_t f, uint64_t start, uint32_t L,
+// iff the residue shows), TX writes out[f] (the host stores it little-endian right after the frame,
+// src/linux/ether.c:263, once the batch is complete). Both arrays are the library's own mapped
+// memory. Then the frame counts itself done; the batch's last frame stores seq.
+__device__ __forceinline__ void small_finish(uint32_t fcs, uint8_t *ok, uint32_t *out, uint32_t f, uint32_t L,
                                              int lane, unsigned long long *count, uint64_t count_base, uint32_t n,
                                              uint64_t *flag, uint64_t seq) {
-    if (ok) {
-        if (lane == 0) ok[f] = (L >= 4 && fcs == 0x2144DF1Cu) ? 1 : 0;
-    } else if (lane < 4) {
-        *reinterpret_cast<__attribute__((address_space(1))) uint8_t *>(start + L + lane) = (uint8_t)(fcs >> (8 * lane));
+    if (lane == 0) {
+        if (ok) ok[f] = (L >= 4 && fcs == 0x2144DF1Cu) ? 1 : 0;
+        else out[f] = fcs;
     }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");   // this frame's result has reached host memory
     if (lane == 0) {
@@ -2702,8 +2727,8 @@ __device__ __forceinline__ void small_finish(uint32_t fcs, uint8_t *ok, uint32_t
 
 // One workgroup (one wave) per frame, so the frames' PCIe reads come from as many CUs: one CU
 // reading 16 frames of host memory took 17.7 us, against 10.6 us for one. Each wave writes its
-// FCS into the frame, makes it visible system-wide and counts itself done on a device counter;
-// the last one to finish stores `seq` into the mapped completion word.
+// FCS (or check), makes it visible system-wide and counts itself done on a device counter; the
+// last one to finish stores `seq` into the mapped completion word.
 __global__ __launch_bounds__(64) void fcs_tx_small_kernel(TxSmallArgs a) {
     __shared__ __attribute__((aligned(16))) uint32_t t[kOneBlobWords];
     __shared__ __attribute__((aligned(16))) uint8_t win[kOneWinBytes];
@@ -2716,7 +2741,7 @@ __global__ __launch_bounds__(64) void fcs_tx_small_kernel(TxSmallArgs a) {
     const uint32_t ki = *(const __attribute__((address_space(4))) uint32_t *)(ka + offsetof(TxSmallArgs, kinit) + 4 * f);
     const uint64_t start = (uint64_t)a.base + o;
     const uint32_t x = one_frame_reg(t, a.blob, win, start, start + L, lane);
-    small_finish(~(x ^ ki), a.ok, f, start, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
+    small_finish(~(x ^ ki), a.ok, a.out, f, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
 }
 
 __global__ __launch_bounds__(64) void fcs_small_list_kernel(ListArgs a) {
@@ -2729,7 +2754,7 @@ __global__ __launch_bounds__(64) void fcs_small_list_kernel(ListArgs a) {
     const uint32_t ki = a.kinit[L < kOneBytes ? L : kOneBytes];
     const uint64_t start = (uint64_t)a.base + o;
     const uint32_t x = one_frame_reg(t, a.blob, win, start, start + L, lane);
-    small_finish(~(x ^ ki), a.ok, f, start, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
+    small_finish(~(x ^ ki), a.ok, a.out, f, L, lane, a.count, a.count_base, a.n, a.flag, a.seq);
 }
 
 // TX mode helper: after the FCS kernel wrote crc[i], store it little-endian after each frame.
@@ -2747,48 +2772,91 @@ __global__ __launch_bounds__(256) void tx_store_kernel(uint8_t *base, uint64_t s
 }
 
 // ---- host-side launchers (the engine TU never names the kernels) ----
+// Variable-length batches (and nothing else): windowed = throughput form (64-frame windows per wave,
+// chunks dealt flat to the lanes), otherwise one quarter-wave per frame, every frame in flight at
+// once (small batches).
 hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    if (!var) return hipErrorInvalidValue;   // fixed-length batches: launch_fixed_route
     const bool tiny = fixed_tiny(p);
-    const bool single = !var && fixed_single(p);
-    // fixed_threads(p) (fcs_launch.hpp) picks the workgroup size; the host sized the grid with it
-#define FCS_LAUNCH(V, T, S) \
-    hipLaunchKernelGGL((fcs_kernel<V, T, S, kWgThreads>), dim3(grid), dim3(kWgThreads), 0, st, p)
-    if (var) {
-        // windowed: throughput form (64-frame windows per wave, chunks dealt flat to the lanes);
-        // otherwise one quarter-wave per frame, every frame in flight at once (small batches)
-        if (!windowed) {
-            if (tiny) FCS_LAUNCH(true, true, false);
-            else FCS_LAUNCH(true, false, false);
-        } else if (tiny) {
-            hipLaunchKernelGGL((fcs_flat_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
-        } else {
-            hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    if (!windowed) {
+        if (tiny) hipLaunchKernelGGL((fcs_kernel<true, true, false, kWgThreads>), dim3(grid), dim3(kWgThreads), 0, st, p);
+        else hipLaunchKernelGGL((fcs_kernel<true, false, false, kWgThreads>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    } else if (tiny) {
+        hipLaunchKernelGGL((fcs_flat_kernel<true>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    } else {
+        hipLaunchKernelGGL((fcs_flat_kernel<false>), dim3(grid), dim3(kWgThreads), 0, st, p);
+    }
+    return hipGetLastError();
+}
+
+namespace {
+std::atomic<uint64_t> g_last_fixed{0};   // the last launch_fixed_route launch, packed (kernel, wd, threads)
+}
+
+FixedRoute last_fixed_launch() {
+    const uint64_t v = g_last_fixed.load(std::memory_order_relaxed);
+    FixedRoute r{};
+    r.kernel = (FixedKernel)(v & 0xFF);
+    r.wd = (int)((v >> 8) & 0xFFFF);
+    r.threads = (int)((v >> 24) & 0xFFFF);
+    r.tiny = (v >> 40) & 1;
+    return r;
+}
+
+// Launches exactly the kernel route_fixed named: each case records what it launched (kernel, its
+// window or mask template argument, workgroup size), so a test can compare the launch with the
+// route (tests/test_gpu_routing.py).
+hipError_t launch_fixed_route(const FixedRoute &r, const KParams &p, int grid, hipStream_t st) {
+    (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    auto rec = [](FixedKernel k, int wd, int threads, bool tiny) {
+        g_last_fixed.store((uint64_t)k | ((uint64_t)(uint16_t)wd << 8) | ((uint64_t)(uint16_t)threads << 24) |
+                               ((uint64_t)tiny << 40),
+                           std::memory_order_relaxed);
+    };
+#define FCS_GO(K, WD, T, TINY, ...)                                             \
+    do {                                                                        \
+        hipLaunchKernelGGL(__VA_ARGS__, dim3(grid), dim3(T), 0, st, p);         \
+        rec(K, WD, T, TINY);                                                    \
+    } while (0)
+    switch (r.kernel) {
+    case FixedKernel::kShort:
+        switch (r.wd) {
+            case 16: FCS_GO(FixedKernel::kShort, 16, kWgThreads, false, fcs_short_kernel<16>); break;
+            case 24: FCS_GO(FixedKernel::kShort, 24, kWgThreads, false, fcs_short_kernel<24>); break;
+            case 32: FCS_GO(FixedKernel::kShort, 32, kWgThreads, false, fcs_short_kernel<32>); break;
+            default: return hipErrorInvalidValue;
         }
-    } else if (!tiny && fixed_wide4(p)) {
+        break;
+    case FixedKernel::kFlat:
+        if (r.tiny) FCS_GO(FixedKernel::kFlat, 0, kWgThreads, true, fcs_flat_kernel<true>);
+        else FCS_GO(FixedKernel::kFlat, 0, kWgThreads, false, fcs_flat_kernel<false>);
+        break;
+    case FixedKernel::kWide4:
 #define FCS_WIDE4(W) \
-    case W: hipLaunchKernelGGL((fcs_wide_kernel<W, 4>), dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
-        switch (wide4_wd(p)) {
+    case W: FCS_GO(FixedKernel::kWide4, W, wide_threads(W), false, (fcs_wide_kernel<W, 4>)); break;
+        switch (r.wd) {
             FCS_WIDE4(9) FCS_WIDE4(10) FCS_WIDE4(11) FCS_WIDE4(12) FCS_WIDE4(13) FCS_WIDE4(14) FCS_WIDE4(15)
             FCS_WIDE4(16) FCS_WIDE4(18) FCS_WIDE4(19) FCS_WIDE4(20) FCS_WIDE4(21) FCS_WIDE4(22) FCS_WIDE4(23)
-            FCS_WIDE4(24) FCS_WIDE4(25)
-            default: hipLaunchKernelGGL((fcs_wide_kernel<26, 4>), dim3(grid), dim3(wide_threads(26)), 0, st, p);
+            FCS_WIDE4(24) FCS_WIDE4(25) FCS_WIDE4(26)
+            default: return hipErrorInvalidValue;
         }
 #undef FCS_WIDE4
-    } else if (!tiny && fixed_wide8(p)) {
+        break;
+    case FixedKernel::kWide8:
 #define FCS_WIDE8(W) \
-    case W: hipLaunchKernelGGL((fcs_wide_kernel<W, 8>), dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
-        switch (wide8_wd(p)) {
+    case W: FCS_GO(FixedKernel::kWide8, W, wide_threads(W), false, (fcs_wide_kernel<W, 8>)); break;
+        switch (r.wd) {
             FCS_WIDE8(11) FCS_WIDE8(12) FCS_WIDE8(14) FCS_WIDE8(15) FCS_WIDE8(16) FCS_WIDE8(18) FCS_WIDE8(19)
-            FCS_WIDE8(20) FCS_WIDE8(22) FCS_WIDE8(23) FCS_WIDE8(24) FCS_WIDE8(26) FCS_WIDE8(27)
-            default: hipLaunchKernelGGL((fcs_wide_kernel<28, 8>), dim3(grid), dim3(wide_threads(28)), 0, st, p);
+            FCS_WIDE8(20) FCS_WIDE8(22) FCS_WIDE8(23) FCS_WIDE8(24) FCS_WIDE8(26) FCS_WIDE8(27) FCS_WIDE8(28)
+            default: return hipErrorInvalidValue;
         }
 #undef FCS_WIDE8
-    } else if (!tiny && fixed_wide(p)) {
-        const int wd = wide_wd(p);
+        break;
+    case FixedKernel::kWide16:
 #define FCS_WIDE(W) \
-    case W: hipLaunchKernelGGL(fcs_wide_kernel<W>, dim3(grid), dim3(wide_threads(W)), 0, st, p); break;
-        switch (wd) {
+    case W: FCS_GO(FixedKernel::kWide16, W, wide_threads(W), false, fcs_wide_kernel<W>); break;
+        switch (r.wd) {
 #if FCS_WIDE_MID_WD_MIN <= 11   // the mid-length widths from kWideMidMin (11 .. 12: measurement builds)
             FCS_WIDE(11)
 #endif
@@ -2810,30 +2878,38 @@ hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipSt
 #if FCS_WIDE_MID_WD_MIN <= 19
             FCS_WIDE(19)
 #endif
-            FCS_WIDE(20) FCS_WIDE(22) FCS_WIDE(23) FCS_WIDE(24) FCS_WIDE(26) FCS_WIDE(30)
-            default: hipLaunchKernelGGL(fcs_wide_kernel<32>, dim3(grid), dim3(wide_threads(32)), 0, st, p);
+            FCS_WIDE(20) FCS_WIDE(22) FCS_WIDE(23) FCS_WIDE(24) FCS_WIDE(26) FCS_WIDE(30) FCS_WIDE(32)
+            default: return hipErrorInvalidValue;
         }
 #undef FCS_WIDE
-    } else if (fixed_segil(p)) {
-        hipLaunchKernelGGL(fcs_segil_kernel, dim3(grid), dim3(kSegilThreads), 0, st, p);
-    } else if (!tiny && fixed_dma(p)) {
-        if (p.zmax <= 8) hipLaunchKernelGGL((fcs_dma_kernel<2, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
-        else hipLaunchKernelGGL((fcs_dma_kernel<kSingleMaskWords, false>), dim3(grid), dim3(kDmaWgThreads), 0, st, p);
-    } else if (tiny) {
-        if (single) FCS_LAUNCH(false, true, true);
-        else FCS_LAUNCH(false, true, false);
-    } else if (single) {
+        break;
+    case FixedKernel::kSegment:
+        FCS_GO(FixedKernel::kSegment, 0, kSegilThreads, false, fcs_segil_kernel);
+        break;
+    case FixedKernel::kDma:
+        if (r.wd == 2) FCS_GO(FixedKernel::kDma, 2, kDmaWgThreads, false, (fcs_dma_kernel<2, false>));
+        else if (r.wd == kSingleMaskWords) FCS_GO(FixedKernel::kDma, kSingleMaskWords, kDmaWgThreads, false, (fcs_dma_kernel<kSingleMaskWords, false>));
+        else return hipErrorInvalidValue;
+        break;
+    case FixedKernel::kTiny:
+        if (r.wd) FCS_GO(FixedKernel::kTiny, 1, kWgThreads, true, (fcs_kernel<false, true, true, kWgThreads>));
+        else FCS_GO(FixedKernel::kTiny, 0, kWgThreads, true, (fcs_kernel<false, true, false, kWgThreads>));
+        break;
+    case FixedKernel::kSingle:
 #ifdef FCS_OLD_SINGLE   // measurement-only build: generic kernel's SINGLE instantiation
-        FCS_LAUNCH(false, false, true);
+        FCS_GO(FixedKernel::kSingle, 0, kWgThreads, false, (fcs_kernel<false, false, true, kWgThreads>));
 #else
-        hipLaunchKernelGGL(fcs_single_kernel, dim3(grid), dim3(kFixedWgThreads), 0, st, p);
+        FCS_GO(FixedKernel::kSingle, 0, kFixedWgThreads, false, fcs_single_kernel);
 #endif
-    } else if (fixed_threads(p) == kFixedWgThreads) {
-        hipLaunchKernelGGL((fcs_kernel<false, false, false, kFixedWgThreads>), dim3(grid), dim3(kFixedWgThreads), 0, st, p);
-    } else {
-        FCS_LAUNCH(false, false, false);
+        break;
+    case FixedKernel::kGeneric:
+        if (r.threads == kFixedWgThreads)
+            FCS_GO(FixedKernel::kGeneric, 0, kFixedWgThreads, false, (fcs_kernel<false, false, false, kFixedWgThreads>));
+        else
+            FCS_GO(FixedKernel::kGeneric, 0, kWgThreads, false, (fcs_kernel<false, false, false, kWgThreads>));
+        break;
     }
-#undef FCS_LAUNCH
+#undef FCS_GO
     return hipGetLastError();
 }
 

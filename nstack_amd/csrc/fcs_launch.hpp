@@ -76,9 +76,11 @@ struct OneArgs {
 
 // Small TX (or RX verify) batches in mapped host memory (fcs_tx_small_kernel): 1..kTxSmallMax
 // frames of up to kOneBytes bytes each, their offsets, lengths and A_len(0xFFFFFFFF) in the kernel
-// arguments. One workgroup per frame writes its FCS into the frame in host memory; the last one
-// done (device counter `count`, which has reached count_base when the launch starts) stores
-// `seq` into `flag`.
+// arguments. One workgroup per frame writes its FCS (TX: out[i]) or its check (RX: ok[i]) into
+// library-owned mapped memory, never into the caller's frames, so a kernel left in flight by a
+// failed call cannot write into an arena the caller has reused (the host stores the FCSs after the
+// completion). The last frame done (device counter `count`, which has reached count_base when the
+// launch starts) stores `seq` into `flag`.
 // The same kernel body with the frame list in (mapped) memory instead of the arguments, for any
 // batch size (fcs_small_list_kernel): RX batches checked while the next recvmmsg runs.
 struct ListArgs {
@@ -88,7 +90,8 @@ struct ListArgs {
     uint8_t *base;           // device address of the (mapped) arena
     const uint64_t *off;     // device addresses of mapped arrays of n entries
     const uint32_t *len;
-    uint8_t *ok;             // null: TX (write each FCS); else RX verify
+    uint8_t *ok;             // null: TX (out[i] = FCS); else RX verify
+    uint32_t *out;
     unsigned long long *count;
     uint64_t count_base;
     uint64_t seq;
@@ -99,7 +102,8 @@ struct TxSmallArgs {
     uint64_t *flag;
     const uint32_t *blob;    // kOneBlobWords
     uint8_t *base;           // device address of the (mapped) arena
-    uint8_t *ok;             // null: TX (write each FCS); else RX verify: ok[i] (mapped) per frame
+    uint8_t *ok;             // null: TX (out[i] = FCS, mapped); else RX verify: ok[i] (mapped) per frame
+    uint32_t *out;
     unsigned long long *count;
     uint64_t count_base;
     uint64_t seq;
@@ -298,16 +302,81 @@ static_assert(short_wd(1) == 16 && short_wd(65) == 24 && short_wd(97) == 32 && s
 inline bool fixed_short(const KParams &p) {
     return p.flen >= 1 && p.flen <= kShortMaxLen && short_wd(p.flen) != 0 && !fixed_tiny(p);
 }
-inline int fixed_threads(const KParams &p) {
-    if (!fixed_tiny(p) && fixed_wide4(p)) return wide_threads(wide4_wd(p));
-    if (!fixed_tiny(p) && fixed_wide8(p)) return wide_threads(wide8_wd(p));
-    if (!fixed_tiny(p) && fixed_wide(p)) return wide_threads(wide_wd(p));
-    if (fixed_segil(p)) return kSegilWgThreads;
-    if (!fixed_tiny(p) && fixed_dma(p)) return kDmaWgThreads;
-    return !fixed_tiny(p) && (fixed_single(p) || p.fseg >= kWideSegs) ? kFixedWgThreads : kWgThreads;
+// Fixed-length batches of frames up to this length (and more than the small-batch threshold) take
+// the flat chunk stream when no slot kernel takes them: a 64-B frame then costs one lane instead of a
+// quarter-wave. Measured against the quarter-wave kernel (tools/ab.py): 64 B 11x,
+// 576 B 2.1x, 1300 B +6.5 %; 1504..1536 B stay on the single kernel (the flat kernel is 9 % slower
+// at 1518 B). The slot kernels go first where their slots take the batch.
+#ifndef FCS_FIXED_FLAT_MAX   // measurement-only override (0 = never)
+#define FCS_FIXED_FLAT_MAX 1503
+#endif
+constexpr uint32_t kFixedFlatMaxLen = FCS_FIXED_FLAT_MAX;
+// The flat kernel hands its 64-frame windows out dynamically once there are at least this many
+// windows per wave of the grid; the generic and segment kernels their 4-frame units from this many
+// units per wave (the LDS-DMA family: kDmaDynMinItemsPerWave items).
+#ifndef FCS_FLAT_DYN_MIN   // measurement-only override (a huge value keeps the flat kernel static)
+#define FCS_FLAT_DYN_MIN 4
+#endif
+constexpr uint64_t kFlatDynMinWindowsPerWave = FCS_FLAT_DYN_MIN;
+#ifndef FCS_FIXED_DYN_MIN   // measurement-only override (a huge value keeps the kernel static)
+#define FCS_FIXED_DYN_MIN 4
+#endif
+constexpr uint64_t kFixedDynMinUnitsPerWave = FCS_FIXED_DYN_MIN;
+#ifndef FCS_SHORT_WG_PER_CU   // measurement-only: workgroups per CU (2: -6 to -8 %)
+#define FCS_SHORT_WG_PER_CU 1
+#endif
+
+// THE routing decision for fixed-length batches: launch_fixed (engine) sizes the
+// grid and leases the work counter from it, launch_fixed_route (fcs_kernel.hip) launches exactly
+// the kernel it names, and fcs_debug_fixed_route names it. big: more frames than the small-batch
+// threshold (fcs_engine_set_var_threshold).
+enum class FixedKernel : uint8_t { kShort, kFlat, kWide4, kWide8, kWide16, kSegment, kDma, kTiny, kSingle, kGeneric };
+struct FixedRoute {
+    FixedKernel kernel;
+    int wd;                  // short: window dwords W; wide: WD; LDS-DMA: front mask words; tiny: 1 if single
+    bool tiny;               // flat / generic: the tiny-arena instantiation (guarded loads)
+    int threads;             // workgroup size
+    uint32_t item_frames;    // frames per dispenser item (unit, window)
+    uint64_t dyn_min;        // items per wave from which the schedule is dynamic (0: always static)
+    uint32_t zmax;           // the front-mask bound the kernel is launched with
+};
+inline FixedRoute route_fixed(const KParams &p, bool big) {
+    const bool tiny = fixed_tiny(p);
+    const bool slot = !tiny && (fixed_wide4(p) || fixed_wide8(p) || fixed_wide(p) || fixed_dma(p));
+    if (big && fixed_short(p))
+        return {FixedKernel::kShort, short_wd(p.flen), false, kWgThreads, 64, kDmaDynMinItemsPerWave, p.zmax};
+    if (p.flen <= kFixedFlatMaxLen && big && !slot)   // len == null tells the flat kernel the length is p.flen
+        return {FixedKernel::kFlat, 0, tiny, kWgThreads, 64, kFlatDynMinWindowsPerWave, kChunkBytes};
+    if (!tiny && fixed_wide4(p)) {
+        const int wd = wide4_wd(p);
+        return {FixedKernel::kWide4, wd, false, wide_threads(wd), 16, kDmaDynMinItemsPerWave, p.zmax};
+    }
+    if (!tiny && fixed_wide8(p)) {
+        const int wd = wide8_wd(p);
+        return {FixedKernel::kWide8, wd, false, wide_threads(wd), 8, kDmaDynMinItemsPerWave, p.zmax};
+    }
+    if (!tiny && fixed_wide(p)) {
+        const int wd = wide_wd(p);
+        return {FixedKernel::kWide16, wd, false, wide_threads(wd), 4, kDmaDynMinItemsPerWave, p.zmax};
+    }
+    if (fixed_segil(p)) return {FixedKernel::kSegment, 0, false, kSegilWgThreads, 4, kFixedDynMinUnitsPerWave, p.zmax};
+    if (!tiny && fixed_dma(p)) {   // the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
+        const uint32_t z = kDmaCover - p.flen > 4 ? kDmaCover - p.flen : 4;
+        return {FixedKernel::kDma, z <= 8 ? 2 : (int)(kSingleMaxLead / 4), false, kDmaWgThreads, 4, kDmaDynMinItemsPerWave, z};
+    }
+    if (tiny) return {FixedKernel::kTiny, fixed_single(p) ? 1 : 0, true, kWgThreads, 4, 0, p.zmax};   // wd: single
+    if (fixed_single(p)) return {FixedKernel::kSingle, 0, false, kFixedWgThreads, 4, 0, p.zmax};
+    return {FixedKernel::kGeneric, 0, false, p.fseg >= kWideSegs ? kFixedWgThreads : kWgThreads, 4,
+            kFixedDynMinUnitsPerWave, p.zmax};
 }
 
 hipError_t launch_fcs(bool var, bool windowed, const KParams &p, int grid, hipStream_t st);
+// Launches the kernel route_fixed(p, big) named as `r` (p.zmax = r.zmax) and records it for
+// last_fixed_launch.
+hipError_t launch_fixed_route(const FixedRoute &r, const KParams &p, int grid, hipStream_t st);
+// The kernel the last launch_fixed_route call launched (test introspection): its route with
+// threads/item fields as launched. Zero-initialised before any.
+FixedRoute last_fixed_launch();
 hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st);
 hipError_t launch_one(const OneArgs &a, hipStream_t st);
 hipError_t launch_tx_small(const TxSmallArgs &a, hipStream_t st);

@@ -5,7 +5,9 @@
 // frame + trailer). Two buffers alternate: while the GPU checks one batch, the next recvmmsg fills
 // the other. ether_receive never fails or drops frames for FCS reasons, so when the GPU check of a
 // batch fails (HIP error, timeout, no GPU) the library's host CRC checks it instead
-// (fcs_host_crc.cpp), counted per queue and in fcs_engine_host_batches.
+// (fcs_host_crc.cpp), counted per queue and in fcs_engine_host_batches: the
+// synchronous ether_fcs_verify_host answers a failed GPU step itself; a failed pipelined check
+// (mapped_submit / mapped_wait) or no usable GPU at all is answered here.
 #include <arpa/inet.h>
 #include <sys/socket.h>
 
@@ -14,6 +16,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
+#include <utility>
 #include <vector>
 
 #include "../../include/nstack_fcs.h"
@@ -28,7 +31,7 @@ constexpr uint32_t kMaxLen = 1514;      // ETHER_MAXLEN: ether_receive's buffer 
 constexpr uint32_t kSlot = 2048;        // receive slot: a longer frame shows up as truncated
 constexpr uint32_t kMaxBatch = 4096;
 constexpr uint32_t kResidue = 0x2144DF1Cu;   // CRC-32 of any frame followed by its own LE FCS
-constexpr size_t kMaxQuarantine = 64;   // ok arrays set aside after failed GPU checks (then host-only)
+constexpr size_t kMaxPinnedSpares = 64;   // pinned ok arrays taken to replace set-aside ones (then malloc'd)
 }  // namespace
 
 // One receive buffer: recvmmsg slots plus the frame list the verify kernel reads. With the
@@ -40,7 +43,7 @@ struct RxBuf {
     uint32_t *len = nullptr;
     uint8_t *ok = nullptr;
     bool pinned = false;                // all four from fcs_host_alloc
-    bool ok_pinned = false;             // ok from fcs_host_alloc (it may be replaced, see quarantine)
+    bool ok_pinned = false;             // ok from fcs_host_alloc (it may be replaced, see host_check)
     uint32_t n = 0, next = 0;           // frames in the buffer, next one to hand out
     uint64_t ticket = 0;
     enum State { kEmpty, kInFlight, kReady } state = kEmpty;
@@ -57,11 +60,14 @@ struct fcs_rxq {
     std::vector<iovec> iov;
     uint64_t n_frames = 0, n_bad = 0, n_echo = 0, n_drop = 0, n_batches = 0;
     uint64_t n_host_batches = 0, n_host_frames = 0;   // batches the host CRC checked
-    // ok arrays of batches whose GPU check failed after a launch: a late kernel may still write
-    // them, so they are never reused before fcs_rxq_destroy. After kMaxQuarantine such batches the
-    // queue stops using the GPU (host_only).
+    // ok arrays of pipelined batches whose check failed after its launch: the kernel may still write
+    // them, so they are never reused before fcs_rxq_destroy, whatever else fails (every one is set
+    // aside; their number is bounded because the engine stops launching after repeated failures).
     std::vector<std::pair<uint8_t *, bool>> quarantine;   // (array, from fcs_host_alloc)
-    bool host_only = false;
+    size_t pinned_spares = 0;
+    // One malloc'd ok array per buffer, taken when no fresh array can be allocated: a buffer that
+    // gets a non-pinned array is checked synchronously from then on, so it needs at most one.
+    uint8_t *spare[2] = {nullptr, nullptr};
     std::mutex mu;
 };
 
@@ -127,32 +133,36 @@ int recv_into(fcs_rxq *q, RxBuf &B, int flags) {
     return (int)n;
 }
 
-// The GPU check of B failed: check it with the host CRC instead (ether_receive
-// never drops a frame for FCS reasons). launched: a kernel of the failed step may still be in
-// flight and write B.ok, so that array is set aside and B gets a fresh one.
+void count_host(fcs_rxq *q, RxBuf &B) {
+    q->n_host_batches++;
+    q->n_host_frames += B.n;
+}
+
+// The GPU check of B failed or could not run: check it with the host CRC instead (SURVEY.md §8b;
+// ether_receive never drops a frame for FCS reasons). launched: a pipelined check of B was launched
+// and its wait failed, so that kernel may still write B.ok: the array is set aside in every case
+// and B gets a fresh one (pinned while spares last, so B stays pipelined; else malloc'd, and B's
+// later checks go through the synchronous ether_fcs_verify_host, which never lets a kernel write
+// into the caller's array).
 void host_check(fcs_rxq *q, RxBuf &B, bool launched) {
-    const char *why = q->host_only ? "queue in host-only mode after repeated GPU failures" : fcs_last_error();
-    if (launched && !q->host_only) {
-        uint8_t *fresh = B.pinned ? (uint8_t *)fcs_host_alloc(q->cap) : nullptr;
+    const char *why = fcs_last_error();
+    if (launched) {
+        uint8_t *fresh = nullptr;
+        if (B.ok_pinned && q->pinned_spares < kMaxPinnedSpares && (fresh = (uint8_t *)fcs_host_alloc(q->cap)))
+            q->pinned_spares++;
         const bool fresh_pinned = fresh != nullptr;
         if (!fresh) fresh = (uint8_t *)std::malloc(q->cap);
-        if (fresh && q->quarantine.size() < kMaxQuarantine) {
-            q->quarantine.emplace_back(B.ok, B.ok_pinned);
-            B.ok = fresh;
-            B.ok_pinned = fresh_pinned;
-            if (!fresh_pinned) q->host_only = true;   // mapped_submit needs an fcs_host_alloc array
-        } else {
-            if (fresh) fresh_pinned ? fcs_host_free(fresh) : std::free(fresh);
-            q->host_only = true;
-        }
+        q->quarantine.emplace_back(B.ok, B.ok_pinned);
+        if (!fresh) std::swap(fresh, q->spare[&B == &q->b[1]]);   // allocation failed: the buffer's spare
+        B.ok = fresh;
+        B.ok_pinned = fresh_pinned;
     }
     for (uint32_t i = 0; i < B.n; i++) {
         const uint32_t L = B.len[i];   // 0: runt or oversize, dropped anyway
         B.ok[i] = L >= kFcsLen && fcs::host_crc32(B.arena + B.off[i], L) == kResidue;
     }
     fcs::host_batch_answered("fcs_rxq_receive", why);
-    q->n_host_batches++;
-    q->n_host_frames += B.n;
+    count_host(q, B);
     B.state = RxBuf::kReady;
 }
 
@@ -163,7 +173,6 @@ void start_check(fcs_rxq *q, RxBuf &B) {
         B.state = RxBuf::kReady;
         return;
     }
-    if (q->host_only) return host_check(q, B, false);
     if (q->pipelined && B.ok_pinned) {
         if (fcs::mapped_submit(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n, &B.ticket))
             return host_check(q, B, false);   // nothing launched
@@ -171,7 +180,8 @@ void start_check(fcs_rxq *q, RxBuf &B) {
         return;
     }
     const int64_t bad = ether_fcs_verify_host(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n);
-    if (bad < 0) return host_check(q, B, true);
+    if (bad < 0) return host_check(q, B, false);   // no usable GPU: nothing ran
+    if (fcs::last_call_host_answered()) count_host(q, B);   // the engine answered a failed GPU step
     B.state = RxBuf::kReady;
 }
 
@@ -205,6 +215,11 @@ fcs_rxq_t *fcs_rxq_create(int fd, const uint8_t own_mac[6], uint32_t max_batch, 
         }
     }
     q->pipelined = pinned && (flags & FCS_RXQ_TRAILER);
+    for (uint8_t *&sp : q->spare)
+        if (!(sp = (uint8_t *)std::malloc(max_batch))) {
+            fcs_rxq_destroy(q);
+            return nullptr;
+        }
     q->msgs.resize(max_batch);
     q->iov.resize(max_batch);
     return q;
@@ -290,6 +305,7 @@ void fcs_rxq_destroy(fcs_rxq_t *q) {
         free_buf(B);
     }
     for (auto &x : q->quarantine) x.second ? fcs_host_free(x.first) : std::free(x.first);
+    for (uint8_t *sp : q->spare) std::free(sp);
     delete q;
 }
 

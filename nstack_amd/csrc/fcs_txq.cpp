@@ -2,10 +2,13 @@
 //
 // Mirrors ether_send (/root/reference/src/linux/ether.c:214-272) per call — frame layout
 // (:257-263), -EMSGSIZE rule (:222-224, :234-237), per-call return value (:265-269) — while the
-// FCS of every frame queued by any thread is computed in one GPU batch (ether_fcs_tx_host) and
-// the batch is handed to the sink at once (sendmmsg). ether_send never fails for FCS reasons, so
+// FCS of every frame queued by any thread is computed in one GPU batch (ether_fcs_tx_batch_host)
+// and the batch is handed to the sink at once (sendmmsg). ether_send never fails for FCS reasons, so
 // when the GPU step fails the batch's FCSs come from the library's host CRC (fcs_host_crc.cpp,
-// SURVEY.md §8b), counted per queue and in fcs_engine_host_batches; the frames still leave.
+// SURVEY.md §8b): ether_fcs_tx_batch_host answers a failed GPU step itself, and without any usable
+// GPU (-ENODEV) the queue does; either way counted per queue and in fcs_engine_host_batches, and the
+// frames still leave. The engine never leaves a kernel that can write into the arena after a failed
+// call (its results go through the library's own mapped memory), so arenas are always reused.
 //
 // Producers reserve slots with one atomic add on a reservation word, and the open batch is split
 // into up to 16 shards, each with its own word on its own cache line: a thread reserves in its
@@ -42,7 +45,6 @@ constexpr uint32_t kSlot = 1518;        // ETHER_MAXLEN + ETHER_FCS_LEN: largest
 constexpr uint32_t kStride = 1536;      // arena slot pitch: whole cache lines, so producers filling
                                         // neighbouring slots never share a line
 constexpr uint32_t kMaxBatch = 65536;
-constexpr size_t kMaxQuarantine = 16;   // arenas set aside after failed GPU steps (then host-only)
 
 using Clock = std::chrono::steady_clock;
 
@@ -124,11 +126,6 @@ struct fcs_txq {
     uint64_t flush_target = 0;            // flush() wants batches <= this closed now
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
     uint64_t n_host_batches = 0, n_host_frames = 0;   // batches whose FCSs the host CRC computed
-    // Pinned arenas of batches whose GPU step failed: a kernel of that step may still be in flight
-    // and write FCS words into them, so they are never reused before fcs_txq_destroy. After
-    // kMaxQuarantine such batches the queue stops using the GPU (host_only).
-    std::vector<uint8_t *> quarantine;
-    bool host_only = false;
     uint64_t ns_ready = 0, ns_gpu = 0, ns_sink = 0, ns_busy = 0;   // flusher time split
     uint64_t ns_pickup = 0;               // first frame of a batch queued -> batch closed
     std::string last_error;               // fcs_last_error() of the latest failed GPU step
@@ -260,20 +257,21 @@ void flusher(fcs_txq *q) {
         // FCS of every frame, written little-endian after its covered bytes (ether.c:262-263)
         // the span the frames occupy (not the whole arena): it decides the engine's in-place path
         const uint64_t span = n ? B->off[n - 1] + kStride : 0;
-        int rc = q->host_only ? -EIO : ether_fcs_tx_batch_host(B->arena, span, B->off.data(), B->covered.data(), n);
+        const int rc = ether_fcs_tx_batch_host(B->arena, span, B->off.data(), B->covered.data(), n);
+        const bool host = rc != 0 || fcs::last_call_host_answered();   // the engine answered a failed GPU step
         if (rc != 0) {
-            // the GPU step failed: ether_send cannot fail for FCS reasons (src/linux/ether.c:234-269),
+            // no usable GPU at all: ether_send cannot fail for FCS reasons (src/linux/ether.c:234-269),
             // so the host CRC computes this batch's FCSs, counted and reported
-            const std::string why = q->host_only ? std::string("queue in host-only mode after repeated GPU failures")
-                                                 : std::string(fcs_last_error() ? fcs_last_error() : "");
             for (uint32_t i = 0; i < n; i++) {
                 uint8_t *f = B->arena + B->off[i];
                 const uint32_t c = fcs::host_crc32(f, B->covered[i]);
                 std::memcpy(f + B->covered[i], &c, 4);   // little-endian, as ether.c:263
             }
-            fcs::host_batch_answered("fcs_txq flusher", why.c_str());
+            fcs::host_batch_answered("fcs_txq flusher", fcs_last_error());
+        }
+        if (host) {
             std::lock_guard<std::mutex> lk(q->mu);
-            q->last_error = why;
+            q->last_error = fcs_last_error() ? fcs_last_error() : "";
             q->n_host_batches++;
             q->n_host_frames += n;
         }
@@ -284,18 +282,6 @@ void flusher(fcs_txq *q) {
             B->res[i] = -EIO;   // a sink that forgets a frame reports it as failed
         }
         q->sink(q->ctx, B->frames.data(), B->sizes.data(), B->res.data(), n);
-        if (rc != 0 && B->pinned && !q->host_only) {
-            // a kernel of the failed step may still write into this arena: set it aside (the
-            // FCSs it would write are the ones just sent) and give the batch a fresh one
-            uint8_t *fresh = (uint8_t *)fcs_host_alloc((uint64_t)q->cap * kStride);
-            if (fresh && q->quarantine.size() < kMaxQuarantine) {
-                q->quarantine.push_back(B->arena);
-                B->arena = fresh;
-            } else {
-                if (fresh) fcs_host_free(fresh);
-                q->host_only = true;   // no fresh arena to move to: stop trusting the GPU step
-            }
-        }
         const auto t3 = Clock::now();
 
         std::lock_guard<std::mutex> lk(q->mu);
@@ -496,7 +482,6 @@ void fcs_txq_destroy(fcs_txq_t *q) {
             else std::free(B.arena);
         }
     }
-    for (uint8_t *a : q->quarantine) fcs_host_free(a);
     delete q;
 }
 

@@ -79,10 +79,16 @@ uint32_t oracle_ether_fcs(const void *data, size_t bsize)
 }
 
 /* Same function, slice-by-8 over the standard (non-folded) register: ~r in, ~r out. */
+uint32_t oracle_crc32_fast_from(uint32_t r, const void *data, size_t n);
 uint32_t oracle_crc32_fast(const void *data, size_t n)
 {
+    return oracle_crc32_fast_from(0xFFFFFFFFu, data, n);
+}
+
+/* The slice-by-8 register walk from register r (the standard, non-complemented register). */
+uint32_t oracle_crc32_fast_from(uint32_t r, const void *data, size_t n)
+{
     const uint8_t *p = (const uint8_t *) data;
-    uint32_t r = 0xFFFFFFFFu;
     if (!tables_ready)
         build_tables();
     while (n && ((uintptr_t) p & 7)) {
@@ -210,6 +216,93 @@ void oracle_splitmix_fill(uint8_t *buf, size_t n, uint64_t seed, uint64_t byte_o
         uint64_t w = splitmix64(seed + (pos >> 3));
         buf[i] = (uint8_t)(w >> (8 * (pos & 7)));
     }
+}
+
+/* Bytes [byte_offset, byte_offset + n) of the same stream, one splitmix64 per 8-byte word. */
+static void splitmix_fill_words(uint8_t *buf, size_t n, uint64_t seed, uint64_t byte_offset)
+{
+    size_t i = 0;
+    while (i < n && ((byte_offset + i) & 7)) {
+        uint64_t pos = byte_offset + i;
+        buf[i++] = (uint8_t)(splitmix64(seed + (pos >> 3)) >> (8 * (pos & 7)));
+    }
+    for (; i + 8 <= n; i += 8) {
+        uint64_t w = splitmix64(seed + ((byte_offset + i) >> 3));
+        memcpy(buf + i, &w, 8);   /* little-endian host: byte k of the word is bits 8k..8k+7 */
+    }
+    for (; i < n; i++) {
+        uint64_t pos = byte_offset + i;
+        buf[i] = (uint8_t)(splitmix64(seed + (pos >> 3)) >> (8 * (pos & 7)));
+    }
+}
+
+/* Digest of a whole splitmix batch without materialising it: frame i is the stream's bytes
+ * [off_i, off_i + len_i) (off == NULL: i * stride, len == NULL: flen); the XOR and the 64-bit sum of
+ * every frame's CRC (slice-by-8), over nthreads host threads. For checking full BASELINE-size GPU
+ * launches (tests/test_gpu_parity.py): 64 M x 1518 B, 128 M IMIX frames, 16 M x 9000 B. */
+struct digest_job {
+    uint64_t seed, stride, i0, i1;
+    const uint64_t *off;
+    const uint32_t *len;
+    uint32_t flen;
+    uint32_t x;
+    uint64_t sum;
+};
+
+static void *digest_worker(void *arg)
+{
+    struct digest_job *j = (struct digest_job *) arg;
+    uint8_t buf[65536 + 16];
+    uint32_t x = 0;
+    uint64_t sum = 0;
+    for (uint64_t i = j->i0; i < j->i1; i++) {
+        const uint64_t o = j->off ? j->off[i] : i * j->stride;
+        const uint32_t L = j->len ? j->len[i] : j->flen;
+        uint32_t c;
+        if (L <= 65536) {
+            splitmix_fill_words(buf, L, j->seed, o);
+            c = oracle_crc32_fast(buf, L);
+        } else {   /* longer frames: in pieces, the register carried (~c in, ~c out) */
+            c = 0;   /* the CRC so far; its register is ~c */
+            for (uint64_t k = 0; k < L; k += 65536) {
+                size_t m = L - k < 65536 ? (size_t)(L - k) : 65536;
+                splitmix_fill_words(buf, m, j->seed, o + k);
+                c = oracle_crc32_fast_from(~c, buf, m);
+            }
+        }
+        x ^= c;
+        sum += c;
+    }
+    j->x = x;
+    j->sum = sum;
+    return NULL;
+}
+
+void oracle_splitmix_digest(uint64_t seed, const uint64_t *off, const uint32_t *len, uint64_t stride,
+                            uint32_t flen, uint64_t n, int nthreads, uint32_t *xor_out, uint64_t *sum_out)
+{
+    if (!tables_ready)
+        build_tables();
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    struct digest_job jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (struct digest_job){seed, stride, n * (uint64_t) t / (uint64_t) nthreads,
+                                      n * (uint64_t)(t + 1) / (uint64_t) nthreads, off, len, flen, 0, 0};
+        pthread_create(&th[t], NULL, digest_worker, &jobs[t]);
+    }
+    uint32_t x = 0;
+    uint64_t sum = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        x ^= jobs[t].x;
+        sum += jobs[t].sum;
+    }
+    *xor_out = x;
+    *sum_out = sum;
 }
 
 /* 0 on success; checks the derived tables against SURVEY §8c known answers. */

@@ -36,6 +36,7 @@ def oracle():
     L.oracle_time_fixed.argtypes = [vp, ctypes.c_size_t, u32, ctypes.c_size_t, vp, i32, i32]
     L.oracle_xorshift64_fill.argtypes = [vp, ctypes.c_size_t, ctypes.POINTER(u64)]
     L.oracle_splitmix_fill.argtypes = [vp, ctypes.c_size_t, u64, u64]
+    L.oracle_splitmix_digest.argtypes = [u64, vp, vp, u64, u32, u64, i32, ctypes.POINTER(u32), ctypes.POINTER(u64)]
     L.oracle_selfcheck.restype = i32
     return L
 
@@ -49,6 +50,17 @@ def golden():
     with open(os.path.join(GOLDEN, "kat.json")) as f:
         kat = json.load(f)
     return {"vectors": vec, "arena": arena, "kat": kat}
+
+
+def splitmix_digest(oracle, seed, n, stride=0, flen=0, off=None, lengths=None, threads=16):
+    """(XOR, 64-bit sum) of the CRCs of a whole splitmix batch, computed by the oracle over `threads`
+    host threads without materialising the frames (frame i = stream bytes [off_i, +len_i), or
+    [i * stride, +flen)). 16 threads: one GPU box's CPU share."""
+    x, s = ctypes.c_uint32(0), ctypes.c_uint64(0)
+    oracle.oracle_splitmix_digest(seed, None if off is None else off.ctypes.data,
+                                  None if lengths is None else lengths.ctypes.data, stride, flen, n, threads,
+                                  ctypes.byref(x), ctypes.byref(s))
+    return x.value, s.value
 
 
 @pytest.fixture(params=["quarter", "windowed"])

@@ -16,6 +16,7 @@ import numpy as np
 import pytest
 
 import nstack_amd as na
+from conftest import splitmix_digest
 
 pytestmark = pytest.mark.gpu
 
@@ -227,9 +228,15 @@ def test_device_generator_matches_oracle(dev, oracle):
 
 
 # ---------------------------------------------------------------- BASELINE size (properties)
+def _digest(a):
+    return int(np.bitwise_xor.reduce(a)), int(a.astype(np.uint64).sum()) & ((1 << 64) - 1)
+
+
 def test_baseline_size_properties(dev, oracle):
-    """64 M x 1518 B (94.9 GiB) in one launch: sampled frames == oracle, two half launches ==
-    one launch (shard consistency), and a second launch is bit-identical (determinism)."""
+    """64 M x 1518 B (94.9 GiB) in one launch: every frame covered by the XOR and the 64-bit sum of
+    all CRCs against the oracle's digest of the same splitmix stream, sampled frames == oracle, two
+    half launches == one launch (shard consistency), and a second launch is bit-identical
+    (determinism)."""
     free, _ = torch.cuda.mem_get_info()
     n, L = 64 << 20, 1518
     if free < n * L + (4 << 30):
@@ -237,6 +244,7 @@ def test_baseline_size_properties(dev, oracle):
     arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
     na.fill_splitmix_dev(arena, n * L, 2026, 0)
     a = run_fixed(dev, arena, L, L, n)
+    assert _digest(a) == splitmix_digest(oracle, 2026, n, stride=L, flen=L)
     h = n // 2
     b0 = run_fixed(dev, arena, L, L, h)
     b1 = run_fixed(dev, arena.data_ptr() + h * L, L, L, n - h)
@@ -254,8 +262,9 @@ def test_baseline_size_properties(dev, oracle):
 
 def test_baseline_imix_size_properties(dev, oracle):
     """BASELINE configs[2]: 128 M IMIX frames (7:4:1 of 64/576/1518, shuffled, packed; 47.8 GB) in
-    one launch of the windowed kernel: sampled frames == oracle, the two halves of the frame list
-    launched separately == one launch, and a second launch is bit-identical."""
+    one launch of the windowed kernel: every frame covered by the XOR / sum64 digest of all CRCs
+    against the oracle's, sampled frames == oracle, the two halves of the frame list launched
+    separately == one launch, and a second launch is bit-identical."""
     n = 128 << 20
     rng = np.random.default_rng(2027)
     ln = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), [n * 7 // 12, n * 4 // 12, n - n * 7 // 12 - n * 4 // 12])
@@ -278,6 +287,7 @@ def test_baseline_imix_size_properties(dev, oracle):
         return out.cpu().numpy().view(np.uint32)
 
     a = launch(0, n)
+    assert _digest(a) == splitmix_digest(oracle, 2027, n, off=off, lengths=ln)
     h = n // 2
     assert np.array_equal(a, np.concatenate([launch(0, h), launch(h, n)]))
     assert np.array_equal(a, launch(0, n))
@@ -333,7 +343,8 @@ def test_more_than_2_32_frames(dev, oracle):
 
 def test_baseline_jumbo_size_properties(dev, oracle):
     """BASELINE configs[3]: 16 M x 9000-B frames (151 GB) in one launch of the interleaved segment
-    kernel: sampled frames == oracle, two half launches == one launch, determinism."""
+    kernel: every frame covered by the XOR / sum64 digest against the oracle's, sampled frames ==
+    oracle, two half launches == one launch, determinism."""
     n, L = 16 << 20, 9000
     free, _ = torch.cuda.mem_get_info()
     if free < n * L + (4 << 30):
@@ -341,6 +352,7 @@ def test_baseline_jumbo_size_properties(dev, oracle):
     arena = torch.empty(n * L, dtype=torch.uint8, device=dev)
     na.fill_splitmix_dev(arena, n * L, 2028, 0)
     a = run_fixed(dev, arena, L, L, n)
+    assert _digest(a) == splitmix_digest(oracle, 2028, n, stride=L, flen=L)
     h = n // 2 + 1   # an odd split: the second half starts inside a 4-frame unit of the first launch
     b0 = run_fixed(dev, arena, L, L, h)
     b1 = run_fixed(dev, arena.data_ptr() + h * L, L, L, n - h)

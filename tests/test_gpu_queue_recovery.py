@@ -11,7 +11,9 @@ Runs against nstack_amd/libnstack_fcs_faults.so, the test-only -DFCS_FAULT_HOOK 
 fcs_debug_fail_batches(skip, calls) lets the next `skip` queue batch calls (ether_fcs_tx_batch_host,
 ether_fcs_verify_host, the mapped-list submit and wait) run and fails the `calls` after them; a
 failed wait gives up with its kernel still in flight (the queue then sets the batch's ok array
-aside). Expected frames come from ether_send's layout with the oracle's FCS (TX) and from zlib
+aside). fcs_debug_late_batches(skip, calls) makes the host batch calls give up after their launch,
+with the kernel in flight (the TX queue's arena is reused at once: the engine's kernels never write
+into it). Expected frames come from ether_send's layout with the oracle's FCS (TX) and from zlib
 (RX); every check is exact."""
 import random
 import socket
@@ -39,6 +41,15 @@ def flib():
     L = na.load_faults()
     yield L
     L.fcs_debug_fail_batches(0, 0)
+    L.fcs_debug_late_batches(0, 0)
+
+
+@pytest.fixture(autouse=True)
+def fresh_engine(flib):
+    """Each test starts on a fresh engine: failed waits retire resources, and 16 retirements would
+    put the host batch forms into host-only mode for the tests after it."""
+    flib.fcs_engine_fini()
+    yield
 
 
 def ether_send_frame(oracle, dst, proto, payload, src=MAC):
@@ -111,15 +122,18 @@ def test_tx_failure_after_healthy_batches(flib, oracle):
     assert batches > 6 and hb == 1 and 1 <= hf <= 16
 
 
-def test_tx_host_only_after_repeated_failures(flib, oracle):
-    """After 16 set-aside arenas the queue stops calling the GPU: the 17th failure switches it to
-    the host CRC for good; frames stay exact and every later batch is counted."""
-    flib.fcs_debug_fail_batches(0, 17)
-    ok_res, same, (frames, batches, errors), (hb, hf), why = run_tx(flib, oracle, 1, 0, 1, 40, 11)
-    assert ok_res and same and errors == 0 and frames == 40
-    assert flib.fcs_debug_batch_faults_left() == 0     # the host-only batches made no GPU call
-    assert batches == 40 and hb == 40 and hf == 40
-    assert "host-only" in why
+@pytest.mark.parametrize("max_batch,producers", [(64, 8), (1024, 8), (4, 1)])
+def test_tx_late_failures_with_kernel_in_flight(flib, oracle, max_batch, producers):
+    """The GPU step gives up after its launch, the kernel still in flight (a timeout), on the
+    first three batches: the engine answers them from the host CRC and retires the stream its
+    kernel writes, the queue reuses the arena at once, and every frame that leaves is exact."""
+    h0 = flib.fcs_engine_host_batches()
+    flib.fcs_debug_late_batches(0, 3)
+    ok_res, same, (frames, batches, errors), (hb, hf), why = run_tx(flib, oracle, max_batch, 0, producers, 150, 3)
+    assert flib.fcs_debug_batch_faults_left() == 0
+    assert ok_res and same and errors == 0 and frames == producers * 150
+    assert hb == 3 and flib.fcs_engine_host_batches() - h0 == 3
+    assert "injected late fault" in why
 
 
 def rx_frame(payload, proto=0x0800):

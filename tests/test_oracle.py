@@ -114,3 +114,36 @@ def test_bench_host_generator_matches_device_generator_restatement(oracle):
         buf = np.empty(n, dtype=np.uint8)
         oracle.oracle_splitmix_fill(buf.ctypes.data, n, seed, off)
         assert np.array_equal(bench.splitmix_bytes(seed, off, n), buf)
+
+
+@pytest.mark.parametrize("fixed", [(1518, 1518, 3000), (9000, 9001, 200), (70000, 70000, 5), (64, 100, 4000)])
+def test_splitmix_digest_fixed_matches_zlib(oracle, fixed):
+    """The whole-batch digest the BASELINE-size GPU tests compare against (XOR and 64-bit sum of every
+    frame's CRC, frames regenerated from the splitmix stream on the fly) equals zlib's over the same
+    bytes; frames over 64 KiB take the piecewise path."""
+    from conftest import splitmix_digest
+    L, stride, n = fixed
+    buf = np.empty(L, dtype=np.uint8)
+    x, s = 0, 0
+    for i in range(n):
+        oracle.oracle_splitmix_fill(buf.ctypes.data, L, 31, i * stride)
+        c = zlib.crc32(buf.tobytes())
+        x ^= c
+        s += c
+    assert splitmix_digest(oracle, 31, n, stride=stride, flen=L, threads=3) == (x, s & ((1 << 64) - 1))
+
+
+def test_splitmix_digest_var_matches_zlib(oracle):
+    from conftest import splitmix_digest
+    rng = np.random.default_rng(12)
+    ln = rng.choice(np.array([0, 1, 64, 576, 1518, 9000], dtype=np.uint32), 3000)
+    off = np.zeros(len(ln), dtype=np.uint64)
+    off[1:] = np.cumsum(ln[:-1].astype(np.uint64) + 5)
+    x, s = 0, 0
+    for o, L in zip(off, ln):
+        buf = np.empty(int(L), dtype=np.uint8)
+        oracle.oracle_splitmix_fill(buf.ctypes.data, int(L), 8, int(o))
+        c = zlib.crc32(buf.tobytes())
+        x ^= c
+        s += c
+    assert splitmix_digest(oracle, 8, len(ln), off=off, lengths=ln, threads=5) == (x, s & ((1 << 64) - 1))

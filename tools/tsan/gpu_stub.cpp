@@ -43,6 +43,8 @@ int mapped_submit(uint8_t *arena, uint64_t, const uint64_t *off, const uint32_t 
     g_due.emplace_back(*ticket, std::chrono::steady_clock::now() + std::chrono::microseconds(20));
     return 0;
 }
+void host_batch_answered(const char *, const char *) {}
+bool last_call_host_answered() { return false; }
 int mapped_wait(uint64_t ticket) {
     for (;;) {
         std::chrono::steady_clock::time_point t;
