@@ -3,11 +3,12 @@
 // Replaces ether_fcs() (/root/reference/src/ether_fcs.c:4-19, prototype src/nstack_ether.h:80)
 // and provides the batched forms its TX call site (src/linux/ether.c:262-263) needs.
 // Per-device state (constant tables in HBM, staging buffers, streams) is created lazily and is
-// safe to use from many threads. Every batch and device entry point computes on the GPU only: a
-// missing GPU or code object is reported as -errno. The one exception is the error-less drop-in
-// ether_fcs, whose reference cannot fail: after the GPU attempt and its retry on a
-// fresh lane have both failed, it returns the host CRC of fcs_host_crc.cpp (counted, announced on
-// stderr) instead of aborting.
+// safe to use from many threads. Every entry point computes on the GPU; a missing GPU or code object
+// is reported as -ENODEV and bad arguments as -EINVAL. SURVEY.md §8b ("on any HIP error, fall back
+// to the CPU path so results never differ"): the host batch forms answer any other failure of their
+// GPU step from the host CRC of fcs_host_crc.cpp (with_host_answer; counted, announced on stderr),
+// and the error-less drop-in ether_fcs does so after its GPU attempt and the retry on a fresh lane
+// have both failed. The device forms return the HIP error (their frames are in device memory).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -515,12 +516,12 @@ int launch_var(DevState *ds, const void *arena, uint64_t arena_bytes, const uint
         p.ulist = scr + 1;
         HIPTRY(hipMemsetAsync(p.ucount, 0, 4, st), "zeroing the unit list");
         HIPTRY(fcs::launch_stream(p, (int)std::min<uint64_t>((uint64_t)ds->cus, units), st), "launching fcs_stream_kernel");
-        // the unit-list length, copied out of the slot scratch for fcs_debug_stream_listed (the
-        // scratch is reused and may be regrown once the lease is released)
-        HIPTRY(hipMemcpyAsync(ds->d_last_listed, p.ucount, 4, hipMemcpyDeviceToDevice, st), "recording the unit list length");
+        // the flat kernel stores the unit-list length for fcs_debug_stream_listed (the slot scratch
+        // is reused and may be regrown once the lease is released)
         g_last_stream_dev.store(ds, std::memory_order_relaxed);
         fcs::KParams q = p;
         q.ctr = p.ctr + 1;
+        q.listed_out = ds->d_last_listed;
         HIPTRY(fcs::launch_fcs(true, true, q, grid, st), "launching fcs_flat_kernel<listed units>");
         return 0;
     }
@@ -1063,9 +1064,13 @@ int run_one(DevState *ds, const void *data, size_t bsize, uint32_t *crc, uint32_
             return 0;
         }
         // FCS_FAULT_HOOK builds only: give up with the kernel in flight (drop-in, or a one-frame host batch)
-        if (i == 1 && (injected_timeout() || (batch && injected_late_fault()))) {
-            reset_lane(ds, L);
-            return fail(ETIMEDOUT, "single-frame kernel: injected timeout (FCS_FAULT_HOOK build)");
+        if (i == 1) {
+            const bool late = batch && injected_late_fault();
+            if (late || injected_timeout()) {
+                reset_lane(ds, L);
+                return fail(ETIMEDOUT, "single-frame kernel: injected %s (FCS_FAULT_HOOK build)",
+                            late ? "late fault" : "timeout");
+            }
         }
         __builtin_ia32_pause();
         if ((i & 4095) == 0) {

@@ -2,13 +2,13 @@
 //
 // the reference ether_fcs (src/ether_fcs.c:4-19) cannot fail and has no
 // error channel, and ether_send / ether_receive (src/linux/ether.c:180-272) never fail for FCS
-// reasons. So when the GPU path has failed twice (first attempt and the retry on a fresh lane), or
-// the buffer is too large for the kernels' 32-bit frame lengths (>= 4 GiB), the drop-in returns
-// this instead of aborting; and when the GPU step of a TX or RX queue batch fails, the queue
-// computes or checks that batch's FCSs with it instead of failing or dropping the frames. The
-// batch and device entry points stay GPU-only and fail with -errno. Each use is counted
-// (fcs_engine_host_fallbacks, fcs_engine_host_batches) and announced once on stderr, and the GPU
-// test suite asserts both counts stay 0 (tests/test_gpu_zz_no_host_fallback.py).
+// reasons. So the drop-in returns this when the GPU path has failed twice (first attempt and the
+// retry on a fresh lane) or the buffer is too large for the kernels' 32-bit frame lengths (>= 4 GiB);
+// the host batch forms (ether_fcs_*_host) compute or check a batch with it when their GPU step fails
+// with a runtime error; and the TX/RX queues use it when no GPU is usable at all. The device forms
+// stay GPU-only and fail with -errno. Each use is counted (fcs_engine_host_fallbacks,
+// fcs_engine_host_batches) and announced once on stderr, and the GPU test suite asserts both counts
+// stay 0 (tests/test_gpu_zz_no_host_fallback.py). It is the product's own code, not the test oracle.
 #pragma once
 #include <cstddef>
 #include <cstdint>

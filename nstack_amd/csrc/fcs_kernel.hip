@@ -1440,6 +1440,13 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
                              ? lds_rd(lds, dma_hole(kDmaInvHole + (uint32_t)zr / 32u) + (uint32_t)(zr % 32) * 4u)
                              : 0u;
     const int zb = fdead ? 0 : zf;   // the wave masks word groups up to its largest live claim
+    // front word groups any live lane needs masked: one scalar (as six hoisted lane masks they took
+    // SGPRs the kernel then spilled)
+    uint32_t gmask = 0;
+#pragma unroll
+    for (int g = 0; g < kChunkWords / 4; g++)
+        if (__any(zb > 16 * g)) gmask = (uint32_t)g + 1u;
+    gmask = (uint32_t)__builtin_amdgcn_readfirstlane((int)gmask);
 
     const uint64_t n = p.n, units = (n + 3) >> 2;
     // chunks of about 64 items, and at least 16 units so that result runs fill 256-B groups; jumbo
@@ -1464,7 +1471,11 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     };
     auto issue = [&](uint64_t u, uint32_t r) {   // the item's four runs (wave-uniform control)
         const uint32_t len = r ? kDmaCover : Lf;
+#ifdef FCS_SEGIL_ISSUE_LOOP   // measurement-only: the four runs issued by a scalar loop
+#pragma unroll 1
+#else
 #pragma unroll
+#endif
         for (uint32_t qq = 0; qq < 4; qq++) {
             const uint64_t f = 4 * u + qq;
             if (f < n) {
@@ -1534,9 +1545,13 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
         uint32_t x0;
         if (r == 0) {
             const int zf8 = 8 * zf;
+            // an opaque copy: hoisted out of the item loop, the six group tests would each take an
+            // SGPR pair (twelve SGPRs, which the kernel then spilled to VGPR lanes)
+            uint32_t gm = gmask;
+            asm volatile("" : "+s"(gm));
 #pragma unroll
             for (int g = 0; g < kChunkWords / 4; g++) {
-                if (!__any(zb > 16 * g)) break;
+                if ((uint32_t)g >= gm) break;
 #pragma unroll
                 for (int i = 4 * g; i < 4 * g + 4; i++) {
                     // zf is a loop invariant: the compiler hoists this clamp (no v_med3 asm here)
@@ -1727,7 +1742,9 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_flat_kernel(KParams p) {
     // After fcs_stream_kernel (p.ulist set): only the units it listed, 8 windows each; none -> done.
     uint64_t nwin = (p.n + 63) >> 6;
     if (p.ulist != nullptr) {
-        nwin = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)*p.ucount) * (kStUnitFrames / 64);
+        const uint32_t listed = (uint32_t)__builtin_amdgcn_readfirstlane((int)*p.ucount);
+        if (blockIdx.x == 0 && threadIdx.x == 0 && p.listed_out) *p.listed_out = listed;   // fcs_debug_stream_listed
+        nwin = (uint64_t)listed * (kStUnitFrames / 64);
         if (nwin == 0) return;
     }
     stage_tables_flat(p, lds);
@@ -2020,9 +2037,10 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_short_kernel(KParams p) {
 // The dispenser hands out units of kStUnitFrames frames. A unit whose frames are packed
 // (off[i + 1] == off[i] + len[i]) and 64..1536 B long is taken here; any other unit is listed
 // in p.ulist for fcs_flat_kernel, launched right after on the same stream.
-// A unit's bytes are walked in 4 KiB items at fixed arena positions (the first item at the 16-B
-// boundary below the unit's first frame): one coalesced LDS-DMA per item (four 1 KiB rows from one
-// address register), issued while the previous item is computed, no dealing. Lane l's chunk is the
+// A unit's bytes are walked in 4 KiB items at fixed arena positions (the first item at the 128-B
+// line below the unit's first frame, so items share no line and every row is non-temporal): one
+// coalesced LDS-DMA per item (four 1 KiB rows from one address register), issued while the previous
+// item is computed, no dealing. Lane l's chunk is the
 // item's bytes [64 l, 64 l + 64); its 16-B pieces sit in LDS swizzled (piece m of chunk l at
 // 64 l + 16 ((m + l / 4) mod 4)), so the four ds_read_b128 of a chunk are conflict-free without
 // padding. Its chain L runs over all 16 words from register 0.
@@ -2061,10 +2079,10 @@ constexpr uint32_t kStRings = kStSlots + 16 * kStSlotBytes;           // per wav
 constexpr uint32_t kStLdsBytes = kStRings + 16 * 1024;
 static_assert(kStLdsBytes <= 163840, "LDS per CU");
 constexpr uint32_t kMarkStart = 1u << 31, kMarkEnd = 1u << 30;
-// A frame's end (relative to the unit's first item) and length in one word: end << 11 | len
-// (ends < 2^20: 512 frames of at most 1536 B; lengths < 2^11).
+// A frame's end (relative to the unit's first item, which starts at most 127 B before the unit)
+// and length in one word: end << 11 | len (ends < 2^20: 512 frames of at most 1536 B; lengths < 2^11).
 constexpr uint32_t kStLenBits = 11;
-static_assert(kStUnitFrames * kStMaxLen + 16 < (1u << (32 - kStLenBits)) && kStMaxLen < (1u << kStLenBits), "packing");
+static_assert(kStUnitFrames * kStMaxLen + 128 < (1u << (32 - kStLenBits)) && kStMaxLen < (1u << kStLenBits), "packing");
 // FCS_STAMPS (measurement-only): per-wave s_memtime sums of the item's phases (tools/stamps_stream.py)
 #ifdef FCS_STAMPS
 #define ST_T(v)                              \
@@ -2080,12 +2098,17 @@ static_assert(kStUnitFrames * kStMaxLen + 16 < (1u << (32 - kStLenBits)) && kStM
 #ifndef FCS_ST_AUX   // cache policy of the item DMA's middle rows (measurement-only override)
 #define FCS_ST_AUX 2
 #endif
-// Items at 128-B line boundaries (measurement-only FCS_ST_ALIGN128): a unit's first item starts at
-// the line below its first frame (not past the arena's first 16-B piece), so consecutive items share
-// no line and the first and last rows can be non-temporal too (FCS_ST_EDGE_AUX, default: the
-// default policy, which keeps a line the neighbouring item shares in L2).
+// Items at 128-B line boundaries: a unit's first item starts at the line below its first frame (not
+// before the arena's first 16-B piece), so consecutive items share no line and every row is
+// non-temporal (round 5, tools/ab.py --imix, one process, two boxes: +0.95 % and +1.0 % against
+// 16-B-aligned items whose first and last rows took the default policy to keep the line they shared
+// in L2). Measurement-only: FCS_ST_ALIGN16 restores the 16-B items, FCS_ST_EDGE_AUX their policy.
 #ifndef FCS_ST_EDGE_AUX
+#ifdef FCS_ST_ALIGN16
 #define FCS_ST_EDGE_AUX 0
+#else
+#define FCS_ST_EDGE_AUX FCS_ST_AUX
+#endif
 #endif
 
 // A_n(s) ^ extra from the nibble table at holes h .. h + 3 (h = 4 q for table q; h may differ per
@@ -2255,11 +2278,11 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
         // ---- geometry, relative to X0 (the first item's start) ----
         const uint64_t s0 = p.base + (((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(S[0] >> 32)) << 32) |
                                       (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)S[0]));
-#ifdef FCS_ST_ALIGN128
+#ifdef FCS_ST_ALIGN16
+        const uint64_t X0 = s0 & ~15ull;
+#else
         const uint64_t lo16 = p.lo4 & ~15ull;
         const uint64_t X0 = (s0 & ~127ull) > lo16 ? (s0 & ~127ull) : lo16;
-#else
-        const uint64_t X0 = s0 & ~15ull;
 #endif
         dma_item(X0);
         const uint64_t o0 = X0 - p.base;   // arena offset of X0
@@ -2397,6 +2420,22 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             }
             const uint32_t c0 = x;
             x = hole_shift(lds, c0, kStHoleWord + 4u * 8u, y);
+#elif defined(FCS_ST_TREE)
+            // measurement-only: all 16 chain states kept, the state before word k picked by a tree of
+            // selects on the bits of k (15 selects and 4 bit tests instead of 16 compares and selects)
+            uint32_t xs16[16];
+#pragma unroll
+            for (int i = 0; i < 16; i++) {
+                xs16[i] = x;
+                x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
+            }
+#pragma unroll
+            for (int b = 0; b < 4; b++) {
+                const bool hi = (k >> b) & 1u;
+#pragma unroll
+                for (int i = 0; i < (8 >> b); i++) xs16[i] = hi ? xs16[2 * i + 1] : xs16[2 * i];
+            }
+            xk = xs16[0];
 #elif defined(FCS_ST_SMASK)
             // measurement-only: the state before word k picked by lane masks built with scalar ops from
             // the four bit planes of k (a v_cndmask on an SGPR mask per word, no per-word v_cmp)

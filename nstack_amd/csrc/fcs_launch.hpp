@@ -29,6 +29,7 @@ struct KParams {
     // those units (and returns at once when there are none).
     uint32_t *ulist;
     uint32_t *ucount;
+    uint32_t *listed_out;   // fcs_flat_kernel<listed units>: stores *ucount here (test introspection)
 };
 // Arena-stream kernel geometry: units of frames handed out by the dispenser; 64-B lane chunks at
 // fixed arena positions, 64 per 4 KiB item; frames of 64..1536 B, packed within a unit.

@@ -104,7 +104,7 @@ def model_stream(arena: bytes, offs, lens, unit_frames=None, counts: Counts = No
     """FCS of packed frames (offs[i+1] == offs[i] + lens[i], 64 <= len <= 1536) by the arena-stream
     decomposition. `unit_frames`: split the batch into ranges of this many frames processed
     independently (a wave's dispenser chunks: each range starts its own item sequence at the
-    16-B boundary below its first frame, so the items at range edges are loaded twice)."""
+    128-B line below its first frame, so the lines at range edges are loaded twice)."""
     n = len(offs)
     out = [None] * n
     ranges = [(0, n)] if not unit_frames else [(i, min(n, i + unit_frames)) for i in range(0, n, unit_frames)]
@@ -116,7 +116,7 @@ def model_stream(arena: bytes, offs, lens, unit_frames=None, counts: Counts = No
 def _model_range(arena, offs, lens, f0, f1, out, counts):
     s0 = offs[f0]
     e_last = offs[f1 - 1] + lens[f1 - 1]
-    X0 = s0 & ~15                       # the range's first item starts at the 16-B boundary below
+    X0 = s0 & ~127                      # the range's first item starts at the 128-B line below
     starts = {offs[i]: i for i in range(f0, f1)}          # boundary position -> frame starting there
     end_of = {offs[i] + lens[i]: i for i in range(f0, f1)}  # boundary position -> frame ending there
     acc = {i: 0 for i in range(f0, f1)}
@@ -197,7 +197,7 @@ def imix_structure(lens, unit_frames, base=0):
     items = 0
     for f0 in range(0, len(lens), unit_frames):
         f1 = min(len(lens), f0 + unit_frames)
-        X0 = int(offs[f0]) & ~15
+        X0 = max(int(offs[f0]) & ~127, base & ~15)
         e = int(offs[f1 - 1] + lens[f1 - 1])
         items += (e - X0 + ITEM - 1) // ITEM
     # flat kernel: ceil(len / 96) chunks per frame, dealt 64 at a time per 64-frame window

@@ -35,6 +35,7 @@ def _kernels(lib_path):
                 field = lambda k: re.search(rf"\.{k}:\s+(\S+)", block).group(1)
                 out.append({"name": field("name"), "vgpr": int(field("vgpr_count")),
                             "vgpr_spill": int(field("vgpr_spill_count")),
+                            "sgpr_spill": int(field("sgpr_spill_count")),
                             "scratch": int(field("private_segment_fixed_size")),
                             "wg": int(field("max_flat_workgroup_size"))})
         return out
@@ -54,3 +55,15 @@ def test_no_spills_no_scratch_and_registers_fit_the_workgroup():
     # one workgroup per CU (the LDS tables): wg / 256 waves per SIMD, 512 VGPRs per SIMD lane
     tight = [k for k in ks if k["wg"] > 256 and k["vgpr"] > 512 // (k["wg"] // 256)]
     assert not tight, tight
+
+
+@pytest.mark.skipif(not os.path.exists(f"{LLVM}/llvm-readelf"), reason="ROCm LLVM tools not installed")
+def test_baseline_kernels_spill_no_sgprs():
+    """The kernels of the BASELINE configs (the LDS-DMA kernel: 1518 B; the arena stream: IMIX; the
+    interleaved segments: jumbo) and the wide windows keep every scalar in SGPRs: a spilled SGPR costs
+    a v_writelane / v_readlane pair per use (the segment kernel had 10)."""
+    hot = ("fcs_dma_kernel", "fcs_segil_kernel", "fcs_stream_kernel", "fcs_wide_kernel")
+    ks = [k for k in _kernels(na.LIB_PATH) if any(h in k["name"] for h in hot)]
+    assert len(ks) >= 40
+    bad = [(k["name"], k["sgpr_spill"]) for k in ks if k["sgpr_spill"]]
+    assert not bad, bad

@@ -2,9 +2,10 @@
 call of this session on the GPU. fcs_engine_host_fallbacks counts the calls its host CRC answered
 (only after the GPU attempt and its retry both failed, or for buffers >= 4 GiB); on a
 healthy MI355X it must be 0, which shows the HIP path served every drop-in call of the suite.
-fcs_engine_host_batches counts the TX/RX queue batches its host CRC answered after a failed GPU
-step (test_gpu_txq.py, test_gpu_rxq.py and the pcap/RX paths run through the product library);
-it must be 0 too. The fault-injection tests use the separate libnstack_fcs_faults.so."""
+fcs_engine_host_batches counts the host batch calls (ether_fcs_*_host, and through them the TX/RX
+queue batches of test_gpu_txq.py, test_gpu_rxq.py and the pcap/RX paths) its host CRC answered after
+a failed GPU step; it must be 0 too: every host batch call of the suite ran on the GPU. The
+fault-injection tests use the separate libnstack_fcs_faults.so."""
 import pytest
 
 import nstack_amd as na

@@ -51,6 +51,9 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_ST_UNIT=1024 -DFCS_ST_CHAINS=2"),
     ("fcs_kernel.hip", "-DFCS_ST_ABL_NOCLOSE -DFCS_ST_ABL_NOSHIFT -DFCS_ST_NOSKEW"),
     ("fcs_kernel.hip", "-DFCS_ST_SKIPJ0 -DFCS_ST_PROBE_LDS=8 -DFCS_ST_PROBE_VALU=32"),
+    ("fcs_kernel.hip", "-DFCS_ST_ALIGN16 -DFCS_ST_SMASK -DFCS_SEGIL_ISSUE_LOOP"),
+    ("fcs_kernel.hip", "-DFCS_ST_EDGE_AUX=0"),
+    ("fcs_kernel.hip", "-DFCS_ST_TREE"),
     ("fcs_engine.cpp", "-DFCS_FAULT_HOOK -DFCS_GRID_CUS=128 -DFCS_FLAT_DYN_MIN=1000 -DFCS_FIXED_DYN_MIN=8 "
                        "-DFCS_FIXED_FLAT_MAX=0 -DFCS_ZC_MAX_MB=16 -DFCS_NO_STREAM"),
     ("fcs_engine.cpp", "-DFCS_STAMPS -DFCS_HOST_TRACE -DFCS_PIPE_DEPTH=3"),
