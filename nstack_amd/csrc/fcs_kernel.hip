@@ -1160,9 +1160,8 @@ __host__ __device__ constexpr int wide_cl0(int wd) {
     return wd == 32 ? 16 : (wd == 30 ? 14 : (wd == 26 ? 12 : wd - 2 * (wd / 4)));
 }
 
-template <int WD, int G>
+template <int WD, int G, int NT = wide_threads(WD)>   // NT: the workgroup size (the staging stride)
 __device__ __forceinline__ void stage_wide_tables(const KParams &p, uint8_t *lds, int tid) {
-    constexpr int NT = wide_threads(WD);
     static_assert(G == 16 ? (WD == 26 || WD == 30 || WD == 32 || wide_mid_ok(WD))
                           : (G == 8 ? wide8_ok(WD) : (G == 4 && wide4_ok(WD))), "window width");
     constexpr uint32_t kLane = G == 4 ? kBlobLane4 + (uint32_t)(WD - kWide4Min) * 4096u
@@ -1618,6 +1617,173 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     }
 #endif
     flush_bad<kDmaBad>(p, lds);
+}
+
+// ---------------------------------------------------------------------------------------------
+// Fixed length over 1524 B in segments of the wide kernel's cover (fcs_segw_kernel<WD>, WD 26 / 30;
+// host-selected by segment_wd()). fcs_segil_kernel's schedule (units of four frames, item r =
+// segment r of the four, four DMA runs into 2 KiB parts of an 8 KiB slot, 12 waves) with
+// fcs_wide_kernel<WD>'s lane windows (4 WD bytes every 4 WD - 4): C = wide_cover(WD) bytes per
+// segment (1604 / 1860 B), so a frame takes ceil(L / C) items where fcs_segil_kernel takes
+// ceil(L / 1524) (9216 B: 5 items of 30 words per lane against 7 of 24).
+// The front segment of Lf = L - C (m - 1) bytes is the wide kernel's frame of length Lf (front lane
+// cf, its zc leading bytes masked, INV[zc]; lanes past cf dropped; launch constants). In the other
+// segments every lane masks its first word (the next lane's last) except lane 15, whose window
+// starts at the segment start and whose chain starts from the frame's CRC state after the previous
+// segment (the row XOR), as in fcs_segil_kernel.
+// LDS: the wide kernel's 64 KiB table image, then 12 slots of 8 KiB (160 KiB).
+// CPU model: tests/kernel_model.py model_segw_frame.
+// ---------------------------------------------------------------------------------------------
+template <int WD>
+__global__ __launch_bounds__(kSegilThreads, 1) void fcs_segw_kernel(KParams p) {
+    constexpr uint32_t kWin = wide_win(WD), kStep = wide_step(WD), kCov = wide_cover(WD);
+    constexpr int CL0 = wide_cl0(WD), CL1 = WD - CL0, CLM = CL0 > CL1 ? CL0 : CL1;
+    // a run (at most 15 bytes of alignment, the segment, the last window's extra dword) and the odd
+    // runs' skew stay inside the run's 2 KiB part; two DMA rows of 64 pieces hold it
+    static_assert(FCS_SEGIL_SKEW + 16 + kCov + 16 <= kSegilRunBytes && (kCov + 30) / 16 <= 128, "run part");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kSegilLdsBytes];
+    const int tid = threadIdx.x;
+    stage_wide_tables<WD, 16, kSegilThreads>(p, lds, tid);
+    init_bad<kWideBad>(lds);
+    __syncthreads();
+
+    // ---- frame geometry (wave-uniform) ----
+    const uint32_t L = p.flen;
+    const uint32_t m = (L + kCov - 1) / kCov;   // segments, >= 2
+    const uint32_t Lf = L - kCov * (m - 1);     // front segment, 1 .. kCov
+
+    const int lane = tid & 63;
+    const int c = lane & 15;                    // window index back from the segment end
+    const uint32_t q = (uint32_t)lane >> 4;     // quarter: frame 4 u + q of unit u
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const uint8_t *slot = lds + kDmaRing + (uint32_t)wave * kSegilSlotBytes;
+    const uint8_t *run = slot + q * kSegilRunBytes + (q & 1u) * FCS_SEGIL_SKEW;
+    const uint32_t h = (uint32_t)(lane >> 3) & 3u, r4 = (uint32_t)(lane & 7) * 4u;
+    const uint32_t B[4] = {r4 + 32u * (0u ^ h), r4 + 32u * (1u ^ h), r4 + 32u * (2u ^ h), r4 + 32u * (3u ^ h)};
+    const uint32_t SEL[4] = {0x0C0C0400u + ((0u ^ h) << 8), 0x0C0C0400u + ((1u ^ h) << 8),
+                             0x0C0C0400u + ((2u ^ h) << 8), 0x0C0C0400u + ((3u ^ h) << 8)};
+    const uint32_t lanebase = kDmaHole + (uint32_t)(lane & 31) * 4u;
+
+    // front segment: the wide kernel's front lane for length Lf (scalars but the lane tests)
+    const uint32_t cf = (Lf - 1u) / kStep < 15u ? (Lf - 1u) / kStep : 15u;
+    const uint32_t zc = kStep * cf + kWin - Lf;   // 0 .. kWin - 1
+    const bool flive = (uint32_t)c <= cf, ffront = (uint32_t)c == cf;
+    const uint32_t x0f = ffront ? lds_rd(lds, dma_hole(kWideInvHole + zc / 32u) + (zc % 32u) * 4u) : 0u;
+    const uint32_t m0f = ffront ? (zc >= 4u ? 0u : (uint32_t)(0xFFFFFFFFull << (8u * zc))) : 0u;
+    uint32_t keepf = ffront ? 0u : 0xFFFFFFFFu;
+    asm volatile("" : "+v"(keepf));
+    const uint32_t fgroups = (zc + 15u) / 16u;    // word groups of four holding masked front bytes
+    // other segments: lane 15 takes the segment's first word whole
+    const uint32_t m0n = c == 15 ? 0xFFFFFFFFu : 0u;
+
+    const uint64_t n = p.n, units = (n + 3) >> 2;
+    // chunk sizes as fcs_segil_kernel's
+    constexpr uint32_t kSegilChunkItems = FCS_SEGIL_CMAX_ITEMS;
+    const uint32_t cmax = m >= 4 ? (kSegilChunkItems / m > 32u ? 32u : (kSegilChunkItems / m < 1u ? 1u : kSegilChunkItems / m))
+                                 : 64u / m;
+    Dispenser D(p.ctr, units, (uint64_t)gridDim.x * kSegilWaves, (uint64_t)blockIdx.x * kSegilWaves + (uint64_t)wave,
+                lane, 100, 1, cmax);
+    D.align = 16;
+    constexpr uint64_t kEnd = Dispenser::kEnd;
+    auto seg_start = [&](uint64_t f, uint32_t r) {
+        return p.base + f * p.stride + (r ? (uint64_t)Lf + (uint64_t)kCov * (r - 1) : 0ull);
+    };
+    auto issue = [&](uint64_t u, uint32_t r) {   // the item's four runs (wave-uniform control)
+        const uint32_t len = r ? kCov : Lf;
+#pragma unroll
+        for (uint32_t qq = 0; qq < 4; qq++) {
+            const uint64_t f = 4 * u + qq;
+            if (f < n) {
+                const uint64_t s0 = seg_start(f, r), a = s0 & ~15ull;
+                const uint32_t pieces = (uint32_t)((((s0 + len) + 15) & ~15ull) - a) >> 4;
+                segil_run(slot + qq * kSegilRunBytes + (qq & 1u) * FCS_SEGIL_SKEW, a, lane, pieces);
+            }
+        }
+    };
+
+    uint64_t u = D.first();
+    uint32_t r = 0;
+    if (u != kEnd) issue(u, 0);
+    uint32_t acc = 0;     // this quarter's frame: CRC state after its segments so far
+    uint32_t cbuf = 0;    // FCSs of the current run of units, lane 4 (unit & 15) + frame
+    uint64_t cmask = 0;   // lanes of cbuf that hold one (wave-uniform)
+    while (u != kEnd) {   // wave-uniform
+        const uint64_t f = 4 * u + q;
+        const uint64_t s0 = f < n ? seg_start(f, r) : 0ull;
+        const uint32_t len = r ? kCov : Lf;
+        // window start in the run: >= -(kWin - 1) for live lanes (the front lane's masked bytes may
+        // lie before it); dropped front lanes read below the run, inside the LDS, and are discarded
+        const int64_t x = (int64_t)(s0 & 15ull) + (int64_t)len - (int64_t)(kStep * (uint32_t)c) - (int64_t)kWin;
+        const uint32_t ra = (uint32_t)x & 3u;
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's runs have landed
+        const uint32_t *wp = reinterpret_cast<const uint32_t *>(run + (x & ~3ll));
+        uint32_t d[WD + 1];
+#pragma unroll
+        for (int i = 0; i <= WD; i++) d[i] = wp[i];
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+
+        // ---- the next item: the next segment of the unit, or the dispenser's next unit ----
+        uint64_t un = u;
+        uint32_t rn = r + 1;
+        if (rn == m) {
+            un = D.next(u);
+            rn = 0;
+        }
+        if (un != kEnd) issue(un, rn);
+
+        // ---- this item ----
+        uint32_t w[WD];
+#pragma unroll
+        for (int i = 0; i < WD; i++) w[i] = __builtin_amdgcn_alignbyte(d[i + 1], d[i], ra);
+        uint32_t x0;
+        bool live = true;
+        if (r == 0) {
+            w[0] &= m0f;
+            // words 1.. of the front lane up to its zc bytes: groups of four below an opaque scalar
+            // bound (hoisted group tests would each hold an SGPR pair)
+            uint32_t gm = fgroups;
+            asm volatile("" : "+s"(gm));
+#pragma unroll
+            for (int g = 0; g < (WD + 3) / 4; g++) {
+                if ((uint32_t)g >= gm) break;
+#pragma unroll
+                for (int i = (4 * g > 1 ? 4 * g : 1); i < 4 * g + 4 && i < WD; i++) {
+                    const int t = (int)zc - 4 * i;
+                    const uint32_t mk = t >= 4 ? 0u : (uint32_t)(0xFFFFFFFFull << (8 * (t < 0 ? 0 : t)));
+                    w[i] &= mk | keepf;
+                }
+            }
+            x0 = x0f;
+            live = flive;
+        } else {
+            w[0] &= m0n;
+            x0 = c == 15 ? acc : 0u;
+        }
+        uint32_t xa = w[0] ^ x0, xb = w[CL0];
+#pragma unroll
+        for (int i = 0; i < CLM; i++) {
+            if (i < CL0) xa = step4_l8(lds, xa, i < CL0 - 1 ? w[i + 1] : 0u, B, SEL);
+            if (i < CL1) xb = step4_l8(lds, xb, i < CL1 - 1 ? w[CL0 + i + 1] : 0u, B, SEL);
+        }
+        const uint32_t mv = merge_shift_dma(lds, 0, xa, xb);
+        uint32_t v = lane_shift_dma(lds, mv, lanebase);
+        if (!live) v = 0u;
+        acc = row_xor(v);
+        if (r == m - 1) {   // results of consecutive units leave as one coalesced store
+            const uint32_t k = (uint32_t)(u & 15u);
+            const uint32_t vq = (uint32_t)__shfl((int)~acc, (lane & 3) * 16);
+            if ((uint32_t)(lane >> 2) == k) cbuf = vq;
+            const uint64_t f0 = 4 * u;
+            cmask |= (f0 + 4 <= n ? 0xFull : ((1ull << (n - f0)) - 1ull)) << (4 * k);
+            if (k == 15 || un != u + 1) {
+                emit<kWideBad>(p, lds, (cmask >> lane) & 1ull, 4 * (u & ~15ull) + (uint64_t)lane, cbuf);
+                cmask = 0;
+            }
+        }
+        u = un;
+        r = rn;
+    }
+    flush_bad<kWideBad>(p, lds);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -2923,7 +3089,13 @@ hipError_t launch_fixed_route(const FixedRoute &r, const KParams &p, int grid, h
 #undef FCS_WIDE
         break;
     case FixedKernel::kSegment:
-        FCS_GO(FixedKernel::kSegment, 0, kSegilThreads, false, fcs_segil_kernel);
+        switch (r.wd) {
+            case 24: FCS_GO(FixedKernel::kSegment, 24, kSegilThreads, false, fcs_segil_kernel); break;
+            case 26: FCS_GO(FixedKernel::kSegment, 26, kSegilThreads, false, fcs_segw_kernel<26>); break;
+            case 30: FCS_GO(FixedKernel::kSegment, 30, kSegilThreads, false, fcs_segw_kernel<30>); break;
+            case 32: FCS_GO(FixedKernel::kSegment, 32, kSegilThreads, false, fcs_segw_kernel<32>); break;
+            default: return hipErrorInvalidValue;
+        }
         break;
     case FixedKernel::kDma:
         if (r.wd == 2) FCS_GO(FixedKernel::kDma, 2, kDmaWgThreads, false, (fcs_dma_kernel<2, false>));

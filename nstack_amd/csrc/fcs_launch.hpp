@@ -172,6 +172,31 @@ inline bool fixed_segil(const KParams &p) {
     return p.flen >= kSegilMinLen2;
 #endif
 }
+// Segment width for a batch fixed_segil() takes: 24 (fcs_segil_kernel, 1524-B segments) or 26 / 30 /
+// 32 (fcs_segw_kernel<WD>, segments of wide_cover(WD) = 1604 / 1860 / 1988 B): the least per-lane
+// work per frame, m (WD + kSegItemWords) for m = ceil(len / cover) items of WD words each plus a
+// fixed per-item cost in word equivalents (merge, lane shift, row XOR, waits, four run issues).
+#ifndef FCS_SEG_ITEM_WORDS   // measurement-only override of the per-item cost
+#define FCS_SEG_ITEM_WORDS 8
+#endif
+constexpr uint32_t kSegItemWords = FCS_SEG_ITEM_WORDS;
+__host__ __device__ constexpr int segment_wd(uint32_t len) {
+#ifdef FCS_SEGW_FORCE   // measurement-only: one width for every segment batch
+    return (void)len, FCS_SEGW_FORCE;
+#else
+    int best = 24;
+    uint64_t cost = (uint64_t)((len + kDmaCover - 1) / kDmaCover) * (24u + kSegItemWords);
+    const int wds[3] = {26, 30, 32};
+    for (int i = 0; i < 3; i++) {
+        const uint64_t m = (len + wide_cover(wds[i]) - 1) / wide_cover(wds[i]);
+        if (m * ((uint64_t)wds[i] + kSegItemWords) < cost) {
+            cost = m * ((uint64_t)wds[i] + kSegItemWords);
+            best = wds[i];
+        }
+    }
+    return best;
+#endif
+}
 // Wide LDS-DMA kernel (fcs_wide_kernel): one-item frames of kWideMinLen..kWideCover bytes (128-B
 // lane windows, 12 waves, 8 KiB slots) whose four consecutive frames fit one slot, as fixed_dma().
 // Against the kernels these lengths took before (tools/ab.py, one process): 1537 B
@@ -360,7 +385,8 @@ inline FixedRoute route_fixed(const KParams &p, bool big) {
         const int wd = wide_wd(p);
         return {FixedKernel::kWide16, wd, false, wide_threads(wd), 4, kDmaDynMinItemsPerWave, p.zmax};
     }
-    if (fixed_segil(p)) return {FixedKernel::kSegment, 0, false, kSegilWgThreads, 4, kFixedDynMinUnitsPerWave, p.zmax};
+    if (fixed_segil(p))
+        return {FixedKernel::kSegment, segment_wd(p.flen), false, kSegilWgThreads, 4, kFixedDynMinUnitsPerWave, p.zmax};
     if (!tiny && fixed_dma(p)) {   // the front lane masks kDmaCover - len bytes, lanes 3/7/11 one word
         const uint32_t z = kDmaCover - p.flen > 4 ? kDmaCover - p.flen : 4;
         return {FixedKernel::kDma, z <= 8 ? 2 : (int)(kSingleMaxLead / 4), false, kDmaWgThreads, 4, kDmaDynMinItemsPerWave, z};

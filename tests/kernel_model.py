@@ -450,3 +450,60 @@ def model_wide_item(lds, mem: bytes, base: int, stride: int, flen: int, n: int, 
         out.append((~v & 0xFFFFFFFF) if f + g < n else None)
     return out
 
+
+
+# ---- fcs_segw_kernel<WD>: frame-interleaved segments of the wide kernel's cover (WD 26 / 30) ----
+def model_wide_window_value(lds, win: bytes, lane: int, z: int, x0: int, wd: int):
+    """One lane window of fcs_wide_kernel<WD> (4 WD bytes, the first z masked, x0 into chain 0's
+    start): two chains merged with A_{4 (WD - CL0)}, lane shift A_{(4 WD - 4) c}."""
+    cl0 = WIDE_CL0[wd]
+    w = [int.from_bytes(win[4 * i:4 * i + 4], "little") for i in range(wd)]
+    for i in range(wd):
+        t = max(0, min(4, z - 4 * i))
+        w[i] &= (0xFFFFFFFFFFFFFFFF << (8 * t)) & 0xFFFFFFFF
+    xs = [w[0] ^ x0, w[cl0]]
+    for i in range(cl0):
+        xs[0] = step4_l8(lds, xs[0], lane) ^ (w[i + 1] if i < cl0 - 1 else 0)
+    for i in range(wd - cl0):
+        xs[1] = step4_l8(lds, xs[1], lane) ^ (w[cl0 + i + 1] if i < wd - cl0 - 1 else 0)
+    m = merge_shift(lds, 0, xs[0]) ^ xs[1]
+    lanebase = 128 + (lane & 31) * 4
+    s = 0
+    for t in range(8):
+        sh = (m >> (4 * t - 8)) if 4 * t >= 8 else ((m << (8 - 4 * t)) & 0xFFFFFFFF)
+        s ^= int(lds[(((sh & 0xF00) | lanebase) + t * 4096) // 4])
+    return s
+
+
+def model_segw_frame(lds, frame: bytes, garbage: bytes, wd: int):
+    """FCS of one frame by fcs_segw_kernel<WD>'s decomposition: a front segment of
+    Lf = L - C (m - 1) bytes (C = wide_cover(WD)), then C-byte segments, each the wide kernel's 16
+    windows ending at the segment end. Front: the wide kernel's front lane cf and zc for length Lf
+    (INV[zc], lanes past cf dropped). Other segments: every lane masks its first word (the next
+    lane's last) except lane 15, whose window starts at the segment start and whose chain starts
+    from the frame's CRC state after the previous segment."""
+    C = wide_cover(wd)
+    step, win = 4 * wd - 4, 4 * wd
+    L = len(frame)
+    m = -(-L // C)
+    lf = L - C * (m - 1)
+    padded = bytes(garbage[:C]) + frame
+    acc = 0
+    for r in range(m):
+        end = C + lf + C * r
+        v = 0
+        for c in range(16):
+            ws = end - step * c - win
+            w = padded[ws:ws + win]
+            if r == 0:
+                cf, zc = wide_front(lf, wd)
+                if c > cf:
+                    continue
+                z = zc if c == cf else 4
+                x0 = int(lds[(hole(WIDE_INV_HOLE + zc // 32) + (zc % 32) * 4) // 4]) if c == cf else 0
+            else:
+                z = 0 if c == 15 else 4
+                x0 = acc if c == 15 else 0
+            v ^= model_wide_window_value(lds, w, c, z, x0, wd)
+        acc = v
+    return ~acc & 0xFFFFFFFF

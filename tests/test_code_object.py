@@ -47,7 +47,7 @@ def _kernels(lib_path):
 def test_no_spills_no_scratch_and_registers_fit_the_workgroup():
     ks = _kernels(na.LIB_PATH)
     names = {k["name"] for k in ks}
-    for want in ("fcs_dma_kernel", "fcs_segil_kernel", "fcs_stream_kernel", "fcs_flat_kernel", "fcs_one_kernel",
+    for want in ("fcs_dma_kernel", "fcs_segil_kernel", "fcs_segw_kernel", "fcs_stream_kernel", "fcs_flat_kernel", "fcs_one_kernel",
                  "inet_flat_kernel"):
         assert any(want in n for n in names), want
     bad = [k for k in ks if k["vgpr_spill"] or k["scratch"]]
@@ -60,9 +60,9 @@ def test_no_spills_no_scratch_and_registers_fit_the_workgroup():
 @pytest.mark.skipif(not os.path.exists(f"{LLVM}/llvm-readelf"), reason="ROCm LLVM tools not installed")
 def test_baseline_kernels_spill_no_sgprs():
     """The kernels of the BASELINE configs (the LDS-DMA kernel: 1518 B; the arena stream: IMIX; the
-    interleaved segments: jumbo) and the wide windows keep every scalar in SGPRs: a spilled SGPR costs
+    interleaved segments of either window: jumbo) and the wide windows keep every scalar in SGPRs: a spilled SGPR costs
     a v_writelane / v_readlane pair per use (the segment kernel had 10)."""
-    hot = ("fcs_dma_kernel", "fcs_segil_kernel", "fcs_stream_kernel", "fcs_wide_kernel")
+    hot = ("fcs_dma_kernel", "fcs_segil_kernel", "fcs_segw_kernel", "fcs_stream_kernel", "fcs_wide_kernel")
     ks = [k for k in _kernels(na.LIB_PATH) if any(h in k["name"] for h in hot)]
     assert len(ks) >= 40
     bad = [(k["name"], k["sgpr_spill"]) for k in ks if k["sgpr_spill"]]

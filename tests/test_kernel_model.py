@@ -276,3 +276,17 @@ def test_wide_windows_bank_distinct():
         for E in range(0, 64, 4):
             banks = {((E - km.wide_end_off(c, wd) - 4 * wd) // 4) % 32 for c in range(16)}
             assert len(banks) == 16
+
+
+@pytest.mark.parametrize("L,wd", [(1989, 26), (3100, 26), (3208, 26), (3209, 26), (6100, 26), (9216, 26),
+                                  (1989, 30), (3720, 30), (3721, 30), (5000, 30), (9216, 30), (9300, 30), (9301, 30)])
+def test_segw_decomposition_model(lds_wide, L, wd):
+    """fcs_segw_kernel<WD>'s decomposition: a front segment of L - C (m - 1) bytes (C = the wide
+    kernel's cover: 1604 B for WD 26, 1860 B for WD 30) with the wide kernel's front lane, then
+    C-byte segments whose lane 15 starts unmasked from the frame's CRC state after the previous
+    segment, reproduces the CRC (zlib = src/ether_fcs.c:4-19); cover bytes before the frame are
+    random garbage."""
+    rng = np.random.default_rng(L * 3 + wd)
+    frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
+    garbage = rng.integers(0, 256, 2048, dtype=np.uint8).tobytes()
+    assert km.model_segw_frame(lds_wide[wd], frame, garbage, wd) == zlib.crc32(frame)

@@ -23,7 +23,8 @@ PACKED = {
     868: "wide8:28", 869: "flat", 870: "wide16:15", 1000: "wide16:18", 1157: "wide16:20", 1476: "wide16:24",
     1477: "wide16:26", 1495: "wide16:26", 1496: "lds-dma", 1518: "lds-dma", 1524: "lds-dma", 1525: "wide16:26",
     1536: "wide16:26", 1604: "wide16:26", 1605: "wide16:30", 1787: "wide16:30", 1788: "wide16:32",
-    1988: "wide16:32", 2500: "segment", 3049: "generic", 3073: "segment", 9000: "segment", 65536: "segment",
+    1988: "wide16:32", 2500: "segment", 3049: "generic", 3073: "segment:26", 9000: "segment:30", 9216: "segment:30",
+    65536: "segment:32",
 }
 
 
@@ -79,3 +80,26 @@ def test_sweep_tool_agrees(lib):
             assert fam.startswith("wide") and "lanes" not in fam, (L, got, fam)
         else:
             assert fam.startswith(prefix[kind]), (L, got, fam)
+
+
+def _seg_item_words():
+    import re
+    hdr = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "nstack_amd", "csrc", "fcs_launch.hpp")
+    return int(re.search(r"#define FCS_SEG_ITEM_WORDS (\d+)", open(hdr).read()).group(1))
+
+
+def test_segment_width_rule(lib):
+    """Packed batches the segment route takes pick the segment width with the least per-lane work,
+    m (WD + K) for m = ceil(len / cover) (fcs_launch.hpp segment_wd: cover 1524 B for WD 24, the
+    wide kernel's 1604 / 1860 / 1988 B for WD 26 / 30 / 32; ties keep the narrower width)."""
+    K = _seg_item_words()
+    cover = {24: 1524, 26: 1604, 30: 1860, 32: 1988}
+    seen = set()
+    for L in list(range(1950, 12000, 7)) + [16384, 40000, 65536, 100000]:
+        got = lib.fixed_route(BASE, L, L, BIG)
+        if not got.startswith("segment"):
+            continue
+        best = min((-(-L // cover[w]) * (w + K), w) for w in (24, 26, 30, 32))[1]
+        assert got == ("segment" if best == 24 else f"segment:{best}"), (L, got, best)
+        seen.add(best)
+    assert seen == {24, 26, 30, 32}

@@ -9,6 +9,7 @@
 #   ranks2                the 2-rank bench rehearsal on one GPU (bench.py --gpus 2, self-launched)
 #   profile               tools/profile_round.sh OUT/prof (kernel trace + PMC traffic + rehearsal)
 #   ab:ARGS               python tools/ab.py ARGS (variants built by tools/variants.sh)
+#   pmc:ARGS              tools/pmc.sh OUT/pmc ARGS (SQ counter passes over tools/prof_fixed.py ARGS)
 #   py:SCRIPT[,ARGS]      python SCRIPT ARGS (a measurement tool under tools/)
 set -o pipefail
 out=gpurun_out/${1:?usage: gpu_run.sh OUT STEP...}; shift
@@ -41,6 +42,9 @@ for step in "$@"; do
     ab)
       timeout -k 10 600 python -u tools/ab.py ${arg//,/ } > "$log" 2>&1; rc=$?
       echo "ab rc=$rc"; grep -E "GB/s|TB/s|ms" "$log" | tail -20 ;;
+    pmc)
+      timeout -k 10 900 bash tools/pmc.sh "$out/pmc" ${arg//,/ } > "$log" 2>&1; rc=$?
+      echo "pmc rc=$rc"; tail -8 "$log" ;;
     py)
       timeout -k 10 600 python -u ${arg//,/ } > "$log" 2>&1; rc=$?
       echo "py rc=$rc"; tail -20 "$log" ;;

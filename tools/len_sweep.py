@@ -43,7 +43,9 @@ def family(L):
         return "wide WD32"
     m = (L + 1523) // 1524
     if m >= 4 or (m == 3 and L > 3072) or (m == 2 and L >= 1950):
-        return "segment (interleaved)"
+        cover = {24: 1524, 26: 1604, 30: 1860, 32: 1988}
+        wd = min((-(-L // cover[w]) * (w + 8), w) for w in (24, 26, 30, 32))[1]
+        return "segment (interleaved)" if wd == 24 else f"segment (interleaved, WD{wd})"
     return "generic"
 
 
