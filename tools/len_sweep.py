@@ -51,7 +51,8 @@ def family(L):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--lens", default=",".join(map(str, DEFAULT_LENS)))
+    ap.add_argument("--lens", nargs="+", default=[",".join(map(str, DEFAULT_LENS))],
+                    help="lengths, comma- or space-separated")
     ap.add_argument("--gib", type=float, default=24.0)
     ap.add_argument("--reps", type=int, default=5)
     a = ap.parse_args()
@@ -64,7 +65,7 @@ def main():
     arena = torch.empty(cap + 64, dtype=torch.uint8, device=dev)
     na.fill_splitmix_dev(arena, cap + 64, 5, 0)
     st = torch.cuda.current_stream()
-    for L in [int(x) for x in a.lens.split(",")]:
+    for L in [int(x) for x in ",".join(a.lens).split(",") if x]:
         n = cap // L
         out = torch.empty(n, dtype=torch.int32, device=dev)
         na.fixed_dev(arena, L, L, n, out, st)   # untimed
@@ -79,7 +80,8 @@ def main():
         ms = statistics.median(times)
         print(json.dumps({"len": L, "frames": n, "bytes": n * L, "ms": round(ms, 4),
                           "GB_s": round(n * L / ms / 1e6, 1), "frac_of_8TBs": round(n * L / ms / 1e6 / 8000, 4),
-                          "Mframes_s": round(n / ms / 1e3, 1), "kernel": family(L)}), flush=True)
+                          "Mframes_s": round(n / ms / 1e3, 1), "kernel": family(L),
+                          "route": na.fixed_route(arena.data_ptr(), L, L, n)}), flush=True)
         del out
 
 
