@@ -1470,11 +1470,7 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
     };
     auto issue = [&](uint64_t u, uint32_t r) {   // the item's four runs (wave-uniform control)
         const uint32_t len = r ? kDmaCover : Lf;
-#ifdef FCS_SEGIL_ISSUE_LOOP   // measurement-only: the four runs issued by a scalar loop
-#pragma unroll 1
-#else
 #pragma unroll
-#endif
         for (uint32_t qq = 0; qq < 4; qq++) {
             const uint64_t f = 4 * u + qq;
             if (f < n) {
@@ -2586,33 +2582,6 @@ __global__ __launch_bounds__(kWgThreads, 1) void fcs_stream_kernel(KParams p) {
             }
             const uint32_t c0 = x;
             x = hole_shift(lds, c0, kStHoleWord + 4u * 8u, y);
-#elif defined(FCS_ST_TREE)
-            // measurement-only: all 16 chain states kept, the state before word k picked by a tree of
-            // selects on the bits of k (15 selects and 4 bit tests instead of 16 compares and selects)
-            uint32_t xs16[16];
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                xs16[i] = x;
-                x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
-            }
-#pragma unroll
-            for (int b = 0; b < 4; b++) {
-                const bool hi = (k >> b) & 1u;
-#pragma unroll
-                for (int i = 0; i < (8 >> b); i++) xs16[i] = hi ? xs16[2 * i + 1] : xs16[2 * i];
-            }
-            xk = xs16[0];
-#elif defined(FCS_ST_SMASK)
-            // measurement-only: the state before word k picked by lane masks built with scalar ops from
-            // the four bit planes of k (a v_cndmask on an SGPR mask per word, no per-word v_cmp)
-            const uint64_t kb0 = __ballot(k & 1u), kb1 = __ballot(k & 2u), kb2 = __ballot(k & 4u), kb3 = __ballot(k & 8u);
-#pragma unroll
-            for (int i = 0; i < 16; i++) {
-                const uint64_t mi = ((i & 1) ? kb0 : ~kb0) & ((i & 2) ? kb1 : ~kb1) & ((i & 4) ? kb2 : ~kb2) &
-                                    ((i & 8) ? kb3 : ~kb3);
-                if (__builtin_amdgcn_inverse_ballot_w64(mi)) xk = x;
-                x = step4_l8(lds, x, i < 15 ? w[i + 1] : 0u, B, SEL);
-            }
 #else
 #pragma unroll
             for (int i = 0; i < 16; i++) {

@@ -51,9 +51,8 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_ST_UNIT=1024 -DFCS_ST_CHAINS=2"),
     ("fcs_kernel.hip", "-DFCS_ST_ABL_NOCLOSE -DFCS_ST_ABL_NOSHIFT -DFCS_ST_NOSKEW"),
     ("fcs_kernel.hip", "-DFCS_ST_SKIPJ0 -DFCS_ST_PROBE_LDS=8 -DFCS_ST_PROBE_VALU=32"),
-    ("fcs_kernel.hip", "-DFCS_ST_ALIGN16 -DFCS_ST_SMASK -DFCS_SEGIL_ISSUE_LOOP"),
+    ("fcs_kernel.hip", "-DFCS_ST_ALIGN16"),
     ("fcs_kernel.hip", "-DFCS_ST_EDGE_AUX=0"),
-    ("fcs_kernel.hip", "-DFCS_ST_TREE"),
     ("fcs_kernel.hip", "-DFCS_SEGW_FORCE=26"),
     ("fcs_kernel.hip", "-DFCS_SEG_ITEM_WORDS=6"),
     ("fcs_engine.cpp", "-DFCS_FAULT_HOOK -DFCS_GRID_CUS=128 -DFCS_FLAT_DYN_MIN=1000 -DFCS_FIXED_DYN_MIN=8 "
