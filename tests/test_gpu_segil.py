@@ -1,6 +1,7 @@
-"""GPU parity of the frame-interleaved segment kernel (fcs_segil_kernel).
+"""GPU parity of the frame-interleaved segment route (fcs_segil_kernel, and fcs_segw_kernel<WD>
+where segment_wd() picks wider segments).
 
-Fixed-length frames over 1524 B take this kernel when m = ceil(len / 1524) >= 4, or m = 3 and
+Fixed-length frames over 1524 B take the segment route when m = ceil(len / 1524) >= 4, or m = 3 and
 len > 3072, or m = 2 and len >= 1950 (fixed_segil(), fcs_launch.hpp),
 at any stride: a front segment of len - 1524 (m - 1) bytes, then 1524-B segments; item r of a
 wave's unit is segment r of its four frames (one per quarter-wave, four DMA runs), and a frame's
