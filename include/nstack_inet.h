@@ -62,6 +62,12 @@ int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, cons
  * Results are identical either way. Default 16384. Returns the previous value. */
 uint64_t inet_csum_set_flat_threshold(uint64_t packets);
 
+/* Tuning: fixed-stride batches (inet_csum_fixed_dev) of more than `packets` packets whose packets
+ * fill at least half their stride (64..1550 B, stride <= 2048) stream through LDS by DMA, four
+ * packets per wave item. Results are identical either way. Default 16384. Returns the previous
+ * value. */
+uint64_t inet_csum_set_dma_threshold(uint64_t packets);
+
 /* ---- single packet, same arguments and result as the reference functions ---- */
 uint16_t inet_ip_checksum(const void *dp, size_t bsize);                          /* ip.c:39  */
 uint16_t inet_tcp_checksum(uint32_t src, uint32_t dst, const void *dp, size_t bsize); /* tcp.c:167 */

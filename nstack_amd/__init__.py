@@ -17,7 +17,7 @@ LIB_PATH = os.environ.get("NSTACK_FCS_LIB") or os.path.join(_HERE, "libnstack_fc
 
 __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fixed_host",
            "batch_host", "tx_host", "tx_batch_host", "host_buffer", "host_free", "verify_dev", "verify_fixed_dev", "verify_host", "fill_splitmix_dev", "read_stream_dev", "timed_fixed_dev",
-           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan", "dma_stream_dev", "stream_load_dev", "load_faults", "FAULTS_PATH"]
+           "tables_blob", "TxQueue", "RxQueue", "set_var_threshold", "pcap_scan", "pcap_read", "pcap_write", "inet_batch_dev", "inet_fixed_dev", "inet_batch_host", "inet_set_flat_threshold", "inet_set_dma_threshold", "ip_checksum", "tcp_checksum", "udp_checksum", "INET_MODES", "engine_init", "engine_fini", "version", "LIB_PATH", "EXPORTS", "engine_stats", "shard_plan", "dma_stream_dev", "stream_load_dev", "load_faults", "FAULTS_PATH"]
 
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
@@ -33,7 +33,7 @@ EXPORTS = [
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
     # include/nstack_inet.h — batched Internet checksums (opt-in)
-    "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_csum_set_flat_threshold", "inet_ip_checksum",
+    "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_csum_set_flat_threshold", "inet_csum_set_dma_threshold", "inet_ip_checksum",
     "inet_tcp_checksum", "inet_udp_checksum",
     # include/nstack_rxq.h — batched RX call site with FCS verification
     "fcs_rxq_create", "fcs_rxq_receive", "fcs_rxq_stats", "fcs_rxq_fallbacks", "fcs_rxq_destroy",
@@ -150,6 +150,7 @@ def _bind(path: str) -> ctypes.CDLL:
         "inet_csum_fixed_dev": (i32, [i32, vp, u64, u32, u64, vp, vp, vp]),
         "inet_csum_batch_host": (i32, [i32, vp, u64, vp, vp, vp, vp, u64]),
         "inet_csum_set_flat_threshold": (u64, [u64]),
+        "inet_csum_set_dma_threshold": (u64, [u64]),
         "fcs_rxq_create": (vp, [i32, vp, u32, u32]),
         "fcs_rxq_receive": (i32, [vp, vp, vp, c.c_size_t]),
         "fcs_rxq_stats": (None, [vp] + [c.POINTER(u64)] * 5),
@@ -533,6 +534,12 @@ def inet_batch_host(mode, arena, arena_bytes: int, off, length, addr, out, n: in
 def inet_set_flat_threshold(packets: int) -> int:
     """Variable-length batches of more than `packets` packets use the flat kernel; returns the old value."""
     return int(load().inet_csum_set_flat_threshold(packets))
+
+
+def inet_set_dma_threshold(packets: int) -> int:
+    """Fixed-stride batches of more than `packets` packets use the LDS-DMA kernel (when their
+    geometry fits its slots); returns the old value."""
+    return int(load().inet_csum_set_dma_threshold(packets))
 
 
 def ip_checksum(data) -> int:

@@ -1,6 +1,9 @@
 // fcs_device.hpp — device lookup shared by the library's translation units (not exported).
 #pragma once
+#include <hip/hip_runtime_api.h>
 #include <stdint.h>
+
+#include <functional>
 
 namespace fcs {
 // The calling thread's current HIP device, checked to be a gfx950 (lazily initialised engine
@@ -28,4 +31,8 @@ __attribute__((visibility("hidden"))) void host_batch_answered(const char *site,
 // True when the calling thread's last ether_fcs_*_host call was answered by the host CRC (the
 // queues count their own batches with it).
 __attribute__((visibility("hidden"))) bool last_call_host_answered();
+// Runs launch(ctr) with a zeroed work counter of device `dev` (the Dispenser's, dispenser.hpp)
+// leased for that launch on stream st (zeroed on st after the slot's previous kernel finished).
+__attribute__((visibility("hidden"))) int launch_with_counter(int dev, hipStream_t st,
+                                                              const std::function<int(unsigned long long *)> &launch);
 }  // namespace fcs

@@ -1549,6 +1549,16 @@ int fcs::current_device(int *dev, int *cus) {
     return 0;
 }
 
+int fcs::launch_with_counter(int dev, hipStream_t st, const std::function<int(unsigned long long *)> &launch) {
+    DevState *ds = nullptr;
+    int rc = dev_state(dev, &ds);
+    if (rc) return rc;
+    CounterLease lease;   // released (completion event recorded) after the launch
+    fcs::KParams p{};
+    if ((rc = take_counter(ds, st, p, lease))) return rc;
+    return launch(p.ctr);
+}
+
 int fcs::engine_device0(int *dev, int *cus) {
     std::vector<DevState *> devs;
     const int rc = engine_devices(&devs);

@@ -40,6 +40,7 @@ int hip_fail(hipError_t e, const char *what) {
     } while (0)
 
 std::atomic<uint64_t> g_flat_min{16384};   // see inet_csum_set_flat_threshold
+std::atomic<uint64_t> g_dma_min{16384};    // see inet_csum_set_dma_threshold
 
 int check_mode(int mode, const uint32_t *addr) {
     if (mode != INET_CSUM_IP && mode != INET_CSUM_TCP && mode != INET_CSUM_UDP)
@@ -171,7 +172,7 @@ int run_host(int mode, const uint8_t *arena, const uint64_t *off, const uint32_t
         p.addr = addr ? s.d_addr : nullptr;
         p.out = s.d_out;
         p.n = np;
-        HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), st), "launching inet_kernel");
+        HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), g_dma_min.load(std::memory_order_relaxed), st), "launching inet_kernel");
         HIPTRY(hipMemcpyAsync(s.h_out, s.d_out, np * 2, hipMemcpyDeviceToHost, st), "D2H checksums");
         HIPTRY(hipEventRecord(s.done, st), "hipEventRecord");
         s.live = true;
@@ -230,7 +231,7 @@ int inet_csum_batch_dev(int mode, const void *arena, uint64_t arena_bytes, const
     p.addr = addr;
     p.out = out;
     p.n = n;
-    HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), (hipStream_t)stream), "launching inet_kernel<var>");
+    HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), g_dma_min.load(std::memory_order_relaxed), (hipStream_t)stream), "launching inet_kernel<var>");
     return 0;
 }
 
@@ -249,7 +250,14 @@ int inet_csum_fixed_dev(int mode, const void *base, uint64_t stride, uint32_t le
     p.addr = addr;
     p.out = out;
     p.n = n;
-    HIPTRY(inet::launch_inet(false, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), (hipStream_t)stream), "launching inet_kernel<fixed>");
+    const uint64_t flat_min = g_flat_min.load(std::memory_order_relaxed), dma_min = g_dma_min.load(std::memory_order_relaxed);
+    if (inet::dma_route(false, p, dma_min))   // the LDS-DMA kernel's work counter, leased for this launch
+        return fcs::launch_with_counter(dev, (hipStream_t)stream, [&](unsigned long long *ctr) {
+            p.ctr = ctr;
+            HIPTRY(inet::launch_inet(false, mode, p, cus, flat_min, dma_min, (hipStream_t)stream), "launching inet_dma_kernel");
+            return 0;
+        });
+    HIPTRY(inet::launch_inet(false, mode, p, cus, flat_min, dma_min, (hipStream_t)stream), "launching inet_kernel<fixed>");
     return 0;
 }
 
@@ -267,6 +275,8 @@ int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, cons
 }
 
 uint64_t inet_csum_set_flat_threshold(uint64_t packets) { return g_flat_min.exchange(packets); }
+
+uint64_t inet_csum_set_dma_threshold(uint64_t packets) { return g_dma_min.exchange(packets); }
 
 uint16_t inet_ip_checksum(const void *dp, size_t bsize) {
     return single_or_die(INET_CSUM_IP, dp, bsize, 0, 0, "inet_ip_checksum");

@@ -27,6 +27,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "dispenser.hpp"
 #include "inet_launch.hpp"
 #include "wave_sync.hpp"
 
@@ -75,15 +76,20 @@ __device__ __forceinline__ uint32_t byte_mask(uint32_t keep16, int d) {
 // Pseudo-header contribution and accumulator start of each mode (exact integers, summed in the
 // little-endian word domain the reference uses).
 template <int MODE>
-__device__ __forceinline__ uint32_t pseudo(const IParams &p, uint64_t i, uint32_t len) {
+__device__ __forceinline__ uint32_t pseudo_sd(uint32_t s, uint32_t d, uint32_t len) {
     const uint32_t l16 = swap16(len & 0xffffu);   // htons(len): size_t truncated to 16 bits
     if (MODE == kIp) return 0xffffu;              // acc = 0xffff (src/ip.c:42)
-    const uint32_t s = p.addr[2 * i], d = p.addr[2 * i + 1];
     if (MODE == kTcp)                             // acc = 0xffff; {htonl(src), htonl(dst), 0, 6, htons(len)}
         return 0xffffu + swap16(s >> 16) + swap16(s & 0xffffu) + swap16(d >> 16) + swap16(d & 0xffffu) +
                0x0600u + l16;                     // (src/tcp.c:172-195)
     // udp: sum = 0; raw in_addr_t halves, htons(IPPROTO_UDP), htons(length) (src/udp.c:146,160-167)
     return (s & 0xffffu) + (s >> 16) + (d & 0xffffu) + (d >> 16) + 0x1100u + l16;
+}
+
+template <int MODE>
+__device__ __forceinline__ uint32_t pseudo(const IParams &p, uint64_t i, uint32_t len) {
+    if (MODE == kIp) return pseudo_sd<MODE>(0u, 0u, len);
+    return pseudo_sd<MODE>(p.addr[2 * i], p.addr[2 * i + 1], len);
 }
 
 // One packet's geometry.
@@ -291,8 +297,137 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
     }
 }
 
-hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, hipStream_t st) {
+// ---------------------------------------------------------------------------------------------
+// Fixed-stride batches through LDS (inet_dma_kernel): the FCS headline kernel's load form. A wave
+// item is four consecutive packets; the 16-B pieces from the first packet's start to the fourth
+// packet's end (at most 6 KiB: dma_ok) arrive in the wave's 6 KiB LDS slot by global_load_lds (six
+// 1 KiB rows, non-temporal, each only as far as the item's bytes reach: nothing past the last
+// packet is read). Quarter q of the wave sums packet q of the item from the slot (ds_read_b128 of
+// the packet's aligned pieces, lane j pieces j, j + 16, ...; edge pieces masked as in accumulate),
+// row_sum, fold, pseudo header; the next item's DMA is in flight meanwhile. Items come from the
+// work dispenser in guided chunks of consecutive items; lane 0 of each quarter stores its packet's
+// u16, four adjacent ones per item. 16 waves per CU.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDmaWaves = 16;
+constexpr uint32_t kDmaSlot = 6144;
+#ifndef INET_EDGE_AUX   // cache policy of a slot's first and last rows (measurement-only override)
+#define INET_EDGE_AUX 0
+#endif
+constexpr int kDmaRounds = 7;   // pieces per lane: a packet of at most 1532 B (dma_ok) touches <= 98 pieces
+
+template <int MODE>
+__global__ __launch_bounds__(kDmaWaves * 64, 1) void inet_dma_kernel(IParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kDmaWaves * kDmaSlot];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const uint32_t lane = threadIdx.x & 63, q = lane >> 4, j = lane & 15;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *slot = lds + wave * kDmaSlot;
+    const uint64_t n = p.n, items = (n + 3) >> 2;
+    // items from the work dispenser: guided chunks of consecutive items (as fcs_dma_kernel's; the
+    // waves of the chip run at different speeds, a static interleave ends with the slowest)
+    fcs::Dispenser D(p.ctr, items, (uint64_t)gridDim.x * kDmaWaves, (uint64_t)blockIdx.x * kDmaWaves + wave,
+                     (int)lane, 100, 4, 64);
+    constexpr uint64_t kEnd = fcs::Dispenser::kEnd;
+    // slot source of item i: the 16-B piece holding its first byte; pieces up to its last byte
+    auto src_of = [&](uint64_t i) { return (p.base + 4 * i * p.stride) & ~15ull; };
+    auto dma = [&](uint64_t i) {
+        const uint64_t a = src_of(i);
+        const uint64_t last = (4 * i + 3 < n ? 4 * i + 3 : n - 1);
+        const uint32_t need = (uint32_t)(((p.base + last * p.stride + p.flen + 15) & ~15ull) - a);
+        const uint64_t g = a + 16ull * lane;
+        const uint32_t o = 16u * lane;
+        lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
+        // the first and last rows hold the lines the neighbouring items share: default policy
+        if (o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), la, 16, 0, INET_EDGE_AUX);
+        if (1024u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), la, 16, 1024, 2);
+        if (2048u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), la, 16, 2048, 2);
+        if (3072u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g), la, 16, 3072, 2);
+        if (4096u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 4096), lb, 16, 0, 2);
+        if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(g + 4096), lb, 16, 1024, INET_EDGE_AUX);
+    };
+    // the pseudo-header addresses of a packet (lane j == 0 of its quarter), one item ahead
+    auto addr_of = [&](uint64_t i, uint32_t &s, uint32_t &d) {
+        const uint64_t f = 4 * i + q;
+        s = d = 0;
+        if (MODE != kIp && j == 0 && f < n) {
+            s = p.addr[2 * f];
+            d = p.addr[2 * f + 1];
+        }
+    };
+    uint64_t it = D.first();
+    if (it == kEnd) return;
+    dma(it);
+    uint32_t as, ad;
+    addr_of(it, as, ad);
+    while (it != kEnd) {   // wave-uniform
+        const uint64_t f = 4 * it + q;
+        const bool act = f < n;
+        const uint64_t start = p.base + f * p.stride, c0 = start & ~15ull, end = start + p.flen;
+        const uint32_t nch = act ? (uint32_t)((((end + 15) & ~15ull) - c0) >> 4) : 0u;
+        const uint32_t so = (uint32_t)(c0 - src_of(it));   // the packet's first piece in the slot
+        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot has landed
+        u32x4 v[kDmaRounds];
+#pragma unroll
+        for (int r = 0; r < kDmaRounds; r++) {
+            const uint32_t c = j + kGroup * r;
+            v[r] = c < nch ? *reinterpret_cast<const u32x4 *>(slot + so + 16u * c) : u32x4{0u, 0u, 0u, 0u};
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+        const uint32_t cs = as, cd = ad;
+        const uint64_t nx = D.next(it);
+        if (nx != kEnd) {
+            dma(nx);
+            addr_of(nx, as, ad);
+        }
+        uint64_t acc = 0;
+#pragma unroll
+        for (int r = 0; r < kDmaRounds; r++) {
+            const uint32_t c = j + kGroup * r;
+            u32x4 x = v[r];
+            if (c == 0 || c + 1 == nch) {   // edge pieces: keep bytes in [start, end)
+                const uint64_t ca = c0 + 16ull * c;
+                const uint32_t lo = start > ca ? (uint32_t)(start - ca) : 0u;
+                const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
+                const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+                x.x &= byte_mask(keep, 0);
+                x.y &= byte_mask(keep, 1);
+                x.z &= byte_mask(keep, 2);
+                x.w &= byte_mask(keep, 3);
+            }
+            acc += (uint64_t)x.x + x.y;
+            acc += (uint64_t)x.z + x.w;
+        }
+        const uint32_t s = fold64(row_sum(fold64(acc)));
+        const uint32_t m = (start & 1) ? swap16(s) : s;
+        const uint32_t ps = pseudo_sd<MODE>(cs, cd, p.flen);
+        if (j == 0 && act) p.out[f] = (uint16_t)~fold64((uint64_t)ps + m);
+        it = nx;
+    }
+}
+
+// dma_ok: fixed packets whose four-packet items fit a slot with the 16-B rounding of both ends
+// (so at most kDmaRounds * 16 pieces a packet), and that fill at least half of their stride (the
+// slot also carries the gaps between packets).
+static bool dma_ok(const IParams &p) {
+    return p.flen >= 64 && p.stride <= 2048 && 2 * (uint64_t)p.flen >= p.stride &&
+           3 * p.stride + p.flen + 30 <= kDmaSlot && p.flen + 30 <= 16u * kGroup * kDmaRounds;
+}
+
+bool dma_route(bool var, const IParams &p, uint64_t dma_min) { return !var && p.n > dma_min && dma_ok(p); }
+
+hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
+                       hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    if (dma_route(var, p, dma_min)) {
+        if (!p.ctr) return hipErrorInvalidValue;
+        const uint64_t items = (p.n + 3) / 4;
+        const uint64_t want = (items + kDmaWaves - 1) / kDmaWaves;
+        const int grid = (int)(want < (uint64_t)cus ? want : (uint64_t)cus);
+        if (mode == kTcp) hipLaunchKernelGGL((inet_dma_kernel<kTcp>), dim3(grid), dim3(kDmaWaves * 64), 0, st, p);
+        else if (mode == kUdp) hipLaunchKernelGGL((inet_dma_kernel<kUdp>), dim3(grid), dim3(kDmaWaves * 64), 0, st, p);
+        else hipLaunchKernelGGL((inet_dma_kernel<kIp>), dim3(grid), dim3(kDmaWaves * 64), 0, st, p);
+        return hipGetLastError();
+    }
     if (p.n > flat_min) {
         const uint64_t windows = (p.n + 63) / 64, per_block = kThreads / 64;
         const uint64_t want = (windows + per_block - 1) / per_block, cap = (uint64_t)cus * 8;

@@ -19,10 +19,15 @@ struct IParams {
     uint16_t *out;
     uint64_t n;
     uint32_t flen;          // fixed: packet length
+    unsigned long long *ctr;   // inet_dma_kernel: zeroed device work counter (fcs::launch_with_counter)
 };
 
-// Batches of more than flat_min packets take the flat chunk-stream kernel,
-// smaller ones one 16-lane group per packet (every packet in flight at once).
-hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, hipStream_t st);
+// Fixed-stride batches of more than dma_min packets whose four-packet items fit a 6 KiB slot take
+// the LDS-DMA kernel; otherwise batches of more than flat_min packets take the flat chunk-stream
+// kernel, smaller ones one 16-lane group per packet (every packet in flight at once).
+hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
+                       hipStream_t st);
+// True when launch_inet takes the LDS-DMA kernel: it then needs p.ctr.
+bool dma_route(bool var, const IParams &p, uint64_t dma_min);
 
 }  // namespace inet

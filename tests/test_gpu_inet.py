@@ -26,13 +26,16 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=["group", "flat"])
+@pytest.fixture(params=["group", "flat", "dma"])
 def inet_kernel(request):
-    """Run a test through both kernels (identical results required): group = one 16-lane group
-    per packet (small batches), flat = packets dealt to lanes by size."""
+    """Run a test through every kernel (identical results required): group = one 16-lane group
+    per packet (small batches), flat = packets dealt to lanes by size, dma = fixed-stride packets
+    four to a wave item through LDS (where their geometry fits its slots, else flat)."""
     old = na.inet_set_flat_threshold((1 << 63) if request.param == "group" else 0)
+    old_dma = na.inet_set_dma_threshold(0 if request.param == "dma" else (1 << 63))
     yield request.param
     na.inet_set_flat_threshold(old)
+    na.inet_set_dma_threshold(old_dma)
 
 
 def to_dev(arr: np.ndarray, dev):
@@ -104,7 +107,8 @@ def test_single_forms_match_oracle(dev, inet_oracle):
 
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("start,stride,L", [(14, 1518, 1500), (34, 1518, 1480), (14, 1518, 20),
-                                             (0, 1500, 1500), (1, 97, 61), (3, 9000, 8997), (5, 64, 0)])
+                                             (0, 1500, 1500), (1, 97, 61), (3, 9000, 8997), (5, 64, 0),
+                                             (7, 1532, 1532), (2, 120, 64), (6, 1024, 1000), (9, 2048, 1024), (1, 1519, 1517)])
 def test_fixed_dev_vs_oracle(dev, inet_oracle, mode, start, stride, L, inet_kernel):
     """Fixed-stride packets inside frames: the IP datagram at +14, the TCP segment at +34, the IP
     header alone, odd strides/starts (every alignment), jumbo, and empty packets."""
@@ -195,6 +199,28 @@ def test_large_fixed_sampled(dev, inet_oracle, oracle, inet_kernel):
     for i in idx:   # regenerate the packet's bytes on the host (counter-based generator)
         oracle.oracle_splitmix_fill(p.ctypes.data, L, 0x1E7, int(start + i * stride))
         assert got[i] == inet_oracle.oracle_tcp_checksum(int(a[2 * i]), int(a[2 * i + 1]), p.ctypes.data, L), i
+
+
+@pytest.mark.parametrize("n", [1, 3, 4, 5, 63, 64, 65, 257, 4099, 70001])
+def test_dma_partial_items_and_runs(dev, inet_oracle, inet_kernel, n):
+    """Batch sizes that leave a partial last item (n mod 4) and a partial last run of 16 items
+    (the coalesced result store), on 1518-B strides at an odd start (the IP datagram of frames
+    packed at an odd address), against the oracle for every packet."""
+    if inet_kernel != "dma":
+        pytest.skip("dma geometry")
+    start, stride, L = 15, 1518, 1500
+    rng = np.random.default_rng(n)
+    host = rng.integers(0, 256, start + (n - 1) * stride + L, dtype=np.uint8)
+    addr = rng.integers(0, 2**32, 2 * n, dtype=np.uint64).astype(np.uint32)
+    d = to_dev(host, dev)
+    d_addr = to_dev(addr.view(np.int32), dev)
+    off = start + np.arange(n, dtype=np.uint64) * stride
+    for mode in MODES:
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        na.inet_fixed_dev(mode, d.data_ptr() + start, stride, L, n, None if mode == "ip" else d_addr, out)
+        torch.cuda.synchronize()
+        exp = oracle_batch(inet_oracle, mode, host, off, np.full(n, L, np.uint32), None if mode == "ip" else addr)
+        assert np.array_equal(out.cpu().numpy().view(np.uint16), exp), mode
 
 
 def test_argument_errors(dev):
