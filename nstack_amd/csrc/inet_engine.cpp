@@ -42,6 +42,19 @@ int hip_fail(hipError_t e, const char *what) {
 std::atomic<uint64_t> g_flat_min{16384};   // see inet_csum_set_flat_threshold
 std::atomic<uint64_t> g_dma_min{16384};    // see inet_csum_set_dma_threshold
 
+// launch_inet with the work counter the LDS-DMA route takes, leased from the FCS engine's ring of
+// device `dev` for this launch.
+int launch_counted(bool var, int mode, inet::IParams &p, int dev, int cus, hipStream_t st) {
+    const uint64_t flat_min = g_flat_min.load(std::memory_order_relaxed), dma_min = g_dma_min.load(std::memory_order_relaxed);
+    auto go = [&](unsigned long long *ctr) -> int {
+        p.ctr = ctr;
+        HIPTRY(inet::launch_inet(var, mode, p, cus, flat_min, dma_min, st), "launching the inet kernel");
+        return 0;
+    };
+    if (inet::dma_route(var, p, dma_min)) return fcs::launch_with_counter(dev, st, go);
+    return go(nullptr);
+}
+
 int check_mode(int mode, const uint32_t *addr) {
     if (mode != INET_CSUM_IP && mode != INET_CSUM_TCP && mode != INET_CSUM_UDP)
         return fcs::set_error(EINVAL, "unknown checksum mode %d", mode);
@@ -172,7 +185,7 @@ int run_host(int mode, const uint8_t *arena, const uint64_t *off, const uint32_t
         p.addr = addr ? s.d_addr : nullptr;
         p.out = s.d_out;
         p.n = np;
-        HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), g_dma_min.load(std::memory_order_relaxed), st), "launching inet_kernel");
+        if ((rc = launch_counted(true, mode, p, hp->dev, cus, st))) return rc;
         HIPTRY(hipMemcpyAsync(s.h_out, s.d_out, np * 2, hipMemcpyDeviceToHost, st), "D2H checksums");
         HIPTRY(hipEventRecord(s.done, st), "hipEventRecord");
         s.live = true;
@@ -231,8 +244,7 @@ int inet_csum_batch_dev(int mode, const void *arena, uint64_t arena_bytes, const
     p.addr = addr;
     p.out = out;
     p.n = n;
-    HIPTRY(inet::launch_inet(true, mode, p, cus, g_flat_min.load(std::memory_order_relaxed), g_dma_min.load(std::memory_order_relaxed), (hipStream_t)stream), "launching inet_kernel<var>");
-    return 0;
+    return launch_counted(true, mode, p, dev, cus, (hipStream_t)stream);
 }
 
 int inet_csum_fixed_dev(int mode, const void *base, uint64_t stride, uint32_t len, uint64_t n,
@@ -250,15 +262,7 @@ int inet_csum_fixed_dev(int mode, const void *base, uint64_t stride, uint32_t le
     p.addr = addr;
     p.out = out;
     p.n = n;
-    const uint64_t flat_min = g_flat_min.load(std::memory_order_relaxed), dma_min = g_dma_min.load(std::memory_order_relaxed);
-    if (inet::dma_route(false, p, dma_min))   // the LDS-DMA kernel's work counter, leased for this launch
-        return fcs::launch_with_counter(dev, (hipStream_t)stream, [&](unsigned long long *ctr) {
-            p.ctr = ctr;
-            HIPTRY(inet::launch_inet(false, mode, p, cus, flat_min, dma_min, (hipStream_t)stream), "launching inet_dma_kernel");
-            return 0;
-        });
-    HIPTRY(inet::launch_inet(false, mode, p, cus, flat_min, dma_min, (hipStream_t)stream), "launching inet_kernel<fixed>");
-    return 0;
+    return launch_counted(false, mode, p, dev, cus, (hipStream_t)stream);
 }
 
 int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, const uint64_t *off,

@@ -27,7 +27,8 @@ struct IParams {
 // kernel, smaller ones one 16-lane group per packet (every packet in flight at once).
 hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
                        hipStream_t st);
-// True when launch_inet takes the LDS-DMA kernel: it then needs p.ctr.
+// True when launch_inet takes the LDS-DMA kernel: it then needs p.ctr (the flat kernel keeps a
+// static interleave of its windows: guided chunks measured 4 % slower on IMIX, 17 % on 20-B headers).
 bool dma_route(bool var, const IParams &p, uint64_t dma_min);
 
 }  // namespace inet
