@@ -62,10 +62,11 @@ int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, cons
  * Results are identical either way. Default 16384. Returns the previous value. */
 uint64_t inet_csum_set_flat_threshold(uint64_t packets);
 
-/* Tuning: fixed-stride batches (inet_csum_fixed_dev) of more than `packets` packets whose packets
- * fill at least half their stride (64..1550 B, stride <= 2048) stream through LDS by DMA, four
- * packets per wave item. Results are identical either way. Default 16384. Returns the previous
- * value. */
+/* Tuning: batches of more than `packets` packets stream through LDS by DMA: fixed strides
+ * (inet_csum_fixed_dev) four packets per wave item when the packets fill at least half their
+ * stride (64..1532 B, stride <= 2048); variable batches in windows of 64 packets, each window whose
+ * packets are packed and at least 16 B long as one span (the others by the flat kernel's method).
+ * Results are identical either way. Default 16384. Returns the previous value. */
 uint64_t inet_csum_set_dma_threshold(uint64_t packets);
 
 /* ---- single packet, same arguments and result as the reference functions ---- */

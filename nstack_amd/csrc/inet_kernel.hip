@@ -202,98 +202,321 @@ __global__ __launch_bounds__(kThreads) void inet_kernel(IParams p) {
 // ---------------------------------------------------------------------------------------------
 constexpr int kUnit = 6;   // 16-byte chunks per lane unit
 
+// One window of 64 packets from w0 by the flat chunk stream (acc, mark: this wave's zeroed LDS
+// arrays, left zeroed; list: its scratch).
+template <bool VAR, int MODE>
+__device__ __forceinline__ void flat_window(const IParams &p, uint64_t w0, int lane, unsigned long long *acc,
+                                            uint8_t *mark, uint8_t *list) {
+    const uint64_t i = w0 + lane;
+    const bool act = i < p.n;
+    const uint32_t len = act ? (VAR ? p.len[i] : p.flen) : 0u;
+    const uint64_t start = act ? p.base + (VAR ? p.off[i] : i * p.stride) : 0ull;
+    const uint64_t c0 = start & ~15ull;
+    const uint32_t nch = len ? (uint32_t)((((start + len + 15) & ~15ull) - c0) >> 4) : 0u;
+    const uint32_t k = (nch + kUnit - 1) / kUnit;
+    uint32_t incl = k;   // inclusive prefix over the window
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
+        if (lane >= d) incl += y;
+    }
+    const uint32_t P = incl - k;
+    const uint32_t K = (uint32_t)__shfl((int)incl, 63);
+    const uint64_t fmask = __ballot(k != 0);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
+    if (k) list[rank] = (uint8_t)lane;
+    wave_lds_sync();
+    const uint32_t c0lo = (uint32_t)c0, c0hi = (uint32_t)(c0 >> 32);
+    const uint32_t edges = (uint32_t)(start & 15) | ((uint32_t)((start + len) & 15) << 8);
+
+    for (uint32_t g0 = 0; g0 < K; g0 += 64) {
+        // a long packet spans any number of items, so marks are cleared after use (not tagged)
+        const bool starts = k && P >= g0 && P < g0 + 64;
+        if (starts) mark[P - g0] = 1;
+        wave_lds_sync();
+        const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
+        const uint64_t M = __ballot(mark[lane] != 0);
+        wave_lds_sync();
+        if (starts) mark[P - g0] = 0;
+        const uint32_t g = g0 + (uint32_t)lane;
+        const bool valid = g < K;
+        const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
+        const int src = valid ? (int)list[rk & 63u] : 0;
+        const uint64_t cb = ((uint64_t)(uint32_t)__shfl((int)c0hi, src) << 32) | (uint32_t)__shfl((int)c0lo, src);
+        const uint32_t nc = (uint32_t)__shfl((int)nch, src);
+        const uint32_t Pg = (uint32_t)__shfl((int)P, src);
+        const uint32_t eg = (uint32_t)__shfl((int)edges, src);
+        // unit u of a k-unit packet holds chunks u, u + k, ..., u + 5k: load q of the packet's k
+        // lanes reads k consecutive chunks (coalesced), the sum does not care about the order
+        const uint32_t u = g - Pg, kg = (nc + kUnit - 1) / kUnit;
+        if (valid) {
+            u32x4 v[kUnit];
+#pragma unroll
+            for (int q = 0; q < kUnit; q++) {
+                const uint32_t c = u + q * kg;
+                v[q] = gload<u32x4>(cb + 16ull * (c < nc ? c : nc - 1));   // past the end: a cache hit, zeroed below
+            }
+            uint64_t s = 0;
+#pragma unroll
+            for (int q = 0; q < kUnit; q++) {
+                const uint32_t c = u + q * kg;
+                if (c >= nc) continue;
+                u32x4 w = v[q];
+                if (c == 0 || c + 1 == nc) {   // the packet's edge chunks: keep bytes in [start, end)
+                    const uint32_t lo = c == 0 ? (eg & 0xffu) : 0u;
+                    const uint32_t e15 = (eg >> 8) & 0xffu;
+                    const uint32_t hi = (c + 1 == nc && e15) ? e15 : 16u;
+                    const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+                    w.x &= byte_mask(keep, 0);
+                    w.y &= byte_mask(keep, 1);
+                    w.z &= byte_mask(keep, 2);
+                    w.w &= byte_mask(keep, 3);
+                }
+                s += (uint64_t)w.x + w.y;
+                s += (uint64_t)w.z + w.w;
+            }
+            const uint32_t f = fold64(s);   // 0 only for an all-zero unit
+            if (f) atomicAdd(&acc[src], (unsigned long long)f);
+        }
+    }
+
+    // ---- packet i: fold, odd-start swap, pseudo header and init, complement; clear state ----
+    wave_lds_sync();
+    const uint32_t m0 = fold64(acc[lane]);
+    const uint32_t m = (start & 1) ? swap16(m0) : m0;   // odd start: P = swap16(fold(M))
+    if (act) p.out[i] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, i, len) + m);
+    acc[lane] = 0ull;
+    mark[lane] = 0;
+}
+
 template <bool VAR, int MODE>
 __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
     __shared__ unsigned long long acc_s[kThreads / 64][64];
     __shared__ uint8_t mark_s[kThreads / 64][64];
     __shared__ uint8_t list_s[kThreads / 64][64];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    unsigned long long *acc = acc_s[wave];
-    uint8_t *mark = mark_s[wave], *list = list_s[wave];
-    acc[lane] = 0ull;
-    mark[lane] = 0;
+    acc_s[wave][lane] = 0ull;
+    mark_s[wave][lane] = 0;
     const uint64_t GW = (uint64_t)gridDim.x * (kThreads / 64);
-    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64) {
-        const uint64_t i = w0 + lane;
-        const bool act = i < p.n;
-        const uint32_t len = act ? (VAR ? p.len[i] : p.flen) : 0u;
-        const uint64_t start = act ? p.base + (VAR ? p.off[i] : i * p.stride) : 0ull;
-        const uint64_t c0 = start & ~15ull;
-        const uint32_t nch = len ? (uint32_t)((((start + len + 15) & ~15ull) - c0) >> 4) : 0u;
-        const uint32_t k = (nch + kUnit - 1) / kUnit;
-        uint32_t incl = k;   // inclusive prefix over the window
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, d);
-            if (lane >= d) incl += y;
-        }
-        const uint32_t P = incl - k;
-        const uint32_t K = (uint32_t)__shfl((int)incl, 63);
-        const uint64_t fmask = __ballot(k != 0);
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(fmask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)fmask, 0u));
-        if (k) list[rank] = (uint8_t)lane;
-        wave_lds_sync();
-        const uint32_t c0lo = (uint32_t)c0, c0hi = (uint32_t)(c0 >> 32);
-        const uint32_t edges = (uint32_t)(start & 15) | ((uint32_t)((start + len) & 15) << 8);
+    for (uint64_t w0 = ((uint64_t)blockIdx.x * (kThreads / 64) + wave) * 64; w0 < p.n; w0 += GW * 64)
+        flat_window<VAR, MODE>(p, w0, lane, acc_s[wave], mark_s[wave], list_s[wave]);
+}
 
-        for (uint32_t g0 = 0; g0 < K; g0 += 64) {
-            // a long packet spans any number of items, so marks are cleared after use (not tagged)
-            const bool starts = k && P >= g0 && P < g0 + 64;
-            if (starts) mark[P - g0] = 1;
-            wave_lds_sync();
-            const uint32_t before = (uint32_t)__popcll(__ballot(k && P < g0));
-            const uint64_t M = __ballot(mark[lane] != 0);
-            wave_lds_sync();
-            if (starts) mark[P - g0] = 0;
-            const uint32_t g = g0 + (uint32_t)lane;
-            const bool valid = g < K;
-            const uint32_t rk = before + (uint32_t)__popcll(M & ((2ull << lane) - 1ull)) - 1u;
-            const int src = valid ? (int)list[rk & 63u] : 0;
-            const uint64_t cb = ((uint64_t)(uint32_t)__shfl((int)c0hi, src) << 32) | (uint32_t)__shfl((int)c0lo, src);
-            const uint32_t nc = (uint32_t)__shfl((int)nch, src);
-            const uint32_t Pg = (uint32_t)__shfl((int)P, src);
-            const uint32_t eg = (uint32_t)__shfl((int)edges, src);
-            // unit u of a k-unit packet holds chunks u, u + k, ..., u + 5k: load q of the packet's k
-            // lanes reads k consecutive chunks (coalesced), the sum does not care about the order
-            const uint32_t u = g - Pg, kg = (nc + kUnit - 1) / kUnit;
-            if (valid) {
-                u32x4 v[kUnit];
+// ---------------------------------------------------------------------------------------------
+// Variable-length batches through LDS (inet_stream_kernel): a wave owns windows of 64 consecutive
+// packets (interleaved over the grid). A window whose packets are packed (each starts where the
+// previous one ends) and at least 16 B long is one contiguous span: it arrives in 6 KiB items by
+// LDS-DMA into the wave's slot (rows only as far as the span reaches, the first and last at the
+// default cache policy), and lane l sums the item's bytes [96 l, 96 l + 96) piece by piece into the
+// packet they belong to (the window's packet starts in LDS; a 16-B piece holds at most one packet
+// boundary): even- and odd-addressed bytes by v_dot4_u32_u8 running sums (the word sum is E + 256 O,
+// the same residue as the dword sums), split at a boundary by the running sum before its dword
+// plus that dword's bytes below it; each packet's part goes into its LDS accumulator once per lane
+// (ds_add_u64). The
+// next item's DMA (or the next packed window's first) is in flight while the current one is
+// summed. Lane l finishes packet l (fold, odd-start swap, pseudo header). Other windows take the
+// flat chunk stream (flat_window) inside the same kernel. 16 waves per CU.
+// ---------------------------------------------------------------------------------------------
+constexpr int kStWaves = 16;
+constexpr uint32_t kStSlot = 6144;
+constexpr uint32_t kStLane = kStSlot / 64;   // 96 bytes of an item per lane
+static_assert(kStLane % 16 == 0, "whole pieces per lane");
+
+template <int MODE>
+__global__ __launch_bounds__(kStWaves * 64, 1) void inet_stream_kernel(IParams p) {
+    __shared__ __attribute__((aligned(16))) uint8_t slots[kStWaves * kStSlot];
+    __shared__ unsigned long long acc_s[kStWaves][64];
+    __shared__ uint32_t start_s[kStWaves][64];
+    __shared__ uint8_t mark_s[kStWaves][64], list_s[kStWaves][64];
+    typedef __attribute__((address_space(3))) void lds_void;
+    const int lane = threadIdx.x & 63;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint8_t *slot = slots + wave * kStSlot;
+    unsigned long long *acc = acc_s[wave];
+    uint32_t *st = start_s[wave];
+    acc[lane] = 0ull;
+    mark_s[wave][lane] = 0;
+    const uint64_t n = p.n, nwin = (n + 63) >> 6, W = (uint64_t)gridDim.x * kStWaves;
+
+    // A window's metadata (lane l: packet w0 + l) and, once it has arrived, its geometry.
+    struct Meta {
+        uint64_t off;
+        uint32_t len;
+    };
+    struct Geo {
+        bool packed;
+        uint64_t a0;      // the span's first 16-B piece (byte address)
+        uint32_t total;   // span bytes from a0 to its last byte (exclusive)
+        uint32_t items;
+    };
+    auto meta = [&](uint64_t wi) -> Meta {
+        const uint64_t i = wi * 64 + (uint64_t)lane;
+        Meta m{0ull, 0u};
+        if (wi < nwin && i < n) {
+            m.off = p.off[i];
+            m.len = p.len[i];
+        }
+        return m;
+    };
+    auto geo = [&](uint64_t wi, const Meta &m) -> Geo {
+        Geo g{false, 0ull, 0u, 0u};
+        if (wi >= nwin) return g;
+        const bool act = wi * 64 + (uint64_t)lane < n;
+        const uint64_t end = m.off + m.len;
+        const uint64_t pend = ((uint64_t)(uint32_t)__shfl_up((int)(uint32_t)(end >> 32), 1) << 32) |
+                              (uint32_t)__shfl_up((int)(uint32_t)end, 1);
+        const bool ok = !act || (m.len >= 16 && (lane == 0 || m.off == pend));
+        if (__ballot(!ok) != 0ull) return g;
+        const uint64_t am = __ballot(act);
+        const int last = 63 - __builtin_clzll(am);
+        const uint64_t s0 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(m.off >> 32), 0) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)m.off, 0);
+        const uint64_t e1 = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(end >> 32), last) << 32) |
+                            (uint32_t)__shfl((int)(uint32_t)end, last);
+        const uint64_t a0 = (p.base + s0) & ~15ull, tot = p.base + e1 - a0;
+        if (tot >= (1ull << 31)) return g;
+        g.packed = true;
+        g.a0 = a0;
+        g.total = (uint32_t)tot;
+        g.items = (uint32_t)((tot + kStSlot - 1) / kStSlot);
+        return g;
+    };
+    // item k of a packed window: pieces from a0 + k kStSlot up to the span's last byte's piece
+    auto dma = [&](const Geo &g, uint32_t k) {
+        const uint32_t base = k * kStSlot;
+        const uint32_t span16 = (g.total + 15u) & ~15u;
+        const uint32_t need = span16 - base < kStSlot ? span16 - base : kStSlot;
+        const uint64_t a = g.a0 + base + 16ull * (uint32_t)lane;
+        const uint32_t o = 16u * (uint32_t)lane;
+        lds_void *la = (lds_void *)slot, *lb = (lds_void *)(slot + 4096);
+        if (o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 0, 0);
+        if (1024u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 1024, 2);
+        if (2048u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 2048, 2);
+        if (3072u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a), la, 16, 3072, 2);
+        if (4096u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a + 4096), lb, 16, 0, 2);
+        if (5120u + o < need) __builtin_amdgcn_global_load_lds(reinterpret_cast<const void *>(a + 4096), lb, 16, 1024, 0);
+    };
+
+    uint64_t wi = (uint64_t)blockIdx.x * kStWaves + wave;
+    Meta cm = meta(wi);
+    Geo cg = geo(wi, cm);
+    if (cg.packed) dma(cg, 0);   // the first window's first item
+    while (wi < nwin) {          // wave-uniform
+        const uint64_t wn = wi + W;
+        const Meta nm = meta(wn);   // in flight while the current window is summed
+        const uint64_t w0 = wi * 64;
+        if (!cg.packed) {
+            flat_window<true, MODE>(p, w0, lane, acc, mark_s[wave], list_s[wave]);
+            const Geo ng = geo(wn, nm);
+            if (ng.packed) dma(ng, 0);
+            wi = wn;
+            cm = nm;
+            cg = ng;
+            continue;
+        }
+        const bool act = w0 + (uint64_t)lane < n;
+        const uint32_t my = act ? (uint32_t)(p.base + cm.off - cg.a0) : cg.total;   // packet start in the span
+        st[lane] = my;
+        wave_lds_sync();
+        const uint32_t st0 = st[0];
+        Geo ng{false, 0ull, 0u, 0u};
+        for (uint32_t k = 0; k < cg.items; k++) {
+            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): this wave's slot has landed
+            u32x4 v[kStLane / 16];
 #pragma unroll
-                for (int q = 0; q < kUnit; q++) {
-                    const uint32_t c = u + q * kg;
-                    v[q] = gload<u32x4>(cb + 16ull * (c < nc ? c : nc - 1));   // past the end: a cache hit, zeroed below
-                }
-                uint64_t s = 0;
+            for (int q = 0; q < (int)(kStLane / 16); q++)
+                v[q] = *reinterpret_cast<const u32x4 *>(slot + kStLane * (uint32_t)lane + 16u * (uint32_t)q);
+            __builtin_amdgcn_s_waitcnt(0xC07F);   // lgkmcnt(0): the slot is free for the next DMA
+            if (k + 1 < cg.items) {
+                dma(cg, k + 1);
+            } else {   // the next window's metadata has landed with this item: its first item now
+                ng = geo(wn, nm);
+                if (ng.packed) dma(ng, 0);
+            }
+            // ---- this lane's 96 bytes: positions [P0, P0 + 96) of the span ----
+            const uint32_t P0 = k * kStSlot + kStLane * (uint32_t)lane;
+#ifdef INET_ST_NOSUM   // measurement-only: the pieces XORed into the lane's own packet (wrong sums)
+            if (P0 < cg.total) {
+                uint32_t xx = 0;
 #pragma unroll
-                for (int q = 0; q < kUnit; q++) {
-                    const uint32_t c = u + q * kg;
-                    if (c >= nc) continue;
-                    u32x4 w = v[q];
-                    if (c == 0 || c + 1 == nc) {   // the packet's edge chunks: keep bytes in [start, end)
-                        const uint32_t lo = c == 0 ? (eg & 0xffu) : 0u;
-                        const uint32_t e15 = (eg >> 8) & 0xffu;
-                        const uint32_t hi = (c + 1 == nc && e15) ? e15 : 16u;
+                for (int q = 0; q < (int)(kStLane / 16); q++) xx ^= v[q].x ^ v[q].y ^ v[q].z ^ v[q].w;
+                atomicAdd(&acc[lane], (unsigned long long)xx);
+            }
+            if (false) {
+#else
+            if (P0 < cg.total) {
+#endif
+                int cur = 0;   // the packet holding P0 (or the first one, before st0)
+#pragma unroll
+                for (int b = 32; b >= 1; b >>= 1)
+                    if (st[cur + b] <= P0) cur += b;
+                uint32_t nxt = cur + 1 < 64 ? st[cur + 1] : cg.total;
+                // the current packet's part: even- and odd-addressed bytes (sum = E + 256 O)
+                uint32_t E = 0, O = 0;
+                auto flush = [&]() {
+                    const uint32_t part = E + (O << 8);
+                    if (part) atomicAdd(&acc[cur], (unsigned long long)part);
+                    E = O = 0;
+                    cur++;
+                    nxt = cur + 1 < 64 ? st[cur + 1] : cg.total;
+                };
+#pragma unroll
+                for (int q = 0; q < (int)(kStLane / 16); q++) {
+                    const uint32_t Pq = P0 + 16u * (uint32_t)q;
+                    if (Pq >= cg.total) break;
+                    u32x4 x = v[q];
+                    if (Pq < st0 || cg.total - Pq < 16u) {   // the span's first or last piece
+                        const uint32_t lo = Pq < st0 ? st0 - Pq : 0u;
+                        const uint32_t hi = cg.total - Pq < 16u ? cg.total - Pq : 16u;
                         const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-                        w.x &= byte_mask(keep, 0);
-                        w.y &= byte_mask(keep, 1);
-                        w.z &= byte_mask(keep, 2);
-                        w.w &= byte_mask(keep, 3);
+                        x.x &= byte_mask(keep, 0);
+                        x.y &= byte_mask(keep, 1);
+                        x.z &= byte_mask(keep, 2);
+                        x.w &= byte_mask(keep, 3);
                     }
-                    s += (uint64_t)w.x + w.y;
-                    s += (uint64_t)w.z + w.w;
+                    if (nxt <= Pq) flush();   // a packet starts exactly at this piece
+                    // running sums over the piece's dwords
+                    const uint32_t e0 = __builtin_amdgcn_udot4(x.x, 0x00010001u, 0u, false);
+                    const uint32_t o0 = __builtin_amdgcn_udot4(x.x, 0x01000100u, 0u, false);
+                    const uint32_t e1 = __builtin_amdgcn_udot4(x.y, 0x00010001u, e0, false);
+                    const uint32_t o1 = __builtin_amdgcn_udot4(x.y, 0x01000100u, o0, false);
+                    const uint32_t e2 = __builtin_amdgcn_udot4(x.z, 0x00010001u, e1, false);
+                    const uint32_t o2 = __builtin_amdgcn_udot4(x.z, 0x01000100u, o1, false);
+                    const uint32_t e3 = __builtin_amdgcn_udot4(x.w, 0x00010001u, e2, false);
+                    const uint32_t o3 = __builtin_amdgcn_udot4(x.w, 0x01000100u, o2, false);
+                    const uint32_t b = nxt - Pq;
+                    if (b < 16u) {   // the next packet starts inside the piece, in dword b / 4 at byte b % 4
+                        const uint32_t db = b >> 2, lm = (1u << (8u * (b & 3u))) - 1u;
+                        uint32_t eb = db == 0 ? 0u : (db == 1 ? e0 : (db == 2 ? e1 : e2));
+                        uint32_t ob = db == 0 ? 0u : (db == 1 ? o0 : (db == 2 ? o1 : o2));
+                        const uint32_t xd = db == 0 ? x.x : (db == 1 ? x.y : (db == 2 ? x.z : x.w));
+                        eb = __builtin_amdgcn_udot4(xd, 0x00010001u & lm, eb, false);
+                        ob = __builtin_amdgcn_udot4(xd, 0x01000100u & lm, ob, false);
+                        E += eb;
+                        O += ob;
+                        flush();
+                        E = e3 - eb;
+                        O = o3 - ob;
+                    } else {
+                        E += e3;
+                        O += o3;
+                    }
                 }
-                const uint32_t f = fold64(s);   // 0 only for an all-zero unit
-                if (f) atomicAdd(&acc[src], (unsigned long long)f);
+                const uint32_t part = E + (O << 8);
+                if (part) atomicAdd(&acc[cur], (unsigned long long)part);
             }
         }
-
-        // ---- packet i: fold, odd-start swap, pseudo header and init, complement; clear state ----
+        // ---- packet w0 + lane: fold, odd-start swap, pseudo header and init, complement ----
         wave_lds_sync();
-        const uint32_t m0 = fold64(acc[lane]);
-        const uint32_t m = (start & 1) ? swap16(m0) : m0;   // odd start: P = swap16(fold(M))
-        if (act) p.out[i] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, i, len) + m);
+        if (act) {
+            const uint32_t m0 = fold64(acc[lane]);
+            const uint32_t m = ((p.base + cm.off) & 1) ? swap16(m0) : m0;   // odd start: P = swap16(fold(M))
+            p.out[w0 + lane] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, w0 + lane, cm.len) + m);
+        }
         acc[lane] = 0ull;
-        mark[lane] = 0;
+        wi = wn;
+        cm = nm;
+        cg = ng;
     }
 }
 
@@ -413,11 +636,20 @@ static bool dma_ok(const IParams &p) {
            3 * p.stride + p.flen + 30 <= kDmaSlot && p.flen + 30 <= 16u * kGroup * kDmaRounds;
 }
 
-bool dma_route(bool var, const IParams &p, uint64_t dma_min) { return !var && p.n > dma_min && dma_ok(p); }
+bool dma_route(bool var, const IParams &p, uint64_t dma_min) { return p.n > dma_min && (var || dma_ok(p)); }
 
 hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
                        hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
+    if (var && dma_route(var, p, dma_min)) {
+        const uint64_t nwin = (p.n + 63) / 64;
+        const uint64_t want = (nwin + kStWaves - 1) / kStWaves;
+        const int grid = (int)(want < (uint64_t)cus ? want : (uint64_t)cus);
+        if (mode == kTcp) hipLaunchKernelGGL((inet_stream_kernel<kTcp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
+        else if (mode == kUdp) hipLaunchKernelGGL((inet_stream_kernel<kUdp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
+        else hipLaunchKernelGGL((inet_stream_kernel<kIp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
+        return hipGetLastError();
+    }
     if (dma_route(var, p, dma_min)) {
         if (!p.ctr) return hipErrorInvalidValue;
         const uint64_t items = (p.n + 3) / 4;

@@ -27,8 +27,9 @@ struct IParams {
 // kernel, smaller ones one 16-lane group per packet (every packet in flight at once).
 hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
                        hipStream_t st);
-// True when launch_inet takes the LDS-DMA kernel: it then needs p.ctr (the flat kernel keeps a
-// static interleave of its windows: guided chunks measured 4 % slower on IMIX, 17 % on 20-B headers).
+// True when launch_inet takes an LDS-DMA kernel: fixed strides inet_dma_kernel (which needs p.ctr),
+// variable batches inet_stream_kernel (windows interleaved statically, like the flat kernel's:
+// guided chunks measured 4 % slower there on IMIX, 17 % on 20-B headers).
 bool dma_route(bool var, const IParams &p, uint64_t dma_min);
 
 }  // namespace inet

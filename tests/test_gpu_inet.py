@@ -142,6 +142,30 @@ def test_random_var_vs_oracle(dev, inet_oracle, mode, inet_kernel):
     assert np.array_equal(got, oracle_batch(inet_oracle, mode, arena, off, ln, a))
 
 
+@pytest.mark.parametrize("mode", MODES)
+@pytest.mark.parametrize("lead", [0, 1, 3])
+def test_packed_var_windows(dev, inet_oracle, mode, lead, inet_kernel):
+    """Packed variable batches (each packet starts where the previous ends), as the LDS stream takes
+    them window by window (64 packets): IMIX lengths, 16-B packets, long ones spanning several 6 KiB
+    items, and windows the stream hands to its flat path (a gap, an overlap, a packet under 16 B, an
+    empty one), at every base alignment."""
+    rng = np.random.default_rng(100 + lead + 7 * len(mode))
+    n = 64 * 60 + 17
+    ln = rng.choice([16, 17, 63, 64, 65, 576, 1500, 1518], n).astype(np.int64)
+    ln[64 * 5:64 * 6] = rng.integers(3000, 9000, 64)      # a window of long packets (many items)
+    ln[64 * 7 + 9] = 15                                     # a short packet: flat window
+    ln[64 * 9 + 40] = 0                                     # an empty packet: flat window
+    off = lead + np.concatenate([[0], np.cumsum(ln)[:-1]])
+    off[64 * 11 + 3:] += 5                                  # a gap: flat window
+    off[64 * 13 + 50] -= 8                                  # an overlap: flat window
+    arena = rng.integers(0, 256, int(off[-1] + ln[-1]) + 64, dtype=np.uint8)
+    arena[int(off[64 * 15]):int(off[64 * 15]) + 2000] = 0  # all-zero packets
+    addr = rng.integers(0, 2**32, 2 * n, dtype=np.uint64).astype(np.uint32)
+    a = None if mode == "ip" else addr
+    got = run_batch_dev(dev, mode, arena, off.astype(np.uint64), ln.astype(np.uint32), a)
+    assert np.array_equal(got, oracle_batch(inet_oracle, mode, arena, off, ln, a))
+
+
 def test_quirks(dev, inet_oracle, inet_kernel):
     """nstack-specific results: all-zero data (acc = 0xffff start), sums that are a nonzero
     multiple of 0xffff, the htons(len) truncation above 64 KiB, and headers that verify to 0."""

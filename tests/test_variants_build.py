@@ -55,7 +55,7 @@ VARIANTS = [
     ("fcs_kernel.hip", "-DFCS_ST_EDGE_AUX=0"),
     ("fcs_kernel.hip", "-DFCS_SEGW_FORCE=26"),
     ("fcs_kernel.hip", "-DFCS_SEG_ITEM_WORDS=6"),
-    ("inet_kernel.hip", "-DINET_EDGE_AUX=2"),
+    ("inet_kernel.hip", "-DINET_EDGE_AUX=2 -DINET_ST_NOSUM"),
     ("fcs_engine.cpp", "-DFCS_FAULT_HOOK -DFCS_GRID_CUS=128 -DFCS_FLAT_DYN_MIN=1000 -DFCS_FIXED_DYN_MIN=8 "
                        "-DFCS_FIXED_FLAT_MAX=0 -DFCS_ZC_MAX_MB=16 -DFCS_NO_STREAM"),
     ("fcs_engine.cpp", "-DFCS_STAMPS -DFCS_HOST_TRACE -DFCS_PIPE_DEPTH=3"),
