@@ -58,7 +58,8 @@ int inet_csum_batch_host(int mode, const void *arena, uint64_t arena_bytes, cons
                          const uint32_t *len, const uint32_t *addr, uint16_t *out, uint64_t n);
 
 /* Tuning: batches of more than `packets` packets use the flat kernel (packets dealt to lanes by
- * size, for throughput), smaller ones one 16-lane group per packet (latency).
+ * size, for throughput), smaller ones one 16-lane group per packet (latency); batches above the
+ * DMA threshold (inet_csum_set_dma_threshold) take the LDS-DMA kernels instead.
  * Results are identical either way. Default 16384. Returns the previous value. */
 uint64_t inet_csum_set_flat_threshold(uint64_t packets);
 
