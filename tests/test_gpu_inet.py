@@ -226,12 +226,18 @@ def test_large_fixed_sampled(dev, inet_oracle, oracle, inet_kernel):
 
 
 @pytest.mark.parametrize("n", [1, 3, 4, 5, 63, 64, 65, 257, 4099, 70001])
-def test_dma_partial_items_and_runs(dev, inet_oracle, inet_kernel, n):
-    """Batch sizes that leave a partial last item (n mod 4) and a partial last run of 16 items
-    (the coalesced result store), on 1518-B strides at an odd start (the IP datagram of frames
-    packed at an odd address), against the oracle for every packet."""
-    if inet_kernel != "dma":
-        pytest.skip("dma geometry")
+def test_dma_partial_items(dev, inet_oracle, n):
+    """The fixed-stride LDS-DMA kernel at batch sizes that leave a partial last item (n mod 4) and
+    uneven dynamic chunks, on 1518-B strides at an odd start (the IP datagram of frames packed at an
+    odd address), against the oracle for every packet."""
+    old = na.inet_set_dma_threshold(0)
+    try:
+        _dma_partial_items(dev, inet_oracle, n)
+    finally:
+        na.inet_set_dma_threshold(old)
+
+
+def _dma_partial_items(dev, inet_oracle, n):
     start, stride, L = 15, 1518, 1500
     rng = np.random.default_rng(n)
     host = rng.integers(0, 256, start + (n - 1) * stride + L, dtype=np.uint8)
