@@ -1635,7 +1635,7 @@ const char *fcs_engine_version(void) {
     return "nstack-fcs 0.6 gfx950: quarter-wave/frame, 96B lane windows as 2 slice-by-4 chains, v_perm "
            "addressing, DPP reduce; 1496-1524B: LDS-DMA (nt global_load_lds) 6KiB slot/wave, 16 waves/CU, "
            "32KiB 8-replica tables, guided dynamic items; 130-399B: 4 lanes x 36-104B, 400-868B: 8 lanes x 44-112B windows/frame, 870-1476B: 16 lanes x 60-96B windows, 6-7KiB LDS-DMA slots; <=128B: lane/frame; 1477-1495B, 1525-1988B: 104/120/128B-window LDS-DMA, 7/8KiB slots; "
-           ">1524B otherwise: frame-interleaved LDS-DMA segments of 1524/1604/1860/1988B (least m*(WD+8)); var: "
+           ">1524B otherwise: frame-interleaved LDS-DMA segments of 900-1988B (least m*(WD+8)); var: "
            "packed 64-1536B units as an arena stream (4KiB LDS-DMA items, taps at frame boundaries, XOR "
            "scan), other units as a flat chunk stream per 64-frame window";
 }

@@ -1555,8 +1555,8 @@ __global__ __launch_bounds__(kSegilThreads, 1) void fcs_segil_kernel(KParams p) 
 }
 
 // ---------------------------------------------------------------------------------------------
-// Fixed length over 1524 B in segments of the wide kernel's cover (fcs_segw_kernel<WD>, WD 26 / 30;
-// host-selected by segment_wd()). fcs_segil_kernel's schedule (units of four frames, item r =
+// Fixed length over 1524 B in segments of the wide kernel's cover (fcs_segw_kernel<WD>, WD 15..23,
+// 26, 30, 32; host-selected by segment_wd()). fcs_segil_kernel's schedule (units of four frames, item r =
 // segment r of the four, four DMA runs into 2 KiB parts of an 8 KiB slot, 12 waves) with
 // fcs_wide_kernel<WD>'s lane windows (4 WD bytes every 4 WD - 4): C = wide_cover(WD) bytes per
 // segment (1604 / 1860 B), so a frame takes ceil(L / C) items where fcs_segil_kernel takes
@@ -2999,9 +2999,11 @@ hipError_t launch_fixed_route(const FixedRoute &r, const KParams &p, int grid, h
     case FixedKernel::kSegment:
         switch (r.wd) {
             case 24: FCS_GO(FixedKernel::kSegment, 24, kSegilThreads, false, fcs_segil_kernel); break;
-            case 26: FCS_GO(FixedKernel::kSegment, 26, kSegilThreads, false, fcs_segw_kernel<26>); break;
-            case 30: FCS_GO(FixedKernel::kSegment, 30, kSegilThreads, false, fcs_segw_kernel<30>); break;
-            case 32: FCS_GO(FixedKernel::kSegment, 32, kSegilThreads, false, fcs_segw_kernel<32>); break;
+#define FCS_SEGW(W) \
+    case W: FCS_GO(FixedKernel::kSegment, W, kSegilThreads, false, fcs_segw_kernel<W>); break;
+            FCS_SEGW(15) FCS_SEGW(16) FCS_SEGW(18) FCS_SEGW(19) FCS_SEGW(20) FCS_SEGW(22) FCS_SEGW(23)
+            FCS_SEGW(26) FCS_SEGW(30) FCS_SEGW(32)
+#undef FCS_SEGW
             default: return hipErrorInvalidValue;
         }
         break;

@@ -172,10 +172,11 @@ inline bool fixed_segil(const KParams &p) {
     return p.flen >= kSegilMinLen2;
 #endif
 }
-// Segment width for a batch fixed_segil() takes: 24 (fcs_segil_kernel, 1524-B segments) or 26 / 30 /
-// 32 (fcs_segw_kernel<WD>, segments of wide_cover(WD) = 1604 / 1860 / 1988 B): the least per-lane
-// work per frame, m (WD + kSegItemWords) for m = ceil(len / cover) items of WD words each plus a
-// fixed per-item cost in word equivalents (merge, lane shift, row XOR, waits, four run issues).
+// Segment width for a batch fixed_segil() takes: 24 (fcs_segil_kernel, 1524-B segments) or another
+// width with lane tables (fcs_segw_kernel<WD>, segments of wide_cover(WD): 15..23 for 900..1412 B,
+// 26 / 30 / 32 for 1604 / 1860 / 1988 B): the least per-lane work per frame, m (WD + kSegItemWords)
+// for m = ceil(len / cover) items of WD words each plus a fixed per-item cost in word equivalents
+// (merge, lane shift, row XOR, waits, four run issues); ties keep the earlier candidate.
 #ifndef FCS_SEG_ITEM_WORDS   // measurement-only override of the per-item cost
 #define FCS_SEG_ITEM_WORDS 8
 #endif
@@ -186,8 +187,9 @@ __host__ __device__ constexpr int segment_wd(uint32_t len) {
 #else
     int best = 24;
     uint64_t cost = (uint64_t)((len + kDmaCover - 1) / kDmaCover) * (24u + kSegItemWords);
-    const int wds[3] = {26, 30, 32};
-    for (int i = 0; i < 3; i++) {
+    // the bank-safe widths with lane tables (wide_mid_ok: 15..23), then the wide kernel's three
+    const int wds[10] = {15, 16, 18, 19, 20, 22, 23, 26, 30, 32};
+    for (int i = 0; i < 10; i++) {
         const uint64_t m = (len + wide_cover(wds[i]) - 1) / wide_cover(wds[i]);
         if (m * ((uint64_t)wds[i] + kSegItemWords) < cost) {
             cost = m * ((uint64_t)wds[i] + kSegItemWords);

@@ -1,9 +1,9 @@
 """GPU parity of the wide-window segment kernel (fcs_segw_kernel<WD>).
 
 Fixed lengths the segment route takes (fixed_segil(), fcs_launch.hpp) run in segments of the wide
-kernel's cover when segment_wd() finds that cheaper than 1524-B segments: WD 26 / 30 / 32 windows,
-1604 / 1860 / 1988-B segments. The front segment of L - C (m - 1) bytes carries the wide kernel's
-front lane (cf, zc), the other segments carry the frame's CRC state into lane 15. Every case is
+kernel's cover when segment_wd() finds that cheaper than 1524-B segments: WD 15..23 windows
+(900..1412-B segments) or 26 / 30 / 32 (1604 / 1860 / 1988 B). The front segment of L - C (m - 1)
+bytes carries the wide kernel's front lane (cf, zc), the other segments carry the frame's CRC state into lane 15. Every case is
 bit-exact against the oracle (the CPU restatement of src/ether_fcs.c:4-19). The lengths are picked
 through the product's own route (fcs_debug_fixed_route), so the test follows segment_wd()'s cost
 constant: front segments at every front-lane edge (1..5 bytes, around each multiple of the window
@@ -21,8 +21,9 @@ pytestmark = pytest.mark.gpu
 
 torch = pytest.importorskip("torch")
 
-COVER = {26: 1604, 30: 1860, 32: 1988}
-STEP = {26: 100, 30: 116, 32: 124}
+WIDTHS = [15, 16, 18, 19, 20, 22, 23, 26, 30, 32]   # fcs_launch.hpp segment_wd candidates besides 24
+STEP = {wd: 4 * wd - 4 for wd in WIDTHS}
+COVER = {wd: 15 * STEP[wd] + 4 * wd for wd in WIDTHS}
 BASE = 1 << 30
 
 
@@ -90,13 +91,16 @@ def test_segw_front_edges(dev, oracle):
             assert na.last_fixed_launch() == f"segment:{wd}/768", (L, wd, na.last_fixed_launch())
 
 
-@pytest.mark.parametrize("wd", [26, 30, 32])
-def test_segw_many_units(dev, oracle, wd):
-    """More units than the grid's waves (the dynamic schedule), twice (the counter ring reused)."""
-    cases = [L for L, w in routed_lengths() if w == wd]
-    if not cases:
-        pytest.skip(f"no length routes to segment:{wd}")
-    L = cases[len(cases) // 2]
+def test_segw_many_units(dev, oracle):
+    """Every routed width: more units than the grid's waves (the dynamic schedule), twice (the
+    counter ring reused)."""
+    routed = routed_lengths()
+    for wd in sorted({w for _, w in routed}):
+        cases = [L for L, w in routed if w == wd]
+        _many_units(dev, oracle, wd, cases[len(cases) // 2])
+
+
+def _many_units(dev, oracle, wd, L):
     stride = L + 7
     n = max(20001, (200 << 20) // stride)
     host = np.random.default_rng(L + wd).integers(0, 256, n * stride + 8, dtype=np.uint8)
@@ -107,13 +111,15 @@ def test_segw_many_units(dev, oracle, wd):
         assert np.array_equal(got, exp), (L, int(np.argmax(got != exp)))
 
 
-@pytest.mark.parametrize("wd", [26, 30, 32])
-def test_segw_verify_mode(dev, wd):
-    """RX residue check through the kernel: frames carrying their FCS, a few corrupted."""
-    cases = [L for L, w in routed_lengths() if w == wd]
-    if not cases:
-        pytest.skip(f"no length routes to segment:{wd}")
-    L = cases[-1]
+def test_segw_verify_mode(dev):
+    """Every routed width: RX residue check through the kernel, frames carrying their FCS, a few
+    corrupted."""
+    routed = routed_lengths()
+    for wd in sorted({w for _, w in routed}):
+        _verify(dev, [L for L, w in routed if w == wd][-1])
+
+
+def _verify(dev, L):
     n = 2051
     rng = np.random.default_rng(L)
     host = rng.integers(0, 256, n * L, dtype=np.uint8)

@@ -23,7 +23,7 @@ PACKED = {
     868: "wide8:28", 869: "flat", 870: "wide16:15", 1000: "wide16:18", 1157: "wide16:20", 1476: "wide16:24",
     1477: "wide16:26", 1495: "wide16:26", 1496: "lds-dma", 1518: "lds-dma", 1524: "lds-dma", 1525: "wide16:26",
     1536: "wide16:26", 1604: "wide16:26", 1605: "wide16:30", 1787: "wide16:30", 1788: "wide16:32",
-    1988: "wide16:32", 2500: "segment", 3049: "generic", 3073: "segment:26", 9000: "segment:30", 9216: "segment:30",
+    1988: "wide16:32", 2500: "segment:22", 3049: "generic", 3073: "segment:26", 9000: "segment:30", 9216: "segment:30",
     65536: "segment:32",
 }
 
@@ -91,15 +91,18 @@ def _seg_item_words():
 def test_segment_width_rule(lib):
     """Packed batches the segment route takes pick the segment width with the least per-lane work,
     m (WD + K) for m = ceil(len / cover) (fcs_launch.hpp segment_wd: cover 1524 B for WD 24, the
-    wide kernel's 1604 / 1860 / 1988 B for WD 26 / 30 / 32; ties keep the narrower width)."""
+    wide kernel's 15 (4 WD - 4) + 4 WD for the other widths; ties keep the earlier candidate)."""
     K = _seg_item_words()
-    cover = {24: 1524, 26: 1604, 30: 1860, 32: 1988}
+    order = [24, 15, 16, 18, 19, 20, 22, 23, 26, 30, 32]   # candidates in the order segment_wd tries them
+    cover = {w: 15 * (4 * w - 4) + 4 * w for w in order}
+    cover[24] = 1524
     seen = set()
     for L in list(range(1950, 12000, 7)) + [16384, 40000, 65536, 100000]:
         got = lib.fixed_route(BASE, L, L, BIG)
         if not got.startswith("segment"):
             continue
-        best = min((-(-L // cover[w]) * (w + K), w) for w in (24, 26, 30, 32))[1]
+        costs = [-(-L // cover[w]) * (w + K) for w in order]
+        best = order[costs.index(min(costs))]   # the first candidate at the least cost
         assert got == ("segment" if best == 24 else f"segment:{best}"), (L, got, best)
         seen.add(best)
-    assert seen == {24, 26, 30, 32}
+    assert {24, 26, 30, 32} <= seen
