@@ -155,23 +155,6 @@ inline bool fixed_dma(const KParams &p) {
 //     3300 B +16 %; 3049 B -4 %: the generic kernel covers it in 2 segments), or
 //   - m = 2 and len >= 1950 (2000 B +2.7 %, 2285 B +7.4 %; 1560-1900 B -1 to -4 %, and 1525-1536 B
 //     are a single generic segment: -26 %).
-constexpr uint32_t kSegilMinLen2 = 1950;
-constexpr int kSegilWgThreads = 768;
-inline bool fixed_segil(const KParams &p) {
-#ifdef FCS_NO_SEGIL   // measurement-only build
-    (void)p;
-    return false;
-#else
-    const uint64_t m = (p.flen + kDmaCover - 1) / kDmaCover;
-    if (p.flen <= kDmaCover || fixed_tiny(p)) return false;
-#ifdef FCS_SEGIL_ANY   // measurement-only: every fixed length over 1524 B
-    return true;
-#endif
-    if (m >= 4) return true;
-    if (m == 3) return p.flen > 2u * (uint32_t)kSegBytes;
-    return p.flen >= kSegilMinLen2;
-#endif
-}
 // Segment width for a batch fixed_segil() takes: 24 (fcs_segil_kernel, 1524-B segments) or another
 // width with lane tables (fcs_segw_kernel<WD>, segments of wide_cover(WD): 15..23 for 900..1412 B,
 // 26 / 30 / 32 for 1604 / 1860 / 1988 B): the least per-lane work per frame, m (WD + kSegItemWords)
@@ -197,6 +180,24 @@ __host__ __device__ constexpr int segment_wd(uint32_t len) {
         }
     }
     return best;
+#endif
+}
+constexpr uint32_t kSegilMinLen2 = 1950;
+constexpr int kSegilWgThreads = 768;
+inline bool fixed_segil(const KParams &p) {
+#ifdef FCS_NO_SEGIL   // measurement-only build
+    (void)p;
+    return false;
+#else
+    const uint64_t m = (p.flen + kDmaCover - 1) / kDmaCover;
+    if (p.flen <= kDmaCover || fixed_tiny(p)) return false;
+#ifdef FCS_SEGIL_ANY   // measurement-only: every fixed length over 1524 B
+    return true;
+#endif
+    if (m >= 4) return true;
+    // 3049..3072 B: two generic segments, unless a wider segment width covers the frame in two items
+    if (m == 3) return p.flen > 2u * (uint32_t)kSegBytes || segment_wd(p.flen) != 24;
+    return p.flen >= kSegilMinLen2;
 #endif
 }
 // Wide LDS-DMA kernel (fcs_wide_kernel): one-item frames of kWideMinLen..kWideCover bytes (128-B

@@ -70,7 +70,7 @@ def test_strided_routes(dev, oracle, L, stride, want):
 
 @pytest.mark.parametrize("L,stride,n,want", [
     (64, 64, THRESHOLD, "generic"), (64, 64, THRESHOLD + 1, "short:16"), (1518, 1518, 100, "lds-dma"),
-    (1518, 1518, 2, "single"), (100, 100, 1, "tiny"), (9000, 9000, 3, "segment:30"), (3049, 3049, 50, "generic"),
+    (1518, 1518, 2, "single"), (100, 100, 1, "tiny"), (9000, 9000, 3, "segment:30"), (3049, 3049, 50, "segment:26"), (1600, 5000, 50, "generic"),
 ])
 def test_small_batch_routes(dev, oracle, L, stride, n, want):
     route, launched, exact = _run(dev, oracle, L, stride, n)

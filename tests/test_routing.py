@@ -23,7 +23,7 @@ PACKED = {
     868: "wide8:28", 869: "flat", 870: "wide16:15", 1000: "wide16:18", 1157: "wide16:20", 1476: "wide16:24",
     1477: "wide16:26", 1495: "wide16:26", 1496: "lds-dma", 1518: "lds-dma", 1524: "lds-dma", 1525: "wide16:26",
     1536: "wide16:26", 1604: "wide16:26", 1605: "wide16:30", 1787: "wide16:30", 1788: "wide16:32",
-    1988: "wide16:32", 2500: "segment:22", 3049: "generic", 3073: "segment:26", 9000: "segment:30", 9216: "segment:30",
+    1988: "wide16:32", 2500: "segment:22", 3049: "segment:26", 3073: "segment:26", 9000: "segment:30", 9216: "segment:30",
     65536: "segment:32",
 }
 

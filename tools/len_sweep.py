@@ -42,9 +42,12 @@ def family(L):
     if L <= 1988:
         return "wide WD32"
     m = (L + 1523) // 1524
-    if m >= 4 or (m == 3 and L > 3072) or (m == 2 and L >= 1950):
-        cover = {24: 1524, 26: 1604, 30: 1860, 32: 1988}
-        wd = min((-(-L // cover[w]) * (w + 8), w) for w in (24, 26, 30, 32))[1]
+    order = [24, 15, 16, 18, 19, 20, 22, 23, 26, 30, 32]   # fcs_launch.hpp segment_wd's candidates
+    cover = {w: 15 * (4 * w - 4) + 4 * w for w in order}
+    cover[24] = 1524
+    costs = [-(-L // cover[w]) * (w + 8) for w in order]
+    wd = order[costs.index(min(costs))]
+    if m >= 4 or (m == 3 and (L > 3072 or wd != 24)) or (m == 2 and L >= 1950):
         return "segment (interleaved)" if wd == 24 else f"segment (interleaved, WD{wd})"
     return "generic"
 
