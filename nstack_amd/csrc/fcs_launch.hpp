@@ -152,7 +152,9 @@ inline bool fixed_dma(const KParams &p) {
 // length, round 3) when
 //   - m >= 4 (4573 B and 6100 B equal, 9000 B +3 to +8.5 %, 65536 B +16 %), or
 //   - m = 3 and the generic kernel needs 3 segments too, i.e. len > 3072 (3100 B +17 %,
-//     3300 B +16 %; 3049 B -4 %: the generic kernel covers it in 2 segments), or
+//     3300 B +16 %; 3049 B -4 %: the generic kernel covers it in 2 segments), or m = 3 and a wider
+//     segment width covers the frame in two items (round 5: 3049-3072 B on WD 26, +8.5 to +10.6 %
+//     against the generic kernel), or
 //   - m = 2 and len >= 1950 (2000 B +2.7 %, 2285 B +7.4 %; 1560-1900 B -1 to -4 %, and 1525-1536 B
 //     are a single generic segment: -26 %).
 // Segment width for a batch fixed_segil() takes: 24 (fcs_segil_kernel, 1524-B segments) or another
