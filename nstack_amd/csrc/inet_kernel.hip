@@ -484,8 +484,10 @@ __global__ __launch_bounds__(kStWaves * 64, 1) void inet_stream_kernel(IParams p
                     const uint32_t o2 = __builtin_amdgcn_udot4(x.z, 0x01000100u, o1, false);
                     const uint32_t e3 = __builtin_amdgcn_udot4(x.w, 0x00010001u, e2, false);
                     const uint32_t o3 = __builtin_amdgcn_udot4(x.w, 0x01000100u, o2, false);
-                    const uint32_t b = nxt - Pq;
-                    if (b < 16u) {   // the next packet starts inside the piece, in dword b / 4 at byte b % 4
+                    // the next packet starts inside the piece's span bytes (in dword b / 4 at byte b % 4);
+                    // the last packet's `nxt` is the span end, never a start
+                    const uint32_t b = nxt - Pq, hi = cg.total - Pq < 16u ? cg.total - Pq : 16u;
+                    if (b < hi) {
                         const uint32_t db = b >> 2, lm = (1u << (8u * (b & 3u))) - 1u;
                         uint32_t eb = db == 0 ? 0u : (db == 1 ? e0 : (db == 2 ? e1 : e2));
                         uint32_t ob = db == 0 ? 0u : (db == 1 ? o0 : (db == 2 ? o1 : o2));

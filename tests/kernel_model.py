@@ -507,3 +507,73 @@ def model_segw_frame(lds, frame: bytes, garbage: bytes, wd: int):
             v ^= model_wide_window_value(lds, w, c, z, x0, wd)
         acc = v
     return ~acc & 0xFFFFFFFF
+
+
+# ---- inet_stream_kernel: a packed 64-packet window summed from 6 KiB slot items ----
+def _dot4(x, w, c):
+    """v_dot4_u32_u8: c + sum of the four byte products of x and w."""
+    return c + sum(((x >> (8 * k)) & 0xFF) * ((w >> (8 * k)) & 0xFF) for k in range(4))
+
+
+def model_inet_window(span: bytes, starts, total: int, slot=6144, lane_bytes=96):
+    """Per-packet sums E + 256 O (even- and odd-addressed bytes of each packet, span positions
+    relative to the 16-B aligned span start) as inet_stream_kernel attributes them: items of `slot`
+    bytes, lane l takes bytes [96 l, 96 l + 96) of an item piece by piece; the packet holding the
+    lane's first byte by binary search over the 64 starts (inactive lanes hold `total`); a piece
+    holds at most one packet start, split by the running dot4 sums before its dword plus that
+    dword's bytes below it; the span's first and last pieces are masked to [starts[0], total)."""
+    st = list(starts) + [total] * (64 - len(starts))
+    acc = [0] * 64
+    st0 = st[0]
+    for k in range(-(-total // slot)):
+        for lane in range(slot // lane_bytes):
+            P0 = k * slot + lane_bytes * lane
+            if P0 >= total:
+                continue
+            cur = 0
+            b = 32
+            while b:
+                if st[cur + b] <= P0:
+                    cur += b
+                b >>= 1
+            nxt = st[cur + 1] if cur + 1 < 64 else total
+            E = O = 0
+            for q in range(lane_bytes // 16):
+                Pq = P0 + 16 * q
+                if Pq >= total:
+                    break
+                piece = bytearray(span[Pq:Pq + 16].ljust(16, b"\0"))
+                if Pq < st0 or total - Pq < 16:
+                    lo = st0 - Pq if Pq < st0 else 0
+                    hi = min(16, total - Pq)
+                    for j in range(16):
+                        if not lo <= j < hi:
+                            piece[j] = 0
+                x = [int.from_bytes(piece[4 * d:4 * d + 4], "little") for d in range(4)]
+                if nxt <= Pq:
+                    acc[cur] += E + (O << 8)
+                    E = O = 0
+                    cur += 1
+                    nxt = st[cur + 1] if cur + 1 < 64 else total
+                e, o = [0] * 4, [0] * 4
+                ce = co = 0
+                for d in range(4):
+                    ce = _dot4(x[d], 0x00010001, ce)
+                    co = _dot4(x[d], 0x01000100, co)
+                    e[d], o[d] = ce, co
+                bnd = nxt - Pq
+                if bnd < min(16, total - Pq):
+                    db, lm = bnd >> 2, (1 << (8 * (bnd & 3))) - 1
+                    eb = 0 if db == 0 else e[db - 1]
+                    ob = 0 if db == 0 else o[db - 1]
+                    eb = _dot4(x[db], 0x00010001 & lm, eb)
+                    ob = _dot4(x[db], 0x01000100 & lm, ob)
+                    acc[cur] += (E + eb) + ((O + ob) << 8)
+                    cur += 1
+                    nxt = st[cur + 1] if cur + 1 < 64 else total
+                    E, O = e[3] - eb, o[3] - ob
+                else:
+                    E += e[3]
+                    O += o[3]
+            acc[cur] += E + (O << 8)
+    return acc

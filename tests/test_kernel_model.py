@@ -290,3 +290,26 @@ def test_segw_decomposition_model(lds_wide, L, wd):
     frame = rng.integers(0, 256, L, dtype=np.uint8).tobytes()
     garbage = rng.integers(0, 256, 2048, dtype=np.uint8).tobytes()
     assert km.model_segw_frame(lds_wide[wd], frame, garbage, wd) == zlib.crc32(frame)
+
+
+@pytest.mark.parametrize("seed,lead", [(1, 0), (2, 5), (3, 15), (4, 1)])
+def test_inet_stream_attribution(seed, lead):
+    """inet_stream_kernel's attribution of a packed window's bytes to its packets (lane regions of
+    96 B, one packet start per 16-B piece, dot4 running sums split at a start) gives every packet
+    exactly its own even/odd byte sums E + 256 O, the word sum the checksum folds (the RFC 1071
+    sum of src/ip.c:39-62 before the fold). Packets of 16 B to 9 KiB, a window spanning several
+    6 KiB items, a partial window, and every start alignment within the first piece."""
+    rng = np.random.default_rng(seed)
+    npk = 64 if seed != 4 else 37
+    ln = rng.choice([16, 17, 20, 31, 64, 65, 576, 1518], npk)
+    ln[rng.integers(0, npk, 3)] = rng.integers(2000, 9000, 3)
+    starts = lead + np.concatenate([[0], np.cumsum(ln)[:-1]])
+    total = int(starts[-1] + ln[-1])
+    span = rng.integers(0, 256, total + 16, dtype=np.uint8).tobytes()
+    got = km.model_inet_window(span, [int(s) for s in starts], total)
+    for i in range(npk):
+        pk = span[int(starts[i]):int(starts[i]) + int(ln[i])]
+        e = sum(pk[j] for j in range(len(pk)) if (int(starts[i]) + j) % 2 == 0)
+        o = sum(pk[j] for j in range(len(pk)) if (int(starts[i]) + j) % 2 == 1)
+        assert got[i] == e + 256 * o, i
+    assert all(v == 0 for v in got[npk:])
