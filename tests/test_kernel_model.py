@@ -279,10 +279,12 @@ def test_wide_windows_bank_distinct():
 
 
 @pytest.mark.parametrize("L,wd", [(1989, 26), (3100, 26), (3208, 26), (3209, 26), (6100, 26), (9216, 26),
-                                  (1989, 30), (3720, 30), (3721, 30), (5000, 30), (9216, 30), (9300, 30), (9301, 30)])
+                                  (1989, 30), (3720, 30), (3721, 30), (5000, 30), (9216, 30), (9300, 30), (9301, 30),
+                                  (2000, 18), (2184, 18), (2185, 18), (2200, 19), (2500, 22), (2696, 22), (4000, 22),
+                                  (2800, 23), (2824, 23), (3049, 26), (65536, 32)])
 def test_segw_decomposition_model(lds_wide, L, wd):
     """fcs_segw_kernel<WD>'s decomposition: a front segment of L - C (m - 1) bytes (C = the wide
-    kernel's cover: 1604 B for WD 26, 1860 B for WD 30) with the wide kernel's front lane, then
+    kernel's cover 15 (4 WD - 4) + 4 WD: 1092 B for WD 18 ... 1988 B for WD 32) with the wide kernel's front lane, then
     C-byte segments whose lane 15 starts unmasked from the frame's CRC state after the previous
     segment, reproduces the CRC (zlib = src/ether_fcs.c:4-19); cover bytes before the frame are
     random garbage."""
