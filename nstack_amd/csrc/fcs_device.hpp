@@ -1,6 +1,5 @@
 // fcs_device.hpp — device lookup shared by the library's translation units (not exported).
 #pragma once
-#include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
 #include <functional>
@@ -32,7 +31,8 @@ __attribute__((visibility("hidden"))) void host_batch_answered(const char *site,
 // queues count their own batches with it).
 __attribute__((visibility("hidden"))) bool last_call_host_answered();
 // Runs launch(ctr) with a zeroed work counter of device `dev` (the Dispenser's, dispenser.hpp)
-// leased for that launch on stream st (zeroed on st after the slot's previous kernel finished).
-__attribute__((visibility("hidden"))) int launch_with_counter(int dev, hipStream_t st,
+// leased for that launch on stream `stream` (a hipStream_t; zeroed on it after the slot's previous
+// kernel finished). Host-only headers include this file, so the stream travels as void *.
+__attribute__((visibility("hidden"))) int launch_with_counter(int dev, void *stream,
                                                               const std::function<int(unsigned long long *)> &launch);
 }  // namespace fcs

@@ -1549,7 +1549,8 @@ int fcs::current_device(int *dev, int *cus) {
     return 0;
 }
 
-int fcs::launch_with_counter(int dev, hipStream_t st, const std::function<int(unsigned long long *)> &launch) {
+int fcs::launch_with_counter(int dev, void *stream, const std::function<int(unsigned long long *)> &launch) {
+    hipStream_t st = (hipStream_t)stream;
     DevState *ds = nullptr;
     int rc = dev_state(dev, &ds);
     if (rc) return rc;

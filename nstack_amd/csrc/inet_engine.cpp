@@ -51,7 +51,7 @@ int launch_counted(bool var, int mode, inet::IParams &p, int dev, int cus, hipSt
         HIPTRY(inet::launch_inet(var, mode, p, cus, flat_min, dma_min, st), "launching the inet kernel");
         return 0;
     };
-    if (!var && inet::dma_route(var, p, dma_min)) return fcs::launch_with_counter(dev, st, go);
+    if (!var && inet::dma_route(var, p, dma_min)) return fcs::launch_with_counter(dev, (void *)st, go);
     return go(nullptr);
 }
 
