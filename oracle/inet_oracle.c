@@ -147,3 +147,94 @@ void oracle_inet_batch(int mode, const uint8_t *arena, const uint64_t *off, cons
             out[i] = oracle_ip_checksum(p, len[i]);
     }
 }
+
+/* ---- full-batch digests of splitmix batches (tests/test_gpu_inet.py at BASELINE-like sizes) ----
+ * Packet i is bytes [off_i, off_i + len_i) (off == NULL: i * stride; len == NULL: flen) of the
+ * counter-based stream of the product's fcs_fill_splitmix64 (word w = splitmix64(seed + w), little
+ * endian; the same stream as oracle_splitmix_fill in fcs_oracle.c), checksummed by the restatement
+ * above (mode as oracle_inet_batch; tcp/udp addresses addr[2i], addr[2i+1]). The digest is the sum
+ * of the u16 results and the sum of result * (i & 0xffff), over nthreads host threads; packets are
+ * regenerated on the fly, never materialised. */
+#include <pthread.h>
+
+static uint64_t inet_splitmix64(uint64_t x)
+{
+    x += 0x9E3779B97F4A7C15ull;
+    x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+    x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+    return x ^ (x >> 31);
+}
+
+static void inet_splitmix_bytes(uint8_t *buf, size_t n, uint64_t seed, uint64_t pos0)
+{
+    size_t i = 0;
+    for (; i < n && ((pos0 + i) & 7); i++)
+        buf[i] = (uint8_t)(inet_splitmix64(seed + ((pos0 + i) >> 3)) >> (8 * ((pos0 + i) & 7)));
+    for (; i + 8 <= n; i += 8) {   /* whole words (little-endian host) */
+        const uint64_t w = inet_splitmix64(seed + ((pos0 + i) >> 3));
+        memcpy(buf + i, &w, 8);
+    }
+    for (; i < n; i++)
+        buf[i] = (uint8_t)(inet_splitmix64(seed + ((pos0 + i) >> 3)) >> (8 * ((pos0 + i) & 7)));
+}
+
+struct inet_digest_job {
+    int mode;
+    uint64_t seed, stride, i0, i1;
+    const uint64_t *off;
+    const uint32_t *len;
+    const uint32_t *addr;
+    uint32_t flen;
+    uint64_t sum, wsum;
+};
+
+static void *inet_digest_worker(void *arg)
+{
+    struct inet_digest_job *j = (struct inet_digest_job *) arg;
+    static __thread uint8_t buf[1 << 16];
+    uint64_t sum = 0, wsum = 0;
+    for (uint64_t i = j->i0; i < j->i1; i++) {
+        const uint64_t o = j->off ? j->off[i] : i * j->stride;
+        const uint32_t L = j->len ? j->len[i] : j->flen;
+        if (L > sizeof buf)
+            return NULL;   /* not for jumbo packets: sum stays short, the test fails loudly */
+        inet_splitmix_bytes(buf, L, j->seed, o);
+        uint16_t c;
+        if (j->mode == 1)
+            c = oracle_tcp_checksum(j->addr[2 * i], j->addr[2 * i + 1], buf, L);
+        else if (j->mode == 2)
+            c = oracle_udp_checksum(buf, L, j->addr[2 * i], j->addr[2 * i + 1]);
+        else
+            c = oracle_ip_checksum(buf, L);
+        sum += c;
+        wsum += (uint64_t) c * (i & 0xffffu);
+    }
+    j->sum = sum;
+    j->wsum = wsum;
+    return NULL;
+}
+
+void oracle_inet_splitmix_digest(int mode, uint64_t seed, const uint64_t *off, const uint32_t *len,
+                                 uint64_t stride, uint32_t flen, const uint32_t *addr, uint64_t n, int nthreads,
+                                 uint64_t *sum_out, uint64_t *wsum_out)
+{
+    if (nthreads < 1)
+        nthreads = 1;
+    if (nthreads > 256)
+        nthreads = 256;
+    pthread_t th[256];
+    struct inet_digest_job jobs[256];
+    for (int t = 0; t < nthreads; t++) {
+        jobs[t] = (struct inet_digest_job){mode, seed, stride, n * (uint64_t) t / (uint64_t) nthreads,
+                                           n * (uint64_t)(t + 1) / (uint64_t) nthreads, off, len, addr, flen, 0, 0};
+        pthread_create(&th[t], NULL, inet_digest_worker, &jobs[t]);
+    }
+    uint64_t sum = 0, wsum = 0;
+    for (int t = 0; t < nthreads; t++) {
+        pthread_join(th[t], NULL);
+        sum += jobs[t].sum;
+        wsum += jobs[t].wsum;
+    }
+    *sum_out = sum;
+    *wsum_out = wsum;
+}

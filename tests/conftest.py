@@ -88,6 +88,9 @@ def inet_oracle():
     L.oracle_udp_checksum.restype = u16
     L.oracle_udp_checksum.argtypes = [vp, sz, u32, u32]
     L.oracle_inet_batch.argtypes = [ctypes.c_int, vp, vp, vp, vp, vp, sz]
+    u64 = ctypes.c_uint64
+    L.oracle_inet_splitmix_digest.argtypes = [ctypes.c_int, u64, vp, vp, u64, u32, vp, u64, ctypes.c_int,
+                                              ctypes.POINTER(u64), ctypes.POINTER(u64)]
     return L
 
 

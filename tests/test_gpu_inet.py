@@ -260,3 +260,63 @@ def test_argument_errors(dev):
         na.inet_fixed_dev("udp", 64, 20, 20, 1, None, 64)
     with pytest.raises(na.FcsError):
         na.inet_fixed_dev("ip", 64, 10, 20, 2, None, 64)   # stride < len
+
+
+def _dev_digest(out):
+    """Sum of the u16 results and sum of result * (i & 0xffff), on the device (as the oracle's)."""
+    u = out.to(torch.int64) & 0xFFFF
+    idx = torch.arange(out.numel(), device=out.device, dtype=torch.int64) & 0xFFFF
+    return int(u.sum().item()), int((u * idx).sum().item())
+
+
+def _oracle_digest(inet_oracle, mode, seed, off, ln, addr, n):
+    import ctypes
+    s, w = ctypes.c_uint64(), ctypes.c_uint64()
+    inet_oracle.oracle_inet_splitmix_digest(mode, seed, off.ctypes.data, ln.ctypes.data, 0, 0,
+                                            None if addr is None else addr.ctypes.data, n, 16,
+                                            ctypes.byref(s), ctypes.byref(w))
+    return s.value, w.value
+
+
+def test_full_imix_digest(dev, inet_oracle):
+    """Every checksum of 128 M packed IMIX packets (7:4:1 of 64/576/1518 B, shuffled; the LDS
+    stream kernel), against the oracle's digest of the same splitmix stream (16 host threads,
+    packets regenerated on the fly)."""
+    n = 128 << 20
+    c1518, c576 = n // 12, (n * 4) // 12
+    ln = np.repeat(np.array([64, 576, 1518], dtype=np.uint32), [n - c576 - c1518, c576, c1518])
+    np.random.default_rng(7).shuffle(ln)
+    off = np.zeros(n, dtype=np.uint64)
+    np.cumsum(ln[:-1], dtype=np.uint64, out=off[1:])
+    total = int(off[-1]) + int(ln[-1])
+    arena = torch.empty(total + 64, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(arena, total + 64, 0x17A5, 0)
+    d_off = torch.from_numpy(off.view(np.int64)).to(dev)
+    d_len = torch.from_numpy(ln.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    na.inet_batch_dev("ip", arena, total + 64, d_off, d_len, None, out, n)
+    torch.cuda.synchronize()
+    got = _dev_digest(out)
+    del arena, d_off, d_len, out
+    torch.cuda.empty_cache()
+    assert got == _oracle_digest(inet_oracle, 0, 0x17A5, off, ln, None, n)
+
+
+def test_full_tcp_digest(dev, inet_oracle):
+    """Every TCP checksum of 64 M segments (+34, 1480 B) of packed 1518-B frames (the LDS-DMA
+    fixed-stride kernel), against the oracle's digest of the same stream and addresses."""
+    n, stride, start, L = 64 << 20, 1518, 34, 1480
+    nbytes = n * stride + 64
+    buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    na.fill_splitmix_dev(buf, nbytes, 0x7C9, 0)
+    addr = np.random.default_rng(5).integers(0, 2**32, 2 * n, dtype=np.uint64).astype(np.uint32)
+    d_addr = torch.from_numpy(addr.view(np.int32)).to(dev)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    na.inet_fixed_dev("tcp", buf.data_ptr() + start, stride, L, n, d_addr, out)
+    torch.cuda.synchronize()
+    got = _dev_digest(out)
+    del buf, d_addr, out
+    torch.cuda.empty_cache()
+    off = start + np.arange(n, dtype=np.uint64) * np.uint64(stride)
+    ln = np.full(n, L, dtype=np.uint32)
+    assert got == _oracle_digest(inet_oracle, 1, 0x7C9, off, ln, addr, n)

@@ -5,6 +5,7 @@ could not be built here, so parity with them is pinned only thro
 import random
 import struct
 
+import numpy as np
 import pytest
 
 from golden.make_inet_golden import witness
@@ -60,3 +61,27 @@ def test_tcp_segment_with_checksum_in_place_verifies(inet_oracle):
         c = inet_oracle.oracle_tcp_checksum(s, d, bytes(seg), n)
         seg[16:18] = struct.pack("<H", c)
         assert inet_oracle.oracle_tcp_checksum(s, d, bytes(seg), n) == 0
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_splitmix_digest_matches_batch(inet_oracle, oracle, mode):
+    """The threaded digest (packets regenerated from the splitmix stream) equals the digest of the
+    per-packet restatement over the same bytes (fcs_oracle.c's oracle_splitmix_fill)."""
+    import ctypes
+    rng = np.random.default_rng(mode + 40)
+    n = 3001
+    ln = rng.choice([0, 1, 20, 64, 576, 1500, 1518, 4000], n).astype(np.uint32)
+    off = np.concatenate([[3], 3 + np.cumsum(ln)[:-1]]).astype(np.uint64)
+    total = int(off[-1] + ln[-1])
+    arena = np.empty(total, dtype=np.uint8)
+    oracle.oracle_splitmix_fill(arena.ctypes.data, total, 77, 0)
+    addr = rng.integers(0, 2**32, 2 * n, dtype=np.uint64).astype(np.uint32)
+    out = np.empty(n, dtype=np.uint16)
+    inet_oracle.oracle_inet_batch(mode, arena.ctypes.data, off.ctypes.data, ln.ctypes.data,
+                                  addr.ctypes.data if mode else None, out.ctypes.data, n)
+    s, w = ctypes.c_uint64(), ctypes.c_uint64()
+    inet_oracle.oracle_inet_splitmix_digest(mode, 77, off.ctypes.data, ln.ctypes.data, 0, 0,
+                                            addr.ctypes.data if mode else None, n, 4, ctypes.byref(s), ctypes.byref(w))
+    idx = np.arange(n, dtype=np.uint64) & np.uint64(0xFFFF)
+    assert s.value == int(out.astype(np.uint64).sum())
+    assert w.value == int((out.astype(np.uint64) * idx).sum())
