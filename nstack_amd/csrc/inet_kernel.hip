@@ -630,6 +630,70 @@ __global__ __launch_bounds__(kDmaWaves * 64, 1) void inet_dma_kernel(IParams p) 
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Short fixed-stride packets (inet_short_kernel): one lane per packet of at most kShortMax bytes
+// (the IP header ip_hton checksums, src/ip.c:79-80). Each lane loads the (at most five) 16-B pieces
+// its packet touches, masks the first and last, sums the even- and odd-addressed bytes by
+// v_dot4_u32_u8, folds, and 64 results leave as one 128-B store. Two packets per lane are in
+// flight (the next one's loads issued before the current one is summed); a grid of persistent
+// waves walks the batch. The one-packet-per-quarter-wave kernels spend 16 lanes on a 20-B header.
+// ---------------------------------------------------------------------------------------------
+constexpr uint32_t kShortMax = 64;
+constexpr int kShortPieces = (int)(kShortMax + 15 + 15) / 16;   // 5
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads) void inet_short_kernel(IParams p) {
+    const uint64_t G = (uint64_t)gridDim.x * kThreads;
+    const uint32_t L = p.flen;
+    auto issue = [&](uint64_t i, u32x4 (&v)[kShortPieces]) {
+        if (L == 0) return;   // empty packets load nothing
+        const uint64_t start = p.base + i * p.stride, c0 = start & ~15ull;
+        const uint32_t nch = (uint32_t)((((start + L + 15) & ~15ull) - c0) >> 4);
+#pragma unroll
+        for (int q = 0; q < kShortPieces; q++)   // past the last piece: its own piece again (a cache hit)
+            v[q] = gload<u32x4>(c0 + 16ull * ((uint32_t)q < nch ? (uint32_t)q : nch - 1));
+    };
+    uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
+    u32x4 v[kShortPieces], w[kShortPieces];
+    if (i < p.n) issue(i, v);
+    while (i < p.n) {
+        const uint64_t nx = i + G;
+        if (nx < p.n) issue(nx, w);
+        const uint64_t start = p.base + i * p.stride, c0 = start & ~15ull, end = start + L;
+        const uint32_t nch = (uint32_t)((((end + 15) & ~15ull) - c0) >> 4);
+        uint32_t E = 0, O = 0;
+#pragma unroll
+        for (int q = 0; q < kShortPieces; q++) {
+            if ((uint32_t)q >= nch) break;
+            u32x4 x = v[q];
+            if (q == 0 || (uint32_t)q + 1 == nch) {   // edge pieces: keep bytes in [start, end)
+                const uint64_t ca = c0 + 16ull * (uint32_t)q;
+                const uint32_t lo = start > ca ? (uint32_t)(start - ca) : 0u;
+                const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
+                const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+                x.x &= byte_mask(keep, 0);
+                x.y &= byte_mask(keep, 1);
+                x.z &= byte_mask(keep, 2);
+                x.w &= byte_mask(keep, 3);
+            }
+            E = __builtin_amdgcn_udot4(x.x, 0x00010001u, E, false);
+            O = __builtin_amdgcn_udot4(x.x, 0x01000100u, O, false);
+            E = __builtin_amdgcn_udot4(x.y, 0x00010001u, E, false);
+            O = __builtin_amdgcn_udot4(x.y, 0x01000100u, O, false);
+            E = __builtin_amdgcn_udot4(x.z, 0x00010001u, E, false);
+            O = __builtin_amdgcn_udot4(x.z, 0x01000100u, O, false);
+            E = __builtin_amdgcn_udot4(x.w, 0x00010001u, E, false);
+            O = __builtin_amdgcn_udot4(x.w, 0x01000100u, O, false);
+        }
+        const uint32_t s = L ? fold64((uint64_t)E + ((uint64_t)O << 8)) : 0u;
+        const uint32_t m = (start & 1) ? swap16(s) : s;   // odd start: P = swap16(fold(M))
+        p.out[i] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, i, L) + m);
+        i = nx;
+#pragma unroll
+        for (int q = 0; q < kShortPieces; q++) v[q] = w[q];
+    }
+}
+
 // dma_ok: fixed packets whose four-packet items fit a slot with the 16-B rounding of both ends
 // (so at most kDmaRounds * 16 pieces a packet), and that fill at least half of their stride (the
 // slot also carries the gaps between packets).
@@ -650,6 +714,14 @@ hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t f
         if (mode == kTcp) hipLaunchKernelGGL((inet_stream_kernel<kTcp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
         else if (mode == kUdp) hipLaunchKernelGGL((inet_stream_kernel<kUdp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
         else hipLaunchKernelGGL((inet_stream_kernel<kIp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
+        return hipGetLastError();
+    }
+    if (!var && p.n > flat_min && p.flen <= kShortMax) {   // lane per packet
+        const uint64_t want = (p.n + kThreads - 1) / kThreads, cap = (uint64_t)cus * 8;
+        const int grid = (int)(want < cap ? want : cap);
+        if (mode == kTcp) hipLaunchKernelGGL((inet_short_kernel<kTcp>), dim3(grid), dim3(kThreads), 0, st, p);
+        else if (mode == kUdp) hipLaunchKernelGGL((inet_short_kernel<kUdp>), dim3(grid), dim3(kThreads), 0, st, p);
+        else hipLaunchKernelGGL((inet_short_kernel<kIp>), dim3(grid), dim3(kThreads), 0, st, p);
         return hipGetLastError();
     }
     if (dma_route(var, p, dma_min)) {

@@ -108,10 +108,12 @@ def test_single_forms_match_oracle(dev, inet_oracle):
 @pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("start,stride,L", [(14, 1518, 1500), (34, 1518, 1480), (14, 1518, 20),
                                              (0, 1500, 1500), (1, 97, 61), (3, 9000, 8997), (5, 64, 0),
-                                             (7, 1532, 1532), (2, 120, 64), (6, 1024, 1000), (9, 2048, 1024), (1, 1519, 1517)])
+                                             (7, 1532, 1532), (2, 120, 64), (6, 1024, 1000), (9, 2048, 1024), (1, 1519, 1517),
+                                             (3, 64, 64), (15, 33, 33), (1, 20, 1), (2, 4096, 40)])
 def test_fixed_dev_vs_oracle(dev, inet_oracle, mode, start, stride, L, inet_kernel):
     """Fixed-stride packets inside frames: the IP datagram at +14, the TCP segment at +34, the IP
-    header alone, odd strides/starts (every alignment), jumbo, and empty packets."""
+    header alone, odd strides/starts (every alignment), jumbo, empty packets, and packets of up to
+    64 B at tight and wide strides (the lane-per-packet kernel in the large-batch kernels' runs)."""
     n = 6000
     rng = np.random.default_rng(start * 7 + L)
     host = rng.integers(0, 256, start + n * stride + 16, dtype=np.uint8)
@@ -302,21 +304,24 @@ def test_full_imix_digest(dev, inet_oracle):
     assert got == _oracle_digest(inet_oracle, 0, 0x17A5, off, ln, None, n)
 
 
-def test_full_tcp_digest(dev, inet_oracle):
-    """Every TCP checksum of 64 M segments (+34, 1480 B) of packed 1518-B frames (the LDS-DMA
-    fixed-stride kernel), against the oracle's digest of the same stream and addresses."""
-    n, stride, start, L = 64 << 20, 1518, 34, 1480
+@pytest.mark.parametrize("mode,start,L", [("tcp", 34, 1480), ("ip", 14, 20)])
+def test_full_fixed_digest(dev, inet_oracle, mode, start, L):
+    """Every checksum of 64 M packets of packed 1518-B frames: TCP segments (+34, 1480 B; the
+    LDS-DMA fixed-stride kernel) and IP headers (+14, 20 B; the lane-per-packet kernel), against
+    the oracle's digest of the same stream and addresses."""
+    n, stride = 64 << 20, 1518
     nbytes = n * stride + 64
     buf = torch.empty(nbytes, dtype=torch.uint8, device=dev)
     na.fill_splitmix_dev(buf, nbytes, 0x7C9, 0)
     addr = np.random.default_rng(5).integers(0, 2**32, 2 * n, dtype=np.uint64).astype(np.uint32)
     d_addr = torch.from_numpy(addr.view(np.int32)).to(dev)
     out = torch.empty(n, dtype=torch.int16, device=dev)
-    na.inet_fixed_dev("tcp", buf.data_ptr() + start, stride, L, n, d_addr, out)
+    na.inet_fixed_dev(mode, buf.data_ptr() + start, stride, L, n, d_addr if mode != "ip" else None, out)
     torch.cuda.synchronize()
     got = _dev_digest(out)
     del buf, d_addr, out
     torch.cuda.empty_cache()
     off = start + np.arange(n, dtype=np.uint64) * np.uint64(stride)
     ln = np.full(n, L, dtype=np.uint32)
-    assert got == _oracle_digest(inet_oracle, 1, 0x7C9, off, ln, addr, n)
+    m = {"ip": 0, "tcp": 1, "udp": 2}[mode]
+    assert got == _oracle_digest(inet_oracle, m, 0x7C9, off, ln, addr if m else None, n)
