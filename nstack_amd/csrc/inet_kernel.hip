@@ -18,12 +18,13 @@
 // nonzero sum to 0), because ip/tcp start their accumulator at 0xffff (ip.c:42, tcp.c:172):
 // the only input where that differs from a zero start is all-zero data (return 0x0000).
 //
-// Work decomposition. A QUARTER-WAVE (16 lanes) per packet; lane j loads the packet's aligned
-// 16-byte chunks j, j+16, ... (global_load_dwordx4; a group reads 256 contiguous bytes per
-// instruction, the four groups of a wave the next packets), six chunks per lane in flight per
-// round (1536 bytes per packet per round). Only the first and last chunk of a packet are
-// masked. The 16 lane sums are added with 4 DPP steps; lane 0 adds the pseudo header and init,
-// folds, complements and stores. No LDS, no tables: HBM read bandwidth is the roofline.
+// Kernels (launch_inet picks one; results are identical): small batches a QUARTER-WAVE (16 lanes)
+// per packet (inet_kernel: lane j loads the packet's aligned 16-byte chunks j, j+16, ..., six in
+// flight per round; the 16 lane sums added with 4 DPP steps; lane 0 adds the pseudo header and
+// init, folds, complements and stores); large batches the flat chunk stream (inet_flat_kernel),
+// short fixed packets one lane per packet (inet_short_kernel), fixed strides four packets per LDS-DMA
+// slot (inet_dma_kernel) and packed variable windows through LDS (inet_stream_kernel). No tables:
+// HBM read bandwidth is the roofline.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
