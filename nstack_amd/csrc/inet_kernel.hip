@@ -303,6 +303,52 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
         flat_window<VAR, MODE>(p, w0, lane, acc_s[wave], mark_s[wave], list_s[wave]);
 }
 
+// Short packets (at most kShortMax bytes): the 16-B pieces a packet touches, and their sum.
+constexpr uint32_t kShortMax = 64;
+constexpr int kShortPieces = (int)(kShortMax + 15 + 15) / 16;   // 5
+
+// Loads the pieces of the packet [start, start + L) (L >= 1): piece q of the packet's first 16-B
+// boundary, or its last piece again past the end (a cache hit).
+__device__ __forceinline__ void short_issue(uint64_t start, uint32_t L, u32x4 (&v)[kShortPieces]) {
+    const uint64_t c0 = start & ~15ull;
+    const uint32_t nch = (uint32_t)((((start + L + 15) & ~15ull) - c0) >> 4);
+#pragma unroll
+    for (int q = 0; q < kShortPieces; q++)
+        v[q] = gload<u32x4>(c0 + 16ull * ((uint32_t)q < nch ? (uint32_t)q : nch - 1));
+}
+
+// The folded sum of the packet's bytes from its loaded pieces: edge pieces masked to
+// [start, start + L), even- and odd-addressed bytes summed by v_dot4_u32_u8 (0 for L == 0).
+__device__ __forceinline__ uint32_t short_sum(const u32x4 (&v)[kShortPieces], uint64_t start, uint32_t L) {
+    const uint64_t c0 = start & ~15ull, end = start + L;
+    const uint32_t nch = L ? (uint32_t)((((end + 15) & ~15ull) - c0) >> 4) : 0u;
+    uint32_t E = 0, O = 0;
+#pragma unroll
+    for (int q = 0; q < kShortPieces; q++) {
+        if ((uint32_t)q >= nch) break;
+        u32x4 x = v[q];
+        if (q == 0 || (uint32_t)q + 1 == nch) {   // edge pieces: keep bytes in [start, end)
+            const uint64_t ca = c0 + 16ull * (uint32_t)q;
+            const uint32_t lo = start > ca ? (uint32_t)(start - ca) : 0u;
+            const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
+            const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
+            x.x &= byte_mask(keep, 0);
+            x.y &= byte_mask(keep, 1);
+            x.z &= byte_mask(keep, 2);
+            x.w &= byte_mask(keep, 3);
+        }
+        E = __builtin_amdgcn_udot4(x.x, 0x00010001u, E, false);
+        O = __builtin_amdgcn_udot4(x.x, 0x01000100u, O, false);
+        E = __builtin_amdgcn_udot4(x.y, 0x00010001u, E, false);
+        O = __builtin_amdgcn_udot4(x.y, 0x01000100u, O, false);
+        E = __builtin_amdgcn_udot4(x.z, 0x00010001u, E, false);
+        O = __builtin_amdgcn_udot4(x.z, 0x01000100u, O, false);
+        E = __builtin_amdgcn_udot4(x.w, 0x00010001u, E, false);
+        O = __builtin_amdgcn_udot4(x.w, 0x01000100u, O, false);
+    }
+    return L ? fold64((uint64_t)E + ((uint64_t)O << 8)) : 0u;
+}
+
 // ---------------------------------------------------------------------------------------------
 // Variable-length batches through LDS (inet_stream_kernel): a wave owns windows of 64 consecutive
 // packets (interleaved over the grid). A window whose packets are packed (each starts where the
@@ -315,8 +361,9 @@ __global__ __launch_bounds__(kThreads) void inet_flat_kernel(IParams p) {
 // plus that dword's bytes below it; each packet's part goes into its LDS accumulator once per lane
 // (ds_add_u64). The
 // next item's DMA (or the next packed window's first) is in flight while the current one is
-// summed. Lane l finishes packet l (fold, odd-start swap, pseudo header). Other windows take the
-// flat chunk stream (flat_window) inside the same kernel. 16 waves per CU.
+// summed. Lane l finishes packet l (fold, odd-start swap, pseudo header). Other windows take one
+// lane per packet when every packet is at most kShortMax bytes, else the flat chunk stream
+// (flat_window), inside the same kernel. 16 waves per CU.
 // ---------------------------------------------------------------------------------------------
 constexpr int kStWaves = 16;
 constexpr uint32_t kStSlot = 6144;
@@ -407,7 +454,19 @@ __global__ __launch_bounds__(kStWaves * 64, 1) void inet_stream_kernel(IParams p
         const Meta nm = meta(wn);   // in flight while the current window is summed
         const uint64_t w0 = wi * 64;
         if (!cg.packed) {
-            flat_window<true, MODE>(p, w0, lane, acc, mark_s[wave], list_s[wave]);
+            const bool act = w0 + (uint64_t)lane < n;
+            if (__ballot(act && cm.len > kShortMax) == 0ull) {   // short packets: one lane each
+                if (act) {
+                    u32x4 v[kShortPieces];
+                    const uint64_t start = p.base + cm.off;
+                    if (cm.len) short_issue(start, cm.len, v);
+                    const uint32_t s0 = short_sum(v, start, cm.len);
+                    const uint32_t m = (start & 1) ? swap16(s0) : s0;
+                    p.out[w0 + lane] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, w0 + lane, cm.len) + m);
+                }
+            } else {
+                flat_window<true, MODE>(p, w0, lane, acc, mark_s[wave], list_s[wave]);
+            }
             const Geo ng = geo(wn, nm);
             if (ng.packed) dma(ng, 0);
             wi = wn;
@@ -639,54 +698,18 @@ __global__ __launch_bounds__(kDmaWaves * 64, 1) void inet_dma_kernel(IParams p) 
 // flight (the next one's loads issued before the current one is summed); a grid of persistent
 // waves walks the batch. The one-packet-per-quarter-wave kernels spend 16 lanes on a 20-B header.
 // ---------------------------------------------------------------------------------------------
-constexpr uint32_t kShortMax = 64;
-constexpr int kShortPieces = (int)(kShortMax + 15 + 15) / 16;   // 5
-
 template <int MODE>
 __global__ __launch_bounds__(kThreads) void inet_short_kernel(IParams p) {
     const uint64_t G = (uint64_t)gridDim.x * kThreads;
     const uint32_t L = p.flen;
-    auto issue = [&](uint64_t i, u32x4 (&v)[kShortPieces]) {
-        if (L == 0) return;   // empty packets load nothing
-        const uint64_t start = p.base + i * p.stride, c0 = start & ~15ull;
-        const uint32_t nch = (uint32_t)((((start + L + 15) & ~15ull) - c0) >> 4);
-#pragma unroll
-        for (int q = 0; q < kShortPieces; q++)   // past the last piece: its own piece again (a cache hit)
-            v[q] = gload<u32x4>(c0 + 16ull * ((uint32_t)q < nch ? (uint32_t)q : nch - 1));
-    };
     uint64_t i = (uint64_t)blockIdx.x * kThreads + threadIdx.x;
     u32x4 v[kShortPieces], w[kShortPieces];
-    if (i < p.n) issue(i, v);
+    if (i < p.n && L) short_issue(p.base + i * p.stride, L, v);
     while (i < p.n) {
         const uint64_t nx = i + G;
-        if (nx < p.n) issue(nx, w);
-        const uint64_t start = p.base + i * p.stride, c0 = start & ~15ull, end = start + L;
-        const uint32_t nch = (uint32_t)((((end + 15) & ~15ull) - c0) >> 4);
-        uint32_t E = 0, O = 0;
-#pragma unroll
-        for (int q = 0; q < kShortPieces; q++) {
-            if ((uint32_t)q >= nch) break;
-            u32x4 x = v[q];
-            if (q == 0 || (uint32_t)q + 1 == nch) {   // edge pieces: keep bytes in [start, end)
-                const uint64_t ca = c0 + 16ull * (uint32_t)q;
-                const uint32_t lo = start > ca ? (uint32_t)(start - ca) : 0u;
-                const uint32_t hi = end - ca < 16 ? (uint32_t)(end - ca) : 16u;
-                const uint32_t keep = ((1u << hi) - 1u) & ~((1u << lo) - 1u);
-                x.x &= byte_mask(keep, 0);
-                x.y &= byte_mask(keep, 1);
-                x.z &= byte_mask(keep, 2);
-                x.w &= byte_mask(keep, 3);
-            }
-            E = __builtin_amdgcn_udot4(x.x, 0x00010001u, E, false);
-            O = __builtin_amdgcn_udot4(x.x, 0x01000100u, O, false);
-            E = __builtin_amdgcn_udot4(x.y, 0x00010001u, E, false);
-            O = __builtin_amdgcn_udot4(x.y, 0x01000100u, O, false);
-            E = __builtin_amdgcn_udot4(x.z, 0x00010001u, E, false);
-            O = __builtin_amdgcn_udot4(x.z, 0x01000100u, O, false);
-            E = __builtin_amdgcn_udot4(x.w, 0x00010001u, E, false);
-            O = __builtin_amdgcn_udot4(x.w, 0x01000100u, O, false);
-        }
-        const uint32_t s = L ? fold64((uint64_t)E + ((uint64_t)O << 8)) : 0u;
+        if (nx < p.n && L) short_issue(p.base + nx * p.stride, L, w);   // the next packet in flight
+        const uint64_t start = p.base + i * p.stride;
+        const uint32_t s = short_sum(v, start, L);
         const uint32_t m = (start & 1) ? swap16(s) : s;   // odd start: P = swap16(fold(M))
         p.out[i] = (uint16_t)~fold64((uint64_t)pseudo<MODE>(p, i, L) + m);
         i = nx;

@@ -168,6 +168,24 @@ def test_packed_var_windows(dev, inet_oracle, mode, lead, inet_kernel):
     assert np.array_equal(got, oracle_batch(inet_oracle, mode, arena, off, ln, a))
 
 
+@pytest.mark.parametrize("mode", MODES)
+def test_short_var_packets(dev, inet_oracle, mode, inet_kernel):
+    """Variable batches of packets of 0..64 B at scattered and overlapping offsets (IP headers of a
+    TX batch; the stream kernel's lane-per-packet windows), one window with a longer packet (its
+    flat path), every alignment."""
+    rng = np.random.default_rng(300 + len(mode))
+    n = 64 * 40 + 5
+    ln = rng.integers(0, 65, n).astype(np.uint32)
+    ln[::97] = 64
+    ln[64 * 7 + 3] = 65                                     # one window on the flat path
+    arena = rng.integers(0, 256, 1 << 20, dtype=np.uint8)
+    off = rng.integers(0, arena.size - 80, n).astype(np.uint64)
+    addr = rng.integers(0, 2**32, 2 * n, dtype=np.uint64).astype(np.uint32)
+    a = None if mode == "ip" else addr
+    got = run_batch_dev(dev, mode, arena, off, ln, a)
+    assert np.array_equal(got, oracle_batch(inet_oracle, mode, arena, off, ln, a))
+
+
 def test_quirks(dev, inet_oracle, inet_kernel):
     """nstack-specific results: all-zero data (acc = 0xffff start), sums that are a nonzero
     multiple of 0xffff, the htons(len) truncation above 64 KiB, and headers that verify to 0."""

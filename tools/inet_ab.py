@@ -57,8 +57,10 @@ def main():
     m = a.imix_frames
     rng = np.random.default_rng(7)
     lens = rng.permutation(np.tile(np.array([64] * 7 + [576] * 4 + [1518], dtype=np.int64), (m + 11) // 12)[:m])
-    for name, offs, span in (("imix packed", np.concatenate([[0], np.cumsum(lens)[:-1]]), int(lens.sum())),
-                             ("imix slots", np.arange(m, dtype=np.int64) * 1536, m * 1536)):
+    cases = [("imix packed", lens, np.concatenate([[0], np.cumsum(lens)[:-1]]), int(lens.sum())),
+             ("imix slots", lens, np.arange(m, dtype=np.int64) * 1536, m * 1536),
+             ("hdr 20 B", np.full(m, 20, dtype=np.int64), 14 + np.arange(m, dtype=np.int64) * 1518, m * 1518)]
+    for name, lens, offs, span in cases:
         if span > (200 << 30):
             continue
         arena = torch.empty(span + 64, dtype=torch.uint8, device=dev)
