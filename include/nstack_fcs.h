@@ -31,8 +31,8 @@
  *             device memory, so there is no host answer to give.
  *   host forms (ether_fcs_batch_host, _fixed_host, _tx_host, _tx_batch_host, _verify_host): any
  *             other failure of the GPU step (a HIP error, a lost completion, the 10 s timeout, an
- *             allocation failure) is answered by the library's own host CRC (fcs_host_crc.cpp,
- *             slice-by-16, not a test oracle), so the results are the reference's and the call
+ *             allocation failure) is answered by the library's own host CRC (fcs_host_crc32,
+ *             fcs_host_crc.cpp; not a test oracle), so the results are the reference's and the call
  *             returns 0 (verify: the bad count). Each such call is counted in
  *             fcs_engine_host_batches(), the first is reported on stderr, and fcs_last_error() says
  *             "<form> answered by the host CRC after: <the GPU error>". A failed GPU step never leaves
@@ -146,6 +146,14 @@ int ether_fcs_verify_fixed_dev(const void *base, uint64_t stride, uint32_t len, 
 int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
                               const uint32_t *len, uint8_t *ok, uint64_t n);
 
+/* ---- the library's own host CRC (never the GPU) ----
+ * ether_fcs(data, bsize) computed on the calling CPU: carry-less folding (PCLMULQDQ, chosen at
+ * run time; about 10 GB/s per core) or slice-by-16 tables, both derived from the polynomial at run
+ * time (fcs_host_crc.cpp). It is what the failure paths above answer with and what the TX queue
+ * computes batches below its GPU minimum with (nstack_txq.h, fcs_txq_set_host_max). Exported so
+ * callers and tests can see the exact function those paths use; no GPU form falls back to it. */
+uint32_t fcs_host_crc32(const void *data, size_t bsize);
+
 /* ---- pinned host memory for zero-copy-staging callers (optional) ----
  * Pinned, device-mapped, portable host memory. TX and verify batches of up to 64 MiB in it are
  * read by the kernel in place. Release it with fcs_host_free only (the engine keeps the range's
@@ -190,6 +198,9 @@ int fcs_debug_fixed_route(uint64_t base, uint64_t stride, uint32_t len, uint64_t
 /* Test introspection: the kernel the process's last fixed-length launch actually launched, recorded
  * by the launcher in the branch that launches it: "<name as above>/<workgroup threads>", or "none". */
 int fcs_debug_last_fixed_launch(char *out, uint64_t cap);
+/* Test introspection: device-wide synchronisations the engine has issued since load. The paths that
+ * run after a failed call set a kernel aside (a retired stream that may never finish) issue none. */
+uint64_t fcs_debug_device_syncs(void);
 /* Test introspection: copy the constant tables the kernel stages into LDS (GF(2) operators of
  * the CRC, built on the host once; no frame data involved). Returns words written or -errno. */
 int fcs_tables_blob(uint32_t *out, uint64_t words);

@@ -37,12 +37,13 @@ extern "C" {
 
 typedef struct fcs_rxq fcs_rxq_t;
 
-/* struct ether_hdr of the reference (src/nstack_ether.h): h_proto in host order on return. */
+/* struct ether_hdr of the reference (src/nstack_ether.h:54-58), packed like it, so a caller's
+ * struct ether_hdr * converts without an alignment change: h_proto in host order on return. */
 struct fcs_ether_hdr {
     uint8_t h_dst[6];
     uint8_t h_src[6];
     uint16_t h_proto;
-};
+} __attribute__((packed));
 
 #define FCS_RXQ_TRAILER 1u   /* frames carry their 4-byte FCS: verify on the GPU, strip it */
 

@@ -9,8 +9,9 @@
  *
  * fcs_txq_send() keeps that contract per call — same frame bytes, same return value (bytes sent
  * or -errno), same -EMSGSIZE rule — but frames from all producer threads are assembled into one
- * pinned batch arena, their FCSs are computed together on the GPU (ether_fcs_tx_host), and the
- * batch leaves through one sink call (sendmmsg for the provided sinks). A batch is flushed when it
+ * pinned batch arena, their FCSs are computed together on the GPU (ether_fcs_tx_batch_host; where
+ * the GPU does not pay, on the host: see fcs_txq_set_host_max), and the batch leaves through one
+ * sink call (sendmmsg for the provided sinks). A batch is flushed when it
  * holds max_batch frames, or the flusher is idle and the batch's oldest frame has lingered
  * flush_usec microseconds (0: leave as soon as the flusher is free). The queue double-buffers:
  * producers fill batch k+1 while batch k is on the GPU/wire, so batches grow with the offered
@@ -72,6 +73,22 @@ const char *fcs_txq_last_error(const fcs_txq_t *q);
 /* Batches (and their frames) whose FCSs the host CRC computed because the GPU step failed; the
  * frames were sent all the same. 0 on a healthy GPU. Any pointer may be NULL. */
 void fcs_txq_fallbacks(const fcs_txq_t *q, uint64_t *host_batches, uint64_t *host_frames);
+/* Where the GPU does not pay, the library's host CRC (fcs_host_crc32) computes the FCS, by design:
+ * - fcs_txq_send (synchronous) callers compute their own frame's FCS while assembling it: a GPU step
+ *   costs a launch and a completion round trip (9-12 us on MI355X) whatever it holds, synchronous
+ *   callers put one frame each in a batch, and the host CRC takes about 0.08 us per 1518-B frame on
+ *   the caller's own core;
+ * - fire-and-forget frames (fcs_txq_send_async) of one batch take one GPU step when their FCS-covered
+ *   bytes total more than `bytes`, the GPU minimum; at or below it the flusher computes them.
+ * The default GPU minimum (512 KiB, the crossover tools/tx_crossover.c measured: one GPU step against
+ * one host thread over the same frames) can be overridden per process by NSTACK_TXQ_HOST_MAX_BYTES;
+ * 0 sends every frame, synchronous ones too, to the GPU. Returns the previous value (0 for NULL). */
+uint64_t fcs_txq_set_host_max(fcs_txq_t *q, uint64_t bytes);
+/* Batches that took no GPU step and frames whose FCS the host CRC computed, both by design (callers'
+ * own frames and batches at or below the GPU minimum; not failures: those are fcs_txq_fallbacks), and
+ * batches whose FCSs a GPU step computed. Any pointer may be NULL. */
+void fcs_txq_small_batches(const fcs_txq_t *q, uint64_t *small_batches, uint64_t *small_frames,
+                           uint64_t *gpu_batches);
 
 /* ---- provided sinks ---- */
 /* ctx = pointer to an int file descriptor of a CONNECTED socket (e.g. a socketpair or a

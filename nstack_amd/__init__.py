@@ -22,14 +22,15 @@ __all__ = ["FcsError", "lib", "load", "ether_fcs", "fixed_dev", "batch_dev", "fi
 # Every symbol include/nstack_fcs.h declares (tests check the .so exports all of them).
 EXPORTS = [
     "ether_fcs", "fcs_engine_init", "fcs_engine_fini", "fcs_engine_device_count",
-    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "fcs_debug_fixed_route", "fcs_debug_last_fixed_launch", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
+    "fcs_last_error", "fcs_engine_version", "fcs_engine_set_var_threshold", "fcs_engine_host_fallbacks", "fcs_engine_host_batches", "fcs_debug_stream_listed", "fcs_debug_stream_unit_frames", "fcs_debug_fixed_route", "fcs_debug_last_fixed_launch", "fcs_debug_device_syncs", "ether_fcs_batch_dev", "ether_fcs_fixed_dev",
     "ether_fcs_batch_host", "ether_fcs_fixed_host", "ether_fcs_tx_host", "ether_fcs_tx_batch_host", "ether_fcs_verify_dev",
     "ether_fcs_verify_fixed_dev", "ether_fcs_verify_host", "fcs_host_alloc",
     "fcs_host_free", "fcs_fill_splitmix64_dev", "fcs_read_stream_dev", "fcs_timed_fixed_dev",
     "fcs_tables_blob", "fcs_engine_stats", "fcs_engine_host_stats", "fcs_shard_plan", "fcs_dma_stream_dev", "fcs_stream_load_dev",
+    "fcs_host_crc32",
     # include/nstack_txq.h — batched TX call site
     "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error", "fcs_txq_fallbacks",
-    "fcs_txq_sink_fd", "fcs_txq_sink_packet",
+    "fcs_txq_set_host_max", "fcs_txq_small_batches", "fcs_txq_sink_fd", "fcs_txq_sink_packet",
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
     # include/nstack_inet.h — batched Internet checksums (opt-in)
@@ -71,7 +72,8 @@ def load_faults() -> ctypes.CDLL:
     """The TEST-ONLY fault-hook build (-DFCS_FAULT_HOOK), bound like the product library plus its
     fcs_debug_fail_next / fcs_debug_timeout_next (drop-in) and fcs_debug_fail_batches /
     fcs_debug_late_batches (host batch calls: fail before the launch / give up after it with the
-    kernel in flight) hooks. Its engine state is separate from the product library's. Nothing in the
+    kernel in flight) and fcs_debug_hold_small (the next small-batch launch waits behind a kernel
+    that stays busy until a pinned host word turns nonzero) hooks. Its engine state is separate from the product library's. Nothing in the
     product loads it."""
     global _faults
     if _faults is None:
@@ -88,6 +90,8 @@ def load_faults() -> ctypes.CDLL:
         L.fcs_debug_retired.argtypes = []
         L.fcs_debug_batch_faults_left.restype = ctypes.c_int
         L.fcs_debug_batch_faults_left.argtypes = []
+        L.fcs_debug_hold_small.restype = None
+        L.fcs_debug_hold_small.argtypes = [ctypes.c_void_p]
         _faults = L
     return _faults
 
@@ -128,6 +132,7 @@ def _bind(path: str) -> ctypes.CDLL:
         "fcs_debug_stream_unit_frames": (u32, []),
         "fcs_debug_fixed_route": (i32, [u64, u64, u32, u64, c.c_char_p, u64]),
         "fcs_debug_last_fixed_launch": (i32, [c.c_char_p, u64]),
+        "fcs_debug_device_syncs": (u64, []),
         "fcs_engine_host_stats": (None, [c.POINTER(u64)] * 2),
         "fcs_shard_plan": (i32, [vp, u64, u32, vp]),
         "fcs_dma_stream_dev": (i32, [vp, u64, vp, vp]),
@@ -141,6 +146,9 @@ def _bind(path: str) -> ctypes.CDLL:
         "fcs_txq_timing": (None, [vp] + [c.POINTER(u64)] * 5),
         "fcs_txq_last_error": (c.c_char_p, [vp]),
         "fcs_txq_fallbacks": (None, [vp, c.POINTER(u64), c.POINTER(u64)]),
+        "fcs_txq_set_host_max": (u64, [vp, u64]),
+        "fcs_txq_small_batches": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
+        "fcs_host_crc32": (u32, [vp, c.c_size_t]),
         "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
         "fcs_txq_sink_packet": (None, [vp, vp, vp, vp, u32]),
         "fcs_pcap_scan": (i32, [c.c_char_p, c.POINTER(u64), c.POINTER(u64), c.POINTER(u32), c.POINTER(u64)]),
@@ -385,9 +393,11 @@ class TxQueue:
     threads are FCS'd together on the GPU and leave in one sendmmsg per batch."""
 
     def __init__(self, src_mac: bytes, fd: int, max_batch: int = 256, flush_usec: int = 0, sink=None,
-                 sink_ctx=None, lib=None):
+                 sink_ctx=None, lib=None, host_max=None):
         """sink: None (fcs_txq_sink_fd on fd) or a C sink function pointer (e.g. fcs_txq_sink_packet)
-        with sink_ctx its context pointer; lib: the library to use (default: the product)."""
+        with sink_ctx its context pointer; lib: the library to use (default: the product); host_max:
+        the GPU minimum in covered bytes (fcs_txq_set_host_max; None keeps the default, 0 sends every
+        batch to the GPU)."""
         L = self._L = lib or load()
         self._fd = ctypes.c_int(fd)
         self._mac = (ctypes.c_uint8 * 6)(*src_mac)
@@ -396,6 +406,8 @@ class TxQueue:
         self._q = L.fcs_txq_create(self._mac, max_batch, flush_usec, sink, sink_ctx)
         if not self._q:
             raise FcsError(-errno.EINVAL, "fcs_txq_create")
+        if host_max is not None:
+            L.fcs_txq_set_host_max(self._q, host_max)
 
     def send(self, dst: bytes, proto: int, payload: bytes) -> int:
         return self._L.fcs_txq_send(self._q, bytes(dst), proto, bytes(payload), len(payload))
@@ -417,6 +429,17 @@ class TxQueue:
         hb, hf = ctypes.c_uint64(0), ctypes.c_uint64(0)
         self._L.fcs_txq_fallbacks(self._q, ctypes.byref(hb), ctypes.byref(hf))
         return int(hb.value), int(hf.value)
+
+    def set_host_max(self, nbytes: int) -> int:
+        """Set the GPU minimum (covered bytes); returns the previous value."""
+        return int(self._L.fcs_txq_set_host_max(self._q, nbytes))
+
+    def paths(self):
+        """(small_batches, small_frames, gpu_batches): batches at or below the GPU minimum (host CRC by
+        design) and batches the GPU computed."""
+        sb, sf, gb = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._L.fcs_txq_small_batches(self._q, ctypes.byref(sb), ctypes.byref(sf), ctypes.byref(gb))
+        return int(sb.value), int(sf.value), int(gb.value)
 
     def last_error(self) -> str:
         """Text of the most recent failed GPU step ("" if none)."""

@@ -22,6 +22,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <string>
 #include <thread>
 #include <vector>
@@ -133,12 +134,26 @@ struct Injector {
 Injector g_inject_batch, g_inject_late;
 bool injected_batch_fault() { return g_inject_batch.take(); }
 bool injected_late_fault() { return g_inject_late.take(); }
+// ... and the next small-batch launch (TX/verify in mapped memory) is queued behind hold_kernel,
+// which keeps its stream busy until the host word (fcs_host_alloc memory) turns nonzero or 20 s
+// pass: a kernel that really stays in flight after its call gave up (fcs_debug_hold_small).
+std::atomic<const uint32_t *> g_hold_word{nullptr};
+const uint32_t *take_hold() { return g_hold_word.exchange(nullptr); }
 #else
 inline bool injected_fault() { return false; }
 inline bool injected_timeout() { return false; }
 inline bool injected_batch_fault() { return false; }
 inline bool injected_late_fault() { return false; }
+inline const uint32_t *take_hold() { return nullptr; }
 #endif
+
+// Device-wide synchronisations the engine has issued (fcs_debug_device_syncs): a hung kernel on a
+// retired stream would block every one of them, so the paths a failed call leaves behind avoid them.
+std::atomic<uint64_t> g_device_syncs{0};
+hipError_t device_sync() {
+    g_device_syncs.fetch_add(1, std::memory_order_relaxed);
+    return hipDeviceSynchronize();
+}
 
 // Host batch calls (ether_fcs_*_host, and the TX/RX queues' batches, which go through them)
 // answered by the host CRC because their GPU step failed.
@@ -547,6 +562,32 @@ void quarantine(DevState *ds, hipStream_t st, std::initializer_list<void *> host
         if (d) ds->q_dev.push_back(d);
 }
 
+// hipFree and hipHostFree synchronise the device. While a retired stream may still run a kernel
+// (one that never finishes would block them for good), arrays that a growth path replaces join the
+// quarantine instead of being freed; no live kernel uses them any more either way.
+bool quarantine_busy(DevState *ds) {
+    std::lock_guard<std::mutex> lk(ds->q_mu);
+    bool busy = false;
+    for (hipStream_t st : ds->q_streams)
+        if (hipStreamQuery(st) == hipErrorNotReady) {
+            busy = true;
+            break;
+        }
+    (void)hipGetLastError();
+    return busy;
+}
+
+void release(DevState *ds, std::initializer_list<void *> host, std::initializer_list<void *> dev = {}) {
+    if (quarantine_busy(ds)) {
+        quarantine(ds, nullptr, host, dev);
+        return;
+    }
+    for (void *h : host)
+        if (h) (void)hipHostFree(h);
+    for (void *d : dev)
+        if (d) (void)hipFree(d);
+}
+
 // A host batch call failed after launching on the pipeline (a chunk's kernel or copies may still
 // run): its streams, events and staging are set aside and recreated on next use, so a late kernel or
 // D2H copy cannot write into staging that serves a later call. Caller holds pipe_mu.
@@ -575,8 +616,7 @@ int ensure_pipe(DevState *ds, uint64_t bytes, uint64_t frames) {
     }
     if (bytes > pp.cap_bytes) {
         for (int b = 0; b < Pipe::kDepth; b++) {
-            if (pp.d_in[b]) hipFree(pp.d_in[b]);
-            if (pp.h_in[b]) hipHostFree(pp.h_in[b]);
+            release(ds, {pp.h_in[b]}, {pp.d_in[b]});
             pp.d_in[b] = nullptr;
             pp.h_in[b] = nullptr;
         }
@@ -589,10 +629,7 @@ int ensure_pipe(DevState *ds, uint64_t bytes, uint64_t frames) {
     }
     if (frames > pp.cap_frames) {
         for (int b = 0; b < Pipe::kDepth; b++) {
-            if (pp.d_off[b]) hipFree(pp.d_off[b]);
-            if (pp.d_out[b]) hipFree(pp.d_out[b]);
-            if (pp.h_off[b]) hipHostFree(pp.h_off[b]);
-            if (pp.h_out[b]) hipHostFree(pp.h_out[b]);
+            release(ds, {pp.h_off[b], pp.h_out[b]}, {pp.d_off[b], pp.d_out[b]});
             pp.d_off[b] = nullptr; pp.d_out[b] = nullptr;
             pp.h_off[b] = nullptr; pp.h_out[b] = nullptr;
         }
@@ -896,9 +933,10 @@ int ensure_small(DevState *ds) {
         *ds->tx_flag = 0;
     }
     if (!ds->tx_dcount) {
+        // zeroed on tx_stream itself, ahead of every launch on it: a device-wide sync here would wait
+        // on a retired stream whose kernel may never finish (the case retire_small isolates)
         HIPTRY(hipMalloc(&ds->tx_dcount, 64), "hipMalloc(small batch counter)");
-        HIPTRY(hipMemset(ds->tx_dcount, 0, 64), "hipMemset(small batch counter)");
-        HIPTRY(hipDeviceSynchronize(), "hipDeviceSynchronize");   // zeroed before any launch on tx_stream
+        HIPTRY(hipMemsetAsync(ds->tx_dcount, 0, 64, ds->tx_stream), "hipMemsetAsync(small batch counter)");
         ds->tx_count = 0;
     }
     return 0;
@@ -939,13 +977,11 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
     int rc = ensure_small(ds);
     if (rc) return rc;
     if (n > ds->tx_cap) {
-        if (ds->tx_len) HIPTRY(hipHostFree(ds->tx_len), "hipHostFree(tx len)");
-        if (ds->tx_out) HIPTRY(hipHostFree(ds->tx_out), "hipHostFree(tx out)");
-        if (ds->tx_off) HIPTRY(hipHostFree(ds->tx_off), "hipHostFree(tx off)");
+        const uint64_t cap = std::max<uint64_t>({n, 2 * ds->tx_cap, 4096});   // few growths, few kept arrays
+        release(ds, {ds->tx_len, ds->tx_out, ds->tx_off});
         ds->tx_len = ds->tx_out = nullptr;
         ds->tx_off = nullptr;
         ds->tx_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(n, 4096);
         HIPTRY(hipHostMalloc(&ds->tx_len, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx len)");
         HIPTRY(hipHostMalloc(&ds->tx_out, cap * 4, hipHostMallocMapped), "hipHostMalloc(tx out)");
         HIPTRY(hipHostMalloc(&ds->tx_off, cap * 8, hipHostMallocMapped), "hipHostMalloc(tx off)");
@@ -961,6 +997,10 @@ int run_tx_zero_copy(DevState *ds, uint8_t *base, uint64_t bytes, uint64_t strid
     }
     bool small = n <= fcs::kTxSmallMax;
     for (uint64_t i = 0; small && i < n; i++) small = len[i] <= fcs::kOneBytes;
+    if (const uint32_t *hw = take_hold()) {   // FCS_FAULT_HOOK builds only
+        const uint32_t *dw = reinterpret_cast<const uint32_t *>(pinned_dev_ptr(hw, 4));
+        if (dw) HIPTRY(fcs::launch_hold(dw, 20ull * 100000000ull, ds->tx_stream), "launching the hold kernel");
+    }
     uint64_t v = 0;
     if (small) {   // everything the kernel needs rides in its arguments; it writes the FCSs to tx_out
         const std::vector<uint32_t> &kinit = kinit_table();
@@ -1103,14 +1143,12 @@ int64_t run_verify_zero_copy(DevState *ds, const uint8_t *darena, uint64_t arena
     int rc = ensure_small(ds);
     if (rc) return rc;
     if (n > ds->vz_cap) {
-        if (ds->vz_off) HIPTRY(hipHostFree(ds->vz_off), "hipHostFree(verify off)");
-        if (ds->vz_len) HIPTRY(hipHostFree(ds->vz_len), "hipHostFree(verify len)");
-        if (ds->vz_ok) HIPTRY(hipHostFree(ds->vz_ok), "hipHostFree(verify ok)");
+        const uint64_t cap = std::max<uint64_t>({n, 2 * ds->vz_cap, 4096});
+        release(ds, {ds->vz_off, ds->vz_len, ds->vz_ok});
         ds->vz_off = nullptr;
         ds->vz_len = nullptr;
         ds->vz_ok = nullptr;
         ds->vz_cap = 0;
-        const uint64_t cap = std::max<uint64_t>(n, 4096);
         HIPTRY(hipHostMalloc(&ds->vz_off, cap * 8, hipHostMallocMapped), "hipHostMalloc(verify off)");
         HIPTRY(hipHostMalloc(&ds->vz_len, cap * 4, hipHostMallocMapped), "hipHostMalloc(verify len)");
         HIPTRY(hipHostMalloc(&ds->vz_ok, cap, hipHostMallocMapped), "hipHostMalloc(verify ok)");
@@ -1383,7 +1421,7 @@ int run_staged(DevState *ds, const void *data, size_t bsize, uint32_t *crc) {
         ds->one_seq = 0;
     }
     if (bsize > ds->one_cap) {
-        if (ds->one_h) (void)hipHostFree(ds->one_h);
+        release(ds, {ds->one_h});
         ds->one_h = ds->one_hd = nullptr;
         ds->one_cap = 0;
         const uint64_t cap = std::max<uint64_t>(4096, bsize + 64);
@@ -1614,7 +1652,7 @@ static void destroy_state(DevState *ds) {
         if (L.st) hipStreamDestroy(L.st);
         if (L.flag) hipHostFree(L.flag);
     }
-    if (!ds->q_streams.empty() || !ds->q_host.empty() || !ds->q_dev.empty()) (void)hipDeviceSynchronize();
+    if (!ds->q_streams.empty() || !ds->q_host.empty() || !ds->q_dev.empty()) (void)device_sync();
     for (hipStream_t q : ds->q_streams) hipStreamDestroy(q);
     for (void *h : ds->q_host) hipHostFree(h);
     for (void *d : ds->q_dev) hipFree(d);
@@ -1722,6 +1760,7 @@ int ether_fcs_batch_dev(const void *arena, uint64_t arena_bytes, const uint64_t 
 
 int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t *off,
                          const uint32_t *len, uint32_t *out, uint64_t n) {
+    t_host_answered = false;   // early returns below must not report the previous call
     if (n == 0) return 0;
     if (!arena || !off || !len || !out) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
@@ -1731,6 +1770,7 @@ int ether_fcs_batch_host(const void *arena, uint64_t arena_bytes, const uint64_t
 
 int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64_t n,
                          uint32_t *out) {
+    t_host_answered = false;   // early returns below must not report the previous call
     if (n == 0) return 0;
     if (!base || !out) return fail(EINVAL, "null pointer");
     if (n > 1 && stride < len) return fail(EINVAL, "stride %llu < len %u", (unsigned long long)stride, len);
@@ -1740,6 +1780,7 @@ int ether_fcs_fixed_host(const void *base, uint64_t stride, uint32_t len, uint64
 }
 
 int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t n) {
+    t_host_answered = false;   // early returns below must not report the previous call
     if (n == 0) return 0;
     if (!base || !len) return fail(EINVAL, "null pointer");
     for (uint64_t i = 0; i < n; i++)
@@ -1763,6 +1804,7 @@ int ether_fcs_tx_host(void *base, uint64_t stride, const uint32_t *len, uint64_t
 
 int ether_fcs_tx_batch_host(void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
                             uint64_t n) {
+    t_host_answered = false;   // early returns below must not report the previous call
     if (n == 0) return 0;
     if (!arena || !off || !len) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 4, __func__)) return rc;
@@ -1810,6 +1852,7 @@ int ether_fcs_verify_fixed_dev(const void *base, uint64_t stride, uint32_t len, 
 
 int64_t ether_fcs_verify_host(const void *arena, uint64_t arena_bytes, const uint64_t *off, const uint32_t *len,
                               uint8_t *ok, uint64_t n) {
+    t_host_answered = false;   // early returns below must not report the previous call
     if (n == 0) return 0;
     if (!arena || !off || !len || !ok) return fail(EINVAL, "null pointer");
     if (int rc = check_frames(off, len, n, arena_bytes, 0, __func__)) return rc;
@@ -1914,7 +1957,7 @@ int64_t fcs_debug_stream_listed(void) {
     if (!ds) return -1;
     DeviceGuard dg(ds->dev);   // read on the device that ran the launch
     HIPTRY(dg.err, "hipSetDevice");
-    HIPTRY(hipDeviceSynchronize(), "hipDeviceSynchronize");
+    HIPTRY(device_sync(), "hipDeviceSynchronize");
     uint32_t v = 0;
     HIPTRY(hipMemcpy(&v, ds->d_last_listed, 4, hipMemcpyDeviceToHost), "reading the unit-list length");
     return (int64_t)v;
@@ -1935,7 +1978,10 @@ void fcs_engine_stats(uint64_t *dropin_calls, uint64_t *dropin_retries, uint64_t
 
 uint64_t fcs_engine_host_batches(void) { return g_host_batches.load(std::memory_order_relaxed); }
 
+uint64_t fcs_debug_device_syncs(void) { return g_device_syncs.load(std::memory_order_relaxed); }
+
 #ifdef FCS_FAULT_HOOK
+void fcs_debug_hold_small(const uint32_t *word) { g_hold_word.store(word); }
 void fcs_debug_fail_next(int attempts) { g_inject_faults = attempts; }
 void fcs_debug_timeout_next(int attempts) { g_inject_timeouts = attempts; }
 void fcs_debug_fail_batches(int skip, int calls) { g_inject_batch.arm(skip, calls); }
@@ -1983,7 +2029,14 @@ void *fcs_host_alloc(uint64_t bytes) {
 
 // A kernel set aside by a failed call (quarantined stream) may still read pinned memory the caller
 // now frees: wait for the quarantined streams to drain, at most 10 s, and keep the memory mapped (a
-// leak, never a GPU page fault) if one is still busy.
+// leak, never a GPU page fault) if one is still busy. A stream that has already outlived one such
+// wait is remembered as stuck and not waited for again (the memory is kept at once), so a queue's
+// teardown after a hung kernel does not cost 10 s per array.
+namespace {
+std::mutex g_stuck_mu;
+std::set<hipStream_t> g_stuck;
+}  // namespace
+
 void fcs_host_free(void *p) {
     if (!p) return;
     std::vector<hipStream_t> busy;
@@ -1998,11 +2051,21 @@ void fcs_host_free(void *p) {
         for (auto &kv : g_alias)
             if (kv.second) take(kv.second.get());
     }
+    {
+        std::lock_guard<std::mutex> lk(g_stuck_mu);
+        for (hipStream_t st : busy)
+            if (g_stuck.count(st) && hipStreamQuery(st) == hipErrorNotReady) {
+                (void)hipGetLastError();
+                return;   // kept: a kernel known to be stuck may still read it
+            }
+    }
     const auto t0 = std::chrono::steady_clock::now();
     for (hipStream_t st : busy)
         while (hipStreamQuery(st) == hipErrorNotReady) {
             if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
                 (void)hipGetLastError();
+                std::lock_guard<std::mutex> lk(g_stuck_mu);
+                g_stuck.insert(st);
                 return;   // kept: a kernel of a failed call may still read it
             }
             std::this_thread::sleep_for(std::chrono::microseconds(50));

@@ -1,14 +1,25 @@
-// fcs_host_crc.cpp — host CRC-32 for the failure paths of the drop-in and the TX/RX queues only
-// (fcs_host_crc.hpp).
+// fcs_host_crc.cpp — the library's own host CRC-32 (fcs_host_crc.hpp): the failure answers of the
+// drop-in and the host batch forms, and the TX queue's batches below its GPU minimum.
 //
-// Slice-by-16: sixteen 256-entry tables, table k advancing a byte past k further zero bytes, so
-// one step folds 16 input bytes with 16 independent lookups. The tables are derived from the
-// reflected polynomial 0xEDB88320 (the operator the reference's nibble table folds,
-// src/ether_fcs.c:7-10); the register starts at ~0 and is complemented at the end, which is what
-// the reference's complement-folded table computes ("123456789" -> 0xCBF43926).
-// A single host thread: this path exists for correctness when no GPU answers, not for speed.
+// Two forms, one result:
+// - Carry-less folding (x86 PCLMULQDQ, chosen at run time when the CPU has it). CRC-32 is the
+//   message polynomial times x^32 modulo P, so a 128-bit block A may be replaced by any block
+//   congruent to A * x^D mod P that sits D bits later: with A = A_hi x^64 + A_lo, that is
+//   A_hi * (x^(64+D) mod P) + A_lo * (x^D mod P), two 64x32-bit carry-less products. Four
+//   accumulators fold 64 bytes per step (D = 512) and are then folded into one (D = 128); the
+//   remaining block is, modulo P, a 16-byte message of its own, so one slice-by-16 step from a zero
+//   register turns it into the CRC register, and the table loop finishes the tail.
+// - Slice-by-16 tables: sixteen 256-entry tables, table k advancing a byte past k further zero
+//   bytes, so one step folds 16 input bytes with 16 independent lookups.
+// Everything is derived at run time from the polynomial 0x04C11DB7 (reflected 0xEDB88320, the
+// operator the reference's nibble table folds, src/ether_fcs.c:7-10); the register starts at ~0
+// and is complemented at the end, which is what the reference's complement-folded table computes
+// ("123456789" -> 0xCBF43926). It is the product's own code, not the test oracle.
 #include "fcs_host_crc.hpp"
 
+#include <immintrin.h>
+
+#include <cstdlib>
 #include <cstring>
 
 namespace fcs {
@@ -38,23 +49,112 @@ inline uint32_t le32(const uint8_t *p) {
     return v;   // x86-64 and every host this library builds for are little-endian
 }
 
+// One slice-by-16 step: the register after 16 more bytes.
+inline uint32_t step16(const Slice16 &s, const uint8_t *p, uint32_t c) {
+    const uint32_t a = le32(p) ^ c, b = le32(p + 4), d = le32(p + 8), e = le32(p + 12);
+    return s.t[15][a & 0xFF] ^ s.t[14][(a >> 8) & 0xFF] ^ s.t[13][(a >> 16) & 0xFF] ^ s.t[12][a >> 24] ^
+           s.t[11][b & 0xFF] ^ s.t[10][(b >> 8) & 0xFF] ^ s.t[9][(b >> 16) & 0xFF] ^ s.t[8][b >> 24] ^
+           s.t[7][d & 0xFF] ^ s.t[6][(d >> 8) & 0xFF] ^ s.t[5][(d >> 16) & 0xFF] ^ s.t[4][d >> 24] ^
+           s.t[3][e & 0xFF] ^ s.t[2][(e >> 8) & 0xFF] ^ s.t[1][(e >> 16) & 0xFF] ^ s.t[0][e >> 24];
+}
+
+uint32_t tables_crc(const uint8_t *p, size_t n, uint32_t c) {
+    const Slice16 &s = tables16();
+    for (; n >= 16; n -= 16, p += 16) c = step16(s, p, c);
+    while (n--) c = (c >> 8) ^ s.t[0][(c ^ *p++) & 0xFFu];
+    return c;
+}
+
+// ---- carry-less folding ----
+// A 128-bit little-endian load of message bytes holds the coefficient of x^(127-k) in bit k
+// (bit-reflected), and so does a 64-bit half for x^(63-k). The carry-less product of two such
+// halves puts the coefficient of x^(126-t) in bit t: one power short, so each constant carries an
+// x^-1. Folding constant pair for distance D: low half multiplies A_hi, high half A_lo.
+uint64_t xpow_mod(unsigned n) {   // x^n mod P, bit d = coefficient of x^d
+    uint64_t v = 1;
+    for (unsigned i = 0; i < n; i++) v = (v << 1) ^ ((v & 0x80000000u) ? 0x104C11DB7ull : 0);
+    return v;
+}
+
+uint64_t reflect64(uint64_t v) {   // coefficient of x^d moves to bit 63 - d
+    uint64_t r = 0;
+    for (int d = 0; d < 32; d++)
+        if ((v >> d) & 1) r |= 1ull << (63 - d);
+    return r;
+}
+
+struct FoldK {
+    alignas(16) uint64_t k512[2], k128[2];
+    FoldK() {
+        k512[0] = reflect64(xpow_mod(64 + 512 - 1));
+        k512[1] = reflect64(xpow_mod(512 - 1));
+        k128[0] = reflect64(xpow_mod(64 + 128 - 1));
+        k128[1] = reflect64(xpow_mod(128 - 1));
+    }
+};
+
+const FoldK &fold_k() {
+    static const FoldK k;
+    return k;
+}
+
+__attribute__((target("pclmul,sse4.1"))) inline __m128i fold(__m128i x, __m128i k) {
+    return _mm_xor_si128(_mm_clmulepi64_si128(x, k, 0x00), _mm_clmulepi64_si128(x, k, 0x11));
+}
+
+// The register after n >= 64 bytes from register c (not complemented); *used = bytes consumed
+// (a multiple of 16); the caller finishes the rest with the tables.
+__attribute__((target("pclmul,sse4.1"))) uint32_t fold_crc(const uint8_t *p, size_t n, uint32_t c, size_t *used) {
+    const FoldK &K = fold_k();
+    const __m128i k512 = _mm_load_si128((const __m128i *)K.k512), k128 = _mm_load_si128((const __m128i *)K.k128);
+    __m128i x0 = _mm_loadu_si128((const __m128i *)p), x1 = _mm_loadu_si128((const __m128i *)(p + 16)),
+            x2 = _mm_loadu_si128((const __m128i *)(p + 32)), x3 = _mm_loadu_si128((const __m128i *)(p + 48));
+    x0 = _mm_xor_si128(x0, _mm_cvtsi32_si128((int)c));   // the start register enters the first word
+    size_t i = 64;
+    for (; i + 64 <= n; i += 64) {
+        x0 = _mm_xor_si128(fold(x0, k512), _mm_loadu_si128((const __m128i *)(p + i)));
+        x1 = _mm_xor_si128(fold(x1, k512), _mm_loadu_si128((const __m128i *)(p + i + 16)));
+        x2 = _mm_xor_si128(fold(x2, k512), _mm_loadu_si128((const __m128i *)(p + i + 32)));
+        x3 = _mm_xor_si128(fold(x3, k512), _mm_loadu_si128((const __m128i *)(p + i + 48)));
+    }
+    __m128i x = _mm_xor_si128(fold(x0, k128), x1);
+    x = _mm_xor_si128(fold(x, k128), x2);
+    x = _mm_xor_si128(fold(x, k128), x3);
+    for (; i + 16 <= n; i += 16) x = _mm_xor_si128(fold(x, k128), _mm_loadu_si128((const __m128i *)(p + i)));
+    alignas(16) uint8_t last[16];
+    _mm_store_si128((__m128i *)last, x);
+    *used = i;
+    return step16(tables16(), last, 0);   // the folded block is a 16-byte message from register 0
+}
+
+// NSTACK_FCS_HOST_CRC=tables selects the table form (tests run both forms through the C ABI).
+bool have_pclmul() {
+    static const bool ok = __builtin_cpu_supports("pclmul") && __builtin_cpu_supports("sse4.1") &&
+                           !(std::getenv("NSTACK_FCS_HOST_CRC") && !std::strcmp(std::getenv("NSTACK_FCS_HOST_CRC"), "tables"));
+    return ok;
+}
+
 }  // namespace
 
 uint32_t host_crc32(const void *data, size_t bsize) {
-    const Slice16 &s = tables16();
     const uint8_t *p = static_cast<const uint8_t *>(data);
     uint32_t c = 0xFFFFFFFFu;
-    while (bsize >= 16) {
-        const uint32_t a = le32(p) ^ c, b = le32(p + 4), d = le32(p + 8), e = le32(p + 12);
-        c = s.t[15][a & 0xFF] ^ s.t[14][(a >> 8) & 0xFF] ^ s.t[13][(a >> 16) & 0xFF] ^ s.t[12][a >> 24] ^
-            s.t[11][b & 0xFF] ^ s.t[10][(b >> 8) & 0xFF] ^ s.t[9][(b >> 16) & 0xFF] ^ s.t[8][b >> 24] ^
-            s.t[7][d & 0xFF] ^ s.t[6][(d >> 8) & 0xFF] ^ s.t[5][(d >> 16) & 0xFF] ^ s.t[4][d >> 24] ^
-            s.t[3][e & 0xFF] ^ s.t[2][(e >> 8) & 0xFF] ^ s.t[1][(e >> 16) & 0xFF] ^ s.t[0][e >> 24];
-        p += 16;
-        bsize -= 16;
+    if (bsize >= 64 && have_pclmul()) {
+        size_t used = 0;
+        c = fold_crc(p, bsize, c, &used);
+        p += used;
+        bsize -= used;
     }
-    while (bsize--) c = (c >> 8) ^ s.t[0][(c ^ *p++) & 0xFFu];
-    return ~c;
+    return ~tables_crc(p, bsize, c);
+}
+
+uint32_t host_crc32_tables(const void *data, size_t bsize) {
+    return ~tables_crc(static_cast<const uint8_t *>(data), bsize, 0xFFFFFFFFu);
 }
 
 }  // namespace fcs
+
+extern "C" uint32_t fcs_host_crc32(const void *data, size_t bsize) {
+    if (!data && bsize) return 0;   // no error channel: a null buffer has no CRC
+    return fcs::host_crc32(data, bsize);
+}

@@ -1,4 +1,5 @@
-// fcs_host_crc.hpp — the last resort of the reference-contract call sites: CRC-32 on the host CPU.
+// fcs_host_crc.hpp — the library's host CRC-32: the last resort of the reference-contract call sites,
+// and the TX queue's answer for batches below its GPU minimum (fcs_txq.cpp).
 //
 // the reference ether_fcs (src/ether_fcs.c:4-19) cannot fail and has no
 // error channel, and ether_send / ether_receive (src/linux/ether.c:180-272) never fail for FCS
@@ -15,7 +16,10 @@
 
 namespace fcs {
 
-// ether_fcs(data, bsize) of the reference: CRC-32/ISO-HDLC, 0 for bsize == 0.
+// ether_fcs(data, bsize) of the reference: CRC-32/ISO-HDLC, 0 for bsize == 0. Carry-less folding
+// when the CPU has PCLMULQDQ, else the tables.
 uint32_t host_crc32(const void *data, size_t bsize);
+// The same CRC through the slice-by-16 tables only (the form without PCLMULQDQ; tests compare both).
+uint32_t host_crc32_tables(const void *data, size_t bsize);
 
 }  // namespace fcs

@@ -2675,6 +2675,17 @@ __global__ __launch_bounds__(256) void read_stream_kernel(const u32x4 *__restric
 // Completion signal for small host batches: launched behind the FCS kernel on the same stream,
 // it stores `v` into a device-mapped host word, on which the host spins instead of synchronising
 // the stream (cuts the hipStreamSynchronize wake-up from the round trip).
+// Test-only (the fault-hook build's fcs_debug_hold_small): one lane waits until the host stores a
+// nonzero value into the mapped word, or until `ticks` of the 100 MHz constant clock have passed, so
+// every wave reaches its exit. System-scope atomic loads: vector loads that bypass the caches.
+__global__ void hold_kernel(const uint32_t *word, uint64_t ticks) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = wall_clock64();
+    while (__hip_atomic_load(word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0u &&
+           wall_clock64() - t0 < ticks)
+        __builtin_amdgcn_s_sleep(64);
+}
+
 __global__ void signal_kernel(uint64_t *flag, uint64_t v) {
     if (threadIdx.x == 0) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -3031,6 +3042,12 @@ hipError_t launch_fixed_route(const FixedRoute &r, const KParams &p, int grid, h
         break;
     }
 #undef FCS_GO
+    return hipGetLastError();
+}
+
+hipError_t launch_hold(const uint32_t *word, uint64_t ticks, hipStream_t st) {
+    (void)hipGetLastError();
+    hipLaunchKernelGGL(hold_kernel, dim3(1), dim3(64), 0, st, word, ticks);
     return hipGetLastError();
 }
 

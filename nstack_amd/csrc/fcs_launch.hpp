@@ -410,6 +410,9 @@ hipError_t launch_fixed_route(const FixedRoute &r, const KParams &p, int grid, h
 // threads/item fields as launched. Zero-initialised before any.
 FixedRoute last_fixed_launch();
 hipError_t launch_signal(uint64_t *flag, uint64_t v, hipStream_t st);
+// Test-only: a one-lane kernel that waits for a nonzero mapped host word or `ticks` of the 100 MHz
+// constant clock, whichever comes first (fcs_debug_hold_small).
+hipError_t launch_hold(const uint32_t *word, uint64_t ticks, hipStream_t st);
 hipError_t launch_one(const OneArgs &a, hipStream_t st);
 hipError_t launch_tx_small(const TxSmallArgs &a, hipStream_t st);
 hipError_t launch_small_list(const ListArgs &a, hipStream_t st);

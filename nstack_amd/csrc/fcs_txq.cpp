@@ -10,6 +10,18 @@
 // frames still leave. The engine never leaves a kernel that can write into the arena after a failed
 // call (its results go through the library's own mapped memory), so arenas are always reused.
 //
+// Where the GPU does not pay, the host CRC (fcs_host_crc.cpp, carry-less folding, ~18 GB/s on one
+// MI355X host core) computes the FCS by design (counted in fcs_txq_small_batches, not as a failure):
+// - a synchronous caller (fcs_txq_send) computes its own frame's FCS in enqueue: it blocks for the
+//   batch anyway, the frame is hot in its core's cache, and the callers run in parallel; a GPU step
+//   (a launch and a completion round trip, 9-12 us) for the few frames synchronous callers put in a
+//   batch is slower than the reference's per-frame CRC (profiles/r06_txq_vs_reference.jsonl);
+// - fire-and-forget frames (fcs_txq_send_async) go to the GPU in one step per batch when their
+//   covered bytes exceed host_max, the GPU minimum; at or below it the flusher computes them. The
+//   default is the crossover measured on MI355X boxes (tools/tx_crossover.c: one GPU step against
+//   one host thread over the same frames, profiles/r06_tx_crossover.jsonl).
+// host_max 0 sends every frame, synchronous ones too, to the GPU step.
+//
 // Producers reserve slots with one atomic add on a reservation word, and the open batch is split
 // into up to 16 shards, each with its own word on its own cache line: a thread reserves in its
 // home shard (threads are dealt homes round-robin) and moves to higher shards only when that one
@@ -29,6 +41,7 @@
 #include <mutex>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/nstack_fcs.h"
@@ -45,6 +58,11 @@ constexpr uint32_t kSlot = 1518;        // ETHER_MAXLEN + ETHER_FCS_LEN: largest
 constexpr uint32_t kStride = 1536;      // arena slot pitch: whole cache lines, so producers filling
                                         // neighbouring slots never share a line
 constexpr uint32_t kMaxBatch = 65536;
+// Batches of at most this many covered bytes take the host CRC (see the file comment): from 128
+// frames up, one GPU step over n 1514-B frames in pinned memory takes about 15 + 0.037 n us and the
+// host CRC 0.082 n us on one thread, even at about 330 frames (500 KB); 576-B frames cross at a
+// similar byte count, 60-B frames never (the GPU step's per-frame cost exceeds the host's).
+constexpr uint64_t kHostMaxDefault = 512 * 1024;
 
 using Clock = std::chrono::steady_clock;
 
@@ -68,6 +86,7 @@ int64_t now_ns() {
 struct alignas(64) SlotMeta {
     Waiter *w = nullptr;                 // null: fcs_txq_send_async
     uint32_t covered = 0;
+    bool has_fcs = false;                // the sync caller computed it (host CRC, frame cache-hot)
     std::atomic<uint64_t> ready{0};
 };
 
@@ -79,6 +98,8 @@ struct Batch {
     std::vector<uint32_t> slot;          // arena slot of each
     std::vector<uint64_t> off;           // its byte offset in the arena
     std::vector<uint32_t> covered;       // FCS-covered bytes (frame_size - 4)
+    std::vector<uint64_t> need_off;      // the frames that still need their FCS (the GPU step's list)
+    std::vector<uint32_t> need_len;
     std::vector<uint32_t> sizes;         // frame_size
     std::vector<uint8_t *> frames;
     std::vector<int> res;
@@ -100,6 +121,14 @@ struct alignas(64) Shard {
 
 // Home shard of the calling thread: threads are numbered in the order they first send.
 std::atomic<uint32_t> g_thread_count{0};
+// The calling thread's last reservation on a queue (its floor, see enqueue), keyed by the queue's
+// unique id so a queue created at a freed one's address starts from no floor.
+struct Floor {
+    uint64_t seq = 0;
+    uint32_t shard = 0;
+};
+std::atomic<uint64_t> g_queue_ids{0};
+
 uint32_t thread_number() {
     thread_local const uint32_t t = g_thread_count.fetch_add(1, std::memory_order_relaxed);
     return t;
@@ -108,6 +137,7 @@ uint32_t thread_number() {
 }  // namespace
 
 struct fcs_txq {
+    uint64_t id = g_queue_ids.fetch_add(1, std::memory_order_relaxed);   // never reused (Floor)
     uint8_t mac[6];
     uint32_t cap = 0, flush_usec = 0;
     fcs_txq_sink_fn sink = nullptr;
@@ -125,7 +155,10 @@ struct fcs_txq {
     uint64_t seq_done = 0;                // last batch handed to the sink
     uint64_t flush_target = 0;            // flush() wants batches <= this closed now
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
-    uint64_t n_host_batches = 0, n_host_frames = 0;   // batches whose FCSs the host CRC computed
+    uint64_t n_host_batches = 0, n_host_frames = 0;   // failed GPU steps answered by the host CRC
+    uint64_t n_small_batches = 0, n_small_frames = 0; // batches at most host_max bytes: host CRC by design
+    uint64_t n_gpu_batches = 0;                       // batches the GPU computed
+    std::atomic<uint64_t> host_max{kHostMaxDefault};  // see fcs_txq_set_host_max
     uint64_t ns_ready = 0, ns_gpu = 0, ns_sink = 0, ns_busy = 0;   // flusher time split
     uint64_t ns_pickup = 0;               // first frame of a batch queued -> batch closed
     std::string last_error;               // fcs_last_error() of the latest failed GPU step
@@ -223,13 +256,13 @@ void flusher(fcs_txq *q) {
         }
         // close batch seq: producers move on to b[(seq + 1) & 1], which the previous iteration
         // finished with (its results were delivered before we got here). Shards are closed from
-        // the highest down, so a thread climbing from its home shard never finds a closed shard
-        // below an open one (enqueue relies on it for per-thread order).
+        // the lowest up, so a thread that climbs from its home shard (because it is full) finds no
+        // closed shard above an open one; enqueue's per-thread floor keeps the order in any case.
         Batch *B = &q->b[seq & 1];
         Batch &N = q->b[(seq + 1) & 1];
         N.first_ns.store(0, std::memory_order_relaxed);
         uint32_t nk[kMaxShards];
-        for (uint32_t k = q->nsh; k-- > 0;) {
+        for (uint32_t k = 0; k < q->nsh; k++) {
             const uint64_t old = q->sh[k].st.exchange(st_pack(seq + 1, 0), std::memory_order_acq_rel);
             nk[k] = (closed_empty >> k) & 1 ? 0 : std::min(st_res(old), q->per);   // past per: no slot
         }
@@ -242,7 +275,8 @@ void flusher(fcs_txq *q) {
         const uint64_t pickup = f ? (uint64_t)std::max<int64_t>(0, now_ns() - f) : 0;
 
         const auto t0 = Clock::now();
-        uint32_t n = 0;
+        uint32_t n = 0, nn = 0;   // frames; frames still without an FCS (fire-and-forget ones, or all)
+        uint64_t bytes = 0;       // covered bytes of those
         for (uint32_t k = 0; k < q->nsh; k++) {
             for (uint32_t j = 0; j < nk[k]; j++, n++) {   // every reserved slot assembled by its producer
                 const uint32_t slot = k * q->per + j;
@@ -251,29 +285,40 @@ void flusher(fcs_txq *q) {
                 B->slot[n] = slot;
                 B->off[n] = (uint64_t)slot * kStride;
                 B->covered[n] = m.covered;
+                if (!m.has_fcs) {
+                    B->need_off[nn] = B->off[n];
+                    B->need_len[nn] = m.covered;
+                    bytes += m.covered;
+                    nn++;
+                }
             }
         }
         const auto t1 = Clock::now();
-        // FCS of every frame, written little-endian after its covered bytes (ether.c:262-263)
-        // the span the frames occupy (not the whole arena): it decides the engine's in-place path
-        const uint64_t span = n ? B->off[n - 1] + kStride : 0;
-        const int rc = ether_fcs_tx_batch_host(B->arena, span, B->off.data(), B->covered.data(), n);
-        const bool host = rc != 0 || fcs::last_call_host_answered();   // the engine answered a failed GPU step
+        // FCS of every frame that has none yet, written little-endian after its covered bytes
+        // (ether.c:262-263): the host CRC at or below the GPU minimum, else one GPU step
+        const bool small = bytes <= q->host_max.load(std::memory_order_relaxed);
+        int rc = 0;
+        bool host = false;
+        auto host_fcs = [&] {
+            for (uint32_t i = 0; i < nn; i++) {
+                uint8_t *f = B->arena + B->need_off[i];
+                const uint32_t c = fcs::host_crc32(f, B->need_len[i]);
+                std::memcpy(f + B->need_len[i], &c, 4);   // little-endian, as ether.c:263
+            }
+        };
+        if (nn && small) {   // below the GPU minimum: the host CRC by design, not a failure answer
+            host_fcs();
+        } else if (nn) {
+            // the span the frames occupy (not the whole arena): it decides the engine's in-place path
+            const uint64_t span = B->need_off[nn - 1] + kStride;
+            rc = ether_fcs_tx_batch_host(B->arena, span, B->need_off.data(), B->need_len.data(), nn);
+            host = rc != 0 || fcs::last_call_host_answered();   // the engine answered a failed GPU step
+        }
         if (rc != 0) {
             // no usable GPU at all: ether_send cannot fail for FCS reasons (src/linux/ether.c:234-269),
             // so the host CRC computes this batch's FCSs, counted and reported
-            for (uint32_t i = 0; i < n; i++) {
-                uint8_t *f = B->arena + B->off[i];
-                const uint32_t c = fcs::host_crc32(f, B->covered[i]);
-                std::memcpy(f + B->covered[i], &c, 4);   // little-endian, as ether.c:263
-            }
+            host_fcs();
             fcs::host_batch_answered("fcs_txq flusher", fcs_last_error());
-        }
-        if (host) {
-            std::lock_guard<std::mutex> lk(q->mu);
-            q->last_error = fcs_last_error() ? fcs_last_error() : "";
-            q->n_host_batches++;
-            q->n_host_frames += n;
         }
         const auto t2 = Clock::now();
         for (uint32_t i = 0; i < n; i++) {
@@ -285,6 +330,14 @@ void flusher(fcs_txq *q) {
         const auto t3 = Clock::now();
 
         std::lock_guard<std::mutex> lk(q->mu);
+        if (host) {
+            q->last_error = fcs_last_error() ? fcs_last_error() : "";
+            q->n_host_batches++;
+            q->n_host_frames += nn;
+        }
+        if (n && small) q->n_small_batches++;       // no GPU step: every FCS from the host CRC by design
+        if (nn && !small && !host) q->n_gpu_batches++;
+        q->n_small_frames += (n - nn) + (small ? nn : 0);
         auto ns = [](Clock::duration d) { return (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(d).count(); };
         q->ns_ready += ns(t1 - t0);
         q->ns_gpu += ns(t2 - t1);
@@ -323,6 +376,7 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
         q->nsh *= 2;
     q->per = max_batch / q->nsh;
     q->flush_usec = flush_usec;
+    if (const char *e = std::getenv("NSTACK_TXQ_HOST_MAX_BYTES")) q->host_max.store(std::strtoull(e, nullptr, 0));
     q->sink = sink;
     q->ctx = sink_ctx;
     for (int k = 0; k < 2; k++) {
@@ -339,6 +393,8 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
         B.slot.assign(max_batch, 0);
         B.off.assign(max_batch, 0);
         B.covered.assign(max_batch, 0);
+        B.need_off.assign(max_batch, 0);
+        B.need_len.assign(max_batch, 0);
         B.sizes.assign(max_batch, 0);
         B.frames.assign(max_batch, nullptr);
         B.res.assign(max_batch, 0);
@@ -351,20 +407,29 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
 }  // extern "C"
 
 namespace {
+Floor &thread_floor(const fcs_txq *q) {
+    thread_local std::unordered_map<uint64_t, Floor> floors;
+    return floors[q->id];
+}
+
 // Reserve a slot in the open batch (one fetch_add on the home shard's word, no lock), assemble the
 // frame there and mark it ready.
 // w == nullptr: fire-and-forget (the result only feeds the error counter).
 //
-// Per-thread order: a thread only climbs from its home shard to higher ones, and the flusher
-// closes shards from the highest down, so every shard a thread can still reserve in after a slot in
-// shard k of batch s is either shard >= k of batch s or a shard of a later batch. Batches leave in
-// sequence and a batch's frames leave in (shard, slot) order, so a thread's frames leave in the
-// order it queued them.
+// Per-thread order: batches leave in sequence and a batch's frames leave in (shard, slot) order, so
+// a thread's frames leave in the order it queued them if each of its reservations comes after the
+// previous one in (batch, shard) order: the thread keeps that pair per queue (its floor) and skips
+// any shard word that names an earlier batch, or the same batch and a lower shard. Climbing alone
+// does not guarantee it: a thread whose home shard was full may reserve in a higher shard of the
+// next batch, and its next frame would find its home shard open in that same batch (seen under
+// ThreadSanitizer as one frame in ~10 runs out of order before the floor existed). A fetch_add
+// result names the batch the slot is in; it can only be later than the word loaded before it.
 int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize, Waiter *w) {
     if (!q || !dst || (!buf && bsize)) return -EINVAL;
     const size_t frame_size = kHeaderLen + std::max<size_t>(bsize, kMinPayload) + kFcsLen;   // :222-224
     if (frame_size > kSlot) return -EMSGSIZE;                                                // :234-237
     const uint32_t home = thread_number() % q->nsh;
+    Floor &fl = thread_floor(q);
     uint64_t s = 0;
     uint32_t k = home;
     for (;;) {
@@ -373,6 +438,7 @@ int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf
         bool got = false;
         for (k = home; k < q->nsh && !got; k++) {
             s = q->sh[k].st.load(std::memory_order_acquire);
+            if (st_seq(s) < fl.seq || (st_seq(s) == fl.seq && k < fl.shard)) continue;   // before the last frame
             if (st_res(s) < q->per) {
                 // one fetch_add; a producer that overshoots a full shard got no slot and moves on
                 // (the flusher takes min(reserved, per))
@@ -382,6 +448,8 @@ int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf
         }
         if (got) {
             k--;
+            fl.seq = st_seq(s);
+            fl.shard = k;
             break;
         }
         // every shard from home up is full: have the flusher close the batch and wait for it
@@ -423,6 +491,13 @@ int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf
     SlotMeta &m = B.meta[slot];
     m.w = w;
     m.covered = (uint32_t)(frame_size - kFcsLen);
+    // A synchronous caller blocks for its batch anyway: it computes its own frame's FCS here, on its
+    // own core where the frame is cache-hot, in parallel with the other callers (host_max 0: no)
+    m.has_fcs = w && q->host_max.load(std::memory_order_relaxed) > 0;
+    if (m.has_fcs) {
+        const uint32_t c = fcs::host_crc32(f, m.covered);
+        std::memcpy(f + m.covered, &c, 4);   // little-endian, as ether.c:263
+    }
     m.ready.store(seq, std::memory_order_release);
     return (int)frame_size;
 }
@@ -491,6 +566,21 @@ void fcs_txq_fallbacks(const fcs_txq_t *q, uint64_t *host_batches, uint64_t *hos
     std::lock_guard<std::mutex> lk(m->mu);
     if (host_batches) *host_batches = m->n_host_batches;
     if (host_frames) *host_frames = m->n_host_frames;
+}
+
+uint64_t fcs_txq_set_host_max(fcs_txq_t *q, uint64_t bytes) {
+    if (!q) return 0;
+    return q->host_max.exchange(bytes);
+}
+
+void fcs_txq_small_batches(const fcs_txq_t *q, uint64_t *small_batches, uint64_t *small_frames,
+                           uint64_t *gpu_batches) {
+    if (!q) return;
+    fcs_txq *m = const_cast<fcs_txq *>(q);
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (small_batches) *small_batches = m->n_small_batches;
+    if (small_frames) *small_frames = m->n_small_frames;
+    if (gpu_batches) *gpu_batches = m->n_gpu_batches;
 }
 
 void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint64_t *errors) {

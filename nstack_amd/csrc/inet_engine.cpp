@@ -42,8 +42,8 @@ int hip_fail(hipError_t e, const char *what) {
 std::atomic<uint64_t> g_flat_min{16384};   // see inet_csum_set_flat_threshold
 std::atomic<uint64_t> g_dma_min{16384};    // see inet_csum_set_dma_threshold
 
-// launch_inet with the work counter the LDS-DMA route takes, leased from the FCS engine's ring of
-// device `dev` for this launch.
+// launch_inet with the work counter the LDS-DMA route takes (the same route_inet decision the
+// launcher makes), leased from the FCS engine's ring of device `dev` for this launch.
 int launch_counted(bool var, int mode, inet::IParams &p, int dev, int cus, hipStream_t st) {
     const uint64_t flat_min = g_flat_min.load(std::memory_order_relaxed), dma_min = g_dma_min.load(std::memory_order_relaxed);
     auto go = [&](unsigned long long *ctr) -> int {
@@ -51,7 +51,8 @@ int launch_counted(bool var, int mode, inet::IParams &p, int dev, int cus, hipSt
         HIPTRY(inet::launch_inet(var, mode, p, cus, flat_min, dma_min, st), "launching the inet kernel");
         return 0;
     };
-    if (!var && inet::dma_route(var, p, dma_min)) return fcs::launch_with_counter(dev, (void *)st, go);
+    if (inet::route_inet(var, p, flat_min, dma_min) == inet::Route::kDma)
+        return fcs::launch_with_counter(dev, (void *)st, go);
     return go(nullptr);
 }
 

@@ -726,12 +726,23 @@ static bool dma_ok(const IParams &p) {
            3 * p.stride + p.flen + 30 <= kDmaSlot && p.flen + 30 <= 16u * kGroup * kDmaRounds;
 }
 
-bool dma_route(bool var, const IParams &p, uint64_t dma_min) { return p.n > dma_min && (var || dma_ok(p)); }
+// The one routing decision (launch_inet launches what it returns; the engine leases a work counter
+// exactly when it returns kDma).
+Route route_inet(bool var, const IParams &p, uint64_t flat_min, uint64_t dma_min) {
+    if (!p.n) return Route::kNone;
+    if (var && p.n > dma_min) return Route::kStream;
+    if (!var && p.n > flat_min && p.flen <= kShortMax) return Route::kShort;   // lane per packet
+    if (!var && p.n > dma_min && dma_ok(p)) return Route::kDma;
+    if (p.n > flat_min) return Route::kFlat;
+    return Route::kGroup;
+}
 
 hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
                        hipStream_t st) {
     (void)hipGetLastError();   // report this launch's own error, not an earlier call's
-    if (var && dma_route(var, p, dma_min)) {
+    const Route r = route_inet(var, p, flat_min, dma_min);
+    if (r == Route::kNone) return hipSuccess;
+    if (r == Route::kStream) {
         const uint64_t nwin = (p.n + 63) / 64;
         const uint64_t want = (nwin + kStWaves - 1) / kStWaves;
         const int grid = (int)(want < (uint64_t)cus ? want : (uint64_t)cus);
@@ -740,7 +751,7 @@ hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t f
         else hipLaunchKernelGGL((inet_stream_kernel<kIp>), dim3(grid), dim3(kStWaves * 64), 0, st, p);
         return hipGetLastError();
     }
-    if (!var && p.n > flat_min && p.flen <= kShortMax) {   // lane per packet
+    if (r == Route::kShort) {
         const uint64_t want = (p.n + kThreads - 1) / kThreads, cap = (uint64_t)cus * 8;
         const int grid = (int)(want < cap ? want : cap);
         if (mode == kTcp) hipLaunchKernelGGL((inet_short_kernel<kTcp>), dim3(grid), dim3(kThreads), 0, st, p);
@@ -748,7 +759,7 @@ hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t f
         else hipLaunchKernelGGL((inet_short_kernel<kIp>), dim3(grid), dim3(kThreads), 0, st, p);
         return hipGetLastError();
     }
-    if (dma_route(var, p, dma_min)) {
+    if (r == Route::kDma) {
         if (!p.ctr) return hipErrorInvalidValue;
         const uint64_t items = (p.n + 3) / 4;
         const uint64_t want = (items + kDmaWaves - 1) / kDmaWaves;
@@ -758,7 +769,7 @@ hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t f
         else hipLaunchKernelGGL((inet_dma_kernel<kIp>), dim3(grid), dim3(kDmaWaves * 64), 0, st, p);
         return hipGetLastError();
     }
-    if (p.n > flat_min) {
+    if (r == Route::kFlat) {
         const uint64_t windows = (p.n + 63) / 64, per_block = kThreads / 64;
         const uint64_t want = (windows + per_block - 1) / per_block, cap = (uint64_t)cus * 8;
         const int grid = (int)(want < cap ? want : cap);
@@ -775,8 +786,7 @@ hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t f
 #undef INET_FLAT
         return hipGetLastError();
     }
-    if (!p.n) return hipSuccess;
-    const uint64_t per_block = kThreads / kGroup;
+    const uint64_t per_block = kThreads / kGroup;   // Route::kGroup
     uint64_t want = (p.n + per_block - 1) / per_block;
     const uint64_t cap = (uint64_t)cus * 8;   // 32 waves per CU, persistent over the packets
     const int grid = (int)(want < cap ? want : cap);

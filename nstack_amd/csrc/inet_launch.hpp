@@ -27,9 +27,12 @@ struct IParams {
 // kernel, smaller ones one 16-lane group per packet (every packet in flight at once).
 hipError_t launch_inet(bool var, int mode, const IParams &p, int cus, uint64_t flat_min, uint64_t dma_min,
                        hipStream_t st);
-// True when launch_inet takes an LDS-DMA kernel: fixed strides inet_dma_kernel (which needs p.ctr),
-// variable batches inet_stream_kernel (windows interleaved statically, like the flat kernel's:
-// guided chunks measured 4 % slower there on IMIX, 17 % on 20-B headers).
-bool dma_route(bool var, const IParams &p, uint64_t dma_min);
+// The kernel launch_inet takes: kStream (variable batches of more than dma_min packets: windows
+// interleaved statically, like the flat kernel's; guided chunks measured 4 % slower there on IMIX,
+// 17 % on 20-B headers), kShort (fixed packets of at most 64 B, more than flat_min), kDma (fixed
+// strides of more than dma_min packets whose items fit a slot: inet_dma_kernel, the only one that
+// needs p.ctr), kFlat (more than flat_min), kGroup (a 16-lane group per packet), kNone (n == 0).
+enum class Route { kNone, kStream, kShort, kDma, kFlat, kGroup };
+Route route_inet(bool var, const IParams &p, uint64_t flat_min, uint64_t dma_min);
 
 }  // namespace inet

@@ -77,7 +77,8 @@ def run_tx(flib, oracle, max_batch, flush_usec, producers, per, seed, inject=Non
     got, results = [], [[] for _ in range(producers)]
     rd = threading.Thread(target=lambda: got.extend(b.recv(2048) for _ in range(total)))
     rd.start()
-    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=flush_usec, lib=flib) as q:
+    # host_max=0: every batch takes the GPU step (the one the faults are injected into), however small
+    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=flush_usec, lib=flib, host_max=0) as q:
         if inject:
             inject(q)
 
@@ -134,6 +135,55 @@ def test_tx_late_failures_with_kernel_in_flight(flib, oracle, max_batch, produce
     assert ok_res and same and errors == 0 and frames == producers * 150
     assert hb == 3 and flib.fcs_engine_host_batches() - h0 == 3
     assert "injected late fault" in why
+
+
+def test_retired_kernel_that_stays_busy_does_not_block_the_next_batch(flib, oracle):
+    """A small TX batch gives up while its kernel really stays in flight (queued behind a kernel that
+    waits for a pinned host word, at most 20 s): the engine answers it from the host CRC and retires
+    the small-batch stream. The next small batch must run on a fresh stream at once: no device-wide
+    synchronisation (which would wait for the held kernel), answered by the GPU, exact."""
+    import ctypes
+    import time
+    word = flib.fcs_host_alloc(64)
+    arena = flib.fcs_host_alloc(8 * 1536)
+    assert word and arena
+    ctypes.memset(word, 0, 64)
+    n, stride = 4, 1536
+    off = (ctypes.c_uint64 * n)(*[i * stride for i in range(n)])
+    ln = (ctypes.c_uint32 * n)(*[60 + 300 * i for i in range(n)])
+    rng = random.Random(5)
+
+    def fill_and_expect():
+        body = [bytes(rng.randrange(256) for _ in range(ln[i])) for i in range(n)]
+        for i in range(n):
+            ctypes.memmove(arena + off[i], body[i], ln[i])
+        return [struct.pack("<I", oracle.oracle_ether_fcs(b, len(b))) for b in body]
+
+    def got():
+        return [ctypes.string_at(arena + off[i] + ln[i], 4) for i in range(n)]
+
+    try:
+        want = fill_and_expect()
+        h0 = flib.fcs_engine_host_batches()
+        flib.fcs_debug_hold_small(word)          # the next small launch waits behind the hold kernel
+        flib.fcs_debug_late_batches(0, 1)        # ... and its call gives up with it in flight
+        assert flib.ether_fcs_tx_batch_host(arena, 8 * 1536, off, ln, n) == 0
+        assert flib.fcs_engine_host_batches() - h0 == 1 and got() == want   # host CRC answer
+        want = fill_and_expect()
+        s0 = flib.fcs_debug_device_syncs()
+        t0 = time.monotonic()
+        assert flib.ether_fcs_tx_batch_host(arena, 8 * 1536, off, ln, n) == 0
+        dt = time.monotonic() - t0
+        flib.fcs_last_error.restype = ctypes.c_char_p
+        assert flib.fcs_engine_host_batches() - h0 == 1, flib.fcs_last_error()   # the GPU answered
+        assert got() == want
+        assert flib.fcs_debug_device_syncs() == s0           # nothing waited on the held kernel
+        assert dt < 5.0, dt                                   # the held kernel lasts up to 20 s
+    finally:
+        ctypes.memset(word, 0xFF, 4)             # release the held kernel
+        flib.fcs_engine_fini()                   # waits for it (released) before freeing
+        flib.fcs_host_free(arena)
+        flib.fcs_host_free(word)
 
 
 def rx_frame(payload, proto=0x0800):

@@ -36,8 +36,9 @@ def ether_send_frame(oracle, dst, proto, payload):
     return f + struct.pack("<I", oracle.oracle_ether_fcs(f, len(f)))   # :262-263
 
 
+@pytest.mark.parametrize("host_max", [0, None])   # every batch on the GPU / the default GPU minimum
 @pytest.mark.parametrize("max_batch,flush_usec", [(1, 0), (64, 200), (1024, 2000)])
-def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec):
+def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec, host_max):
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
     b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
@@ -58,7 +59,7 @@ def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec)
 
     rd = threading.Thread(target=reader)
     rd.start()
-    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=flush_usec) as q:
+    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=flush_usec, host_max=host_max) as q:
         def producer(t):
             for dst, proto, payload in plans[t]:
                 results[t].append((q.send(dst, proto, payload), 14 + max(len(payload), 56) + 4))
@@ -69,7 +70,11 @@ def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec)
             x.join()
         q.flush()
         frames, batches, errors = q.stats()
-        assert q.fallbacks() == (0, 0)                           # every batch's FCSs came from the GPU
+        small_batches, small_frames, gpu_batches = q.paths()
+        assert q.fallbacks() == (0, 0)                           # no GPU step failed
+        assert small_batches + gpu_batches == batches
+        if host_max == 0:
+            assert gpu_batches == batches                        # every batch's FCSs came from the GPU
     rd.join(timeout=60)
     a.close(), b.close()
     assert all(r == want for rs in results for r, want in rs)   # per-call return = frame_size
@@ -79,3 +84,44 @@ def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec)
     assert Counter(got) == expect
     for f in got:                                                # every frame carries a valid FCS
         assert oracle.oracle_ether_fcs(f, len(f)) == 0x2144DF1C
+
+
+def test_batches_above_the_gpu_minimum_run_the_kernel(dev, oracle):
+    """The GPU minimum (fcs_txq_set_host_max) splits the batches: every batch of more covered bytes
+    than it ran the GPU step (counted as a GPU batch, none answered by the host CRC after a failure),
+    every batch at or below it was computed by the host CRC by design. Fire-and-forget producers
+    with 1500-B payloads (1514 covered bytes) fill batches of up to 64 frames; the minimum is 16 such
+    frames, so both kinds occur; every frame leaves exact."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    P, M = 4, 600
+    payload = [bytes((t * 7 + i) & 255 for i in range(1500)) for t in range(P)]
+    total = P * M
+    got = []
+    rd = threading.Thread(target=lambda: got.extend(b.recv(2048) for _ in range(total)))
+    rd.start()
+    h0 = na.engine_stats()["host_batches"]
+    with na.TxQueue(MAC, a.fileno(), max_batch=64, flush_usec=300, host_max=16 * 1514) as q:
+        def producer(t):
+            for _ in range(M):
+                assert q.send_async(bytes([2, 0, 0, 0, 0, t]), 0x0800, payload[t]) == 1518
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(P)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        q.flush()
+        frames, batches, errors = q.stats()
+        small_batches, small_frames, gpu_batches = q.paths()
+        fb = q.fallbacks()
+    rd.join(timeout=60)
+    a.close(), b.close()
+    assert frames == total and errors == 0 and fb == (0, 0)
+    assert na.engine_stats()["host_batches"] == h0
+    assert small_batches + gpu_batches == batches and gpu_batches >= 1
+    assert small_frames <= 16 * small_batches                  # host batches: at most the minimum
+    assert total - small_frames >= 17 * gpu_batches            # GPU batches: above it
+    want = Counter(ether_send_frame(oracle, bytes([2, 0, 0, 0, 0, t]), 0x0800, payload[t]) for t in range(P)
+                   for _ in range(M))
+    assert Counter(got) == want

@@ -54,7 +54,7 @@ def test_no_gpu_host_crc_sends_every_frame(oracle):
     b.setblocking(False)
     res = []
     plans = [(bytes([k]) * 6, 0x0806 + k, bytes([k]) * (10 * k + (k % 3) * 500)) for k in range(10)]
-    with na.TxQueue(MAC, a.fileno(), max_batch=4, flush_usec=50) as q:
+    with na.TxQueue(MAC, a.fileno(), max_batch=4, flush_usec=50, host_max=0) as q:   # every batch to the GPU
         th = [threading.Thread(target=lambda p=p: res.append((q.send(*p), 14 + max(len(p[2]), 56) + 4)))
               for p in plans]
         for t in th:
@@ -117,3 +117,67 @@ def test_many_producers_no_lost_frames(max_batch, linger):
     assert frames == total and errors == 0
     assert batches >= -(-total // max_batch)
     a.close(), b.close()
+
+
+@pytest.mark.parametrize("host_max,expect_small", [(None, True), (1 << 30, True), (0, False)])
+def test_small_batches_take_the_host_crc_by_design(oracle, host_max, expect_small):
+    """Batches whose covered bytes total at most the GPU minimum (fcs_txq_set_host_max, default
+    96 KiB) are computed by the flusher with the library's host CRC: counted as small batches, not
+    as failure answers, with no GPU step at all (so this runs the same with or without a GPU).
+    host_max 0 sends every batch to the GPU step (here: no GPU, so failure answers)."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    b.setblocking(False)
+    plans = [(bytes([k]) * 6, 0x0800, bytes([k]) * (k * 150 % 1501)) for k in range(24)]
+    with na.TxQueue(MAC, a.fileno(), max_batch=8, flush_usec=0, host_max=host_max) as q:
+        res = [q.send(*p) for p in plans]
+        q.flush()
+        frames, batches, errors = q.stats()
+        small_batches, small_frames, gpu_batches = q.paths()
+        host_batches, host_frames = q.fallbacks()
+        if host_max is not None:
+            assert q.set_host_max(host_max) == host_max
+    assert res == [14 + max(len(p[2]), 56) + 4 for p in plans]
+    assert frames == 24 and errors == 0
+    if expect_small:
+        assert (small_batches, small_frames) == (batches, 24) and host_batches == 0 and gpu_batches == 0
+    else:
+        assert small_batches == 0 and small_frames == 0
+        if not _gpu_visible():
+            assert (host_batches, host_frames) == (batches, 24)
+    got = [b.recv(2048) for _ in range(24)]
+    assert Counter(got) == Counter(ether_send_frame(oracle, *p) for p in plans)
+    a.close(), b.close()
+
+
+@pytest.mark.timeout(120)
+@pytest.mark.parametrize("max_batch", [64, 512])
+def test_per_thread_order_kept(max_batch):
+    """Every producer's frames leave in the order it queued them, across shards and batches (the
+    per-thread floor of enqueue; tools/tsan/run.sh drives the same check with C threads). Host CRC
+    by design here (fire-and-forget batches below the GPU minimum), so no GPU is needed."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    P, per = 6, 1500
+    total = P * per
+    got = []
+    drain = threading.Thread(target=lambda: got.extend(b.recv(2048) for _ in range(total)))
+    drain.start()
+    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=0, host_max=1 << 40) as q:
+        def producer(t):
+            for i in range(per):
+                assert q.send_async(DST, 0x0806, bytes([t]) + i.to_bytes(4, "little") + bytes(i % 90)) > 0
+        th = [threading.Thread(target=producer, args=(t,)) for t in range(P)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        q.flush()
+    drain.join(timeout=60)
+    a.close(), b.close()
+    assert len(got) == total
+    last = [-1] * P
+    for f in got:
+        t, i = f[14], int.from_bytes(f[15:19], "little")
+        assert i > last[t], (t, i, last[t])
+        last[t] = i

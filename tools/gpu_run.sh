@@ -11,6 +11,7 @@
 #   ab:ARGS               python tools/ab.py ARGS (variants built by tools/variants.sh)
 #   pmc:ARGS              tools/pmc.sh OUT/pmc ARGS (SQ counter passes over tools/prof_fixed.py ARGS)
 #   py:SCRIPT[,ARGS]      python SCRIPT ARGS (a measurement tool under tools/)
+#   sh:CMD[,ARGS]         a tool command line (commas become spaces), e.g. sh:tools/tx_crossover,300
 set -o pipefail
 out=gpurun_out/${1:?usage: gpu_run.sh OUT STEP...}; shift
 mkdir -p "$out"
@@ -48,6 +49,9 @@ for step in "$@"; do
     py)
       timeout -k 10 600 python -u ${arg//,/ } > "$log" 2>&1; rc=$?
       echo "py rc=$rc"; tail -20 "$log" ;;
+    sh)
+      timeout -k 10 600 ${arg//,/ } > "$log" 2>&1; rc=$?
+      echo "sh rc=$rc"; tail -20 "$log" ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac

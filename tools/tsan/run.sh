@@ -8,7 +8,8 @@ OUT=${TMPDIR:-/tmp}/txq_tsan
 g++ -std=c++17 -O1 -g -fsanitize=thread -DFCS_TXQ_TSAN -I"$ROOT/include" \
     "$HERE/txq_stress.cpp" "$HERE/gpu_stub.cpp" "$ROOT/nstack_amd/csrc/fcs_txq.cpp" \
     "$ROOT/nstack_amd/csrc/fcs_host_crc.cpp" -o "$OUT" -lpthread
-for c in "1 0" "7 0" "7 30" "64 0" "64 3000" "256 30" "512 0" "4096 0" "4096 30" "4096 3000"; do
+for c in "1 0" "7 0" "7 30" "64 0" "64 3000" "256 30" "512 0" "4096 0" "4096 30" "4096 3000" \
+         "1 0 0" "7 30 0" "64 0 0" "256 30 0" "4096 30 0" "64 0 1000000"; do
   TSAN_OPTIONS="halt_on_error=1 exitcode=66" timeout -k 5 300 "$OUT" $c
 done
 echo "tsan: clean"

@@ -2,7 +2,9 @@
 // ether_send semantics and 3 fire-and-forget producers on one queue, then flush/stats/destroy.
 // Every frame must be sunk exactly once, every sync caller must get its frame_size back, and each
 // fire-and-forget producer's frames must reach the sink in the order it queued them.
-//   usage: txq_stress <max_batch> <flush_usec>      (build and run: tools/tsan/run.sh)
+//   usage: txq_stress <max_batch> <flush_usec> [host_max]   (build and run: tools/tsan/run.sh)
+// host_max (fcs_txq_set_host_max): absent = the default (sync callers compute their own FCS, small
+// fire-and-forget batches on the flusher); 0 = every frame through the (stubbed) GPU step.
 #include <atomic>
 #include <cstdio>
 #include <cstdlib>
@@ -27,10 +29,12 @@ static void sink(void *, uint8_t *const *f, const uint32_t *sz, int *res, uint32
 }
 int main(int argc, char **argv) {
     const uint32_t CAP = atoi(argv[1]), LIN = atoi(argv[2]);
+    const long long HMAX = argc > 3 ? atoll(argv[3]) : -1;
     const uint8_t mac[6] = {2,0,0,0,0,1}, dst[6] = {2,0,0,0,0,2};
     { const uint32_t cap = CAP, linger = LIN;
         sunk = 0;
         fcs_txq_t *q = fcs_txq_create(mac, cap, linger, sink, nullptr);
+        if (HMAX >= 0) fcs_txq_set_host_max(q, (uint64_t)HMAX);
         std::atomic<int> bad{0};
         std::vector<std::thread> th;
         const int per = 400;
