@@ -440,6 +440,80 @@ def imix_sharded(torch, na, dev, stream, world: int, rank: int, dist, n_blk: int
             "spot_checked": 64 * world, "spot_bad": all_bad}
 
 
+def host_aggregate(per_rank, rep_max_secs):
+    """Whole-job host-inclusive rate at N > 1: per_rank = [{"rank", "bytes", "secs"}] (each rank's median
+    of its own timed runs), rep_max_secs = per timed run, the slowest rank's time. The aggregate is all
+    ranks' bytes over the median of those per-run maxima (the ranks run concurrently, barrier between
+    runs), as `value` is all ranks' bytes over the slowest rank."""
+    total = sum(int(r["bytes"]) for r in per_rank)
+    t = sorted(rep_max_secs)[len(rep_max_secs) // 2]
+    return {"GB_s_aggregate": round(total / t / 1e9, 2), "bytes_all_ranks": total,
+            "secs_max_rank": round(t, 4),
+            "per_rank": [{"rank": int(r["rank"]), "bytes": int(r["bytes"]), "secs": round(float(r["secs"]), 4),
+                          "GB_s": round(int(r["bytes"]) / float(r["secs"]) / 1e9, 2)}
+                         for r in sorted(per_rank, key=lambda r: r["rank"])]}
+
+
+def gather_host_times(torch, dist, world: int, rank: int, nbytes: int, secs, bad: int):
+    """Cross-rank part of host_inclusive_sharded (gloo, host values only): every rank's (bytes, median
+    of its runs, spot-check misses), and per timed run the slowest rank's time."""
+    rep_max = torch.tensor(list(secs), dtype=torch.float64)
+    dist.all_reduce(rep_max, op=dist.ReduceOp.MAX)
+    mine = {"rank": rank, "bytes": int(nbytes), "secs": sorted(secs)[len(secs) // 2], "spot_bad": int(bad)}
+    allr = [None] * world
+    dist.all_gather_object(allr, mine)
+    return allr, rep_max.tolist()
+
+
+def host_inclusive_sharded(torch, na, dev, stream, world: int, rank: int, dist, host_gib: float = 4.0):
+    """The host-inclusive rate at N > 1 (bounded by each GPU's PCIe link
+    and the host's DRAM): every rank checksums its own host_gib of 1518-B frames in pinned host memory
+    through ether_fcs_fixed_host (chunked H2D -> kernel -> D2H), all ranks at once, HOST_REPS timed
+    runs after one untimed one with a barrier before each. Rank 0 reports each rank's rate and the
+    aggregate over the slowest rank (host_aggregate)."""
+    import numpy as np
+    L = 1518
+    n = int(host_gib * GIB) // L
+    nbytes = n * L
+    lib = na.load()
+    p = lib.fcs_host_alloc(nbytes)
+    ok = torch.tensor([1 if p else 0], dtype=torch.int64)
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    if not int(ok.item()):
+        if p:
+            lib.fcs_host_free(p)
+        return None
+    try:
+        pinned = np.ctypeslib.as_array((ctypes.c_uint8 * nbytes).from_address(p))
+        d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        na.fill_splitmix_dev(d, nbytes, SEED + 6, rank * nbytes, stream)   # this rank's slice of one stream
+        torch.cuda.synchronize()
+        pinned[:] = d.cpu().numpy()
+        del d
+        torch.cuda.empty_cache()
+        hout = np.zeros(n, dtype=np.uint32)
+        na.fixed_host(p, L, L, n, hout)   # untimed: pipeline buffers and streams allocated
+        secs = []
+        for _ in range(HOST_REPS):
+            dist.barrier()
+            t0 = time.perf_counter()
+            na.fixed_host(p, L, L, n, hout)
+            secs.append(time.perf_counter() - t0)
+        idx = np.random.default_rng(200 + rank).integers(0, n, 64)
+        bad = _spot(hout, lambda i: pinned[i * L:(i + 1) * L].tobytes(), idx)
+        allr, rep_max = gather_host_times(torch, dist, world, rank, nbytes, secs, bad)
+        del pinned, hout
+    finally:
+        lib.fcs_host_free(p)
+    agg = host_aggregate(allr, rep_max)
+    agg.update({"what": "each rank: its own pinned host slice of 1518-B frames -> ether_fcs_fixed_host "
+                        "(chunked H2D -> kernel -> D2H of CRCs), all ranks at once; PCIe bound, never `value`",
+                "frames_per_rank": n, "timed_runs": HOST_REPS,
+                "stat": "median over runs of the slowest rank's time (barrier before each run)",
+                "spot_checked": 64 * world, "spot_bad": sum(int(r["spot_bad"]) for r in allr)})
+    return agg
+
+
 def cpu_baseline(frames: int = 1 << 20, L: int = 1518):
     """Oracle restatement of ether_fcs (src/ether_fcs.c:4-19) on the SURVEY §8d dataset."""
     import numpy as np
@@ -590,6 +664,8 @@ def main():
     ap.add_argument("--no-configs", action="store_true", help="skip the other BASELINE configs")
     ap.add_argument("--imix-frames-per-gpu", type=int, default=128 << 20,
                     help="N > 1: IMIX frames per GPU of the sharded configs[2] run (0 = skip)")
+    ap.add_argument("--host-gib-per-gpu", type=float, default=4.0,
+                    help="N > 1: GiB of pinned host frames per rank for the host-inclusive run (0 = skip)")
     args = ap.parse_args()
 
     # --gpus is authoritative: no launcher -> start the ranks here, before any
@@ -753,6 +829,13 @@ def main():
         torch.cuda.empty_cache()
         configs = {"imix_sharded": imix_sharded(torch, na, dev, stream, world, rank, dist,
                                                 n_blk=args.imix_frames_per_gpu)}
+    if dist and not args.no_configs and args.host_gib_per_gpu > 0:
+        if configs is None:
+            del arena, out
+            torch.cuda.empty_cache()
+            configs = {}
+        configs["host_inclusive_1518_sharded"] = host_inclusive_sharded(torch, na, dev, stream, world, rank, dist,
+                                                                        host_gib=args.host_gib_per_gpu)
     if dist:
         dist.barrier()
     if rank == 0:

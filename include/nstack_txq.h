@@ -39,7 +39,9 @@ typedef struct fcs_txq fcs_txq_t;
 
 /* Transmit n finished frames (header + payload + pad + FCS; sizes[i] bytes at frames[i]).
  * Must store each frame's result in res[i]: bytes sent, or -errno (as sendto's result at
- * src/linux/ether.c:265-269). Called from the queue's flusher thread, one batch at a time. */
+ * src/linux/ether.c:265-269). Must be thread-safe: the flusher thread calls it one batch at a time,
+ * and synchronous senders call it from their own threads with a batch of one frame, concurrently
+ * (see fcs_txq_set_sync_host), as nstack's threads call sendto concurrently. The provided sinks are. */
 typedef void (*fcs_txq_sink_fn)(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res,
                                 uint32_t n);
 
@@ -49,7 +51,8 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
                           fcs_txq_sink_fn sink, void *sink_ctx);
 /* ether_send semantics: returns frame_size = 14 + max(bsize, 56) + 4 on success, -EMSGSIZE when
  * that exceeds 1518 (checked before anything is queued, :234-237), or the sink's / engine's
- * -errno. Thread-safe; blocks until the frame's batch has been sent. */
+ * -errno. Thread-safe; returns once the frame has been handed to the sink (sent by the caller itself
+ * or in its batch). */
 int fcs_txq_send(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize);
 /* Fire-and-forget form: returns frame_size once the frame is queued (or -EMSGSIZE / -EINVAL);
  * its send result only feeds the error counter of fcs_txq_stats. */
@@ -74,16 +77,20 @@ const char *fcs_txq_last_error(const fcs_txq_t *q);
  * frames were sent all the same. 0 on a healthy GPU. Any pointer may be NULL. */
 void fcs_txq_fallbacks(const fcs_txq_t *q, uint64_t *host_batches, uint64_t *host_frames);
 /* Where the GPU does not pay, the library's host CRC (fcs_host_crc32) computes the FCS, by design:
- * - fcs_txq_send (synchronous) callers compute their own frame's FCS while assembling it: a GPU step
- *   costs a launch and a completion round trip (9-12 us on MI355X) whatever it holds, synchronous
- *   callers put one frame each in a batch, and the host CRC takes about 0.08 us per 1518-B frame on
- *   the caller's own core;
- * - fire-and-forget frames (fcs_txq_send_async) of one batch take one GPU step when their FCS-covered
- *   bytes total more than `bytes`, the GPU minimum; at or below it the flusher computes them.
- * The default GPU minimum (512 KiB, the crossover tools/tx_crossover.c measured: one GPU step against
- * one host thread over the same frames) can be overridden per process by NSTACK_TXQ_HOST_MAX_BYTES;
- * 0 sends every frame, synchronous ones too, to the GPU. Returns the previous value (0 for NULL). */
+ * a GPU step costs a launch and a completion round trip (9-12 us on MI355X) whatever it holds, a
+ * hand-off between threads 1-2 us, and the host CRC about 0.08 us per 1518-B frame.
+ * - fcs_txq_send (synchronous): a caller with none of its own frames queued sends its frame itself
+ *   (ether_send's body with the host CRC; the sink gets a batch of one on the caller's thread); a
+ *   caller with fire-and-forget frames queued joins their batch (order kept) and computes its own
+ *   frame's FCS there. fcs_txq_set_sync_host(q, 0) turns this off: synchronous frames then join the
+ *   batch and take its GPU step. Returns the previous setting (1 = on, the default) or -EINVAL.
+ * - fcs_txq_send_async (fire-and-forget): the frames of one batch take one GPU step when their
+ *   FCS-covered bytes total more than `bytes`, the GPU minimum; at or below it the flusher computes
+ *   them. The default (4 KiB) comes from the in-queue scan of tools/txq_vs_reference.sh; it can be
+ *   overridden per process by NSTACK_TXQ_HOST_MAX_BYTES; 0 sends every batch to the GPU.
+ *   fcs_txq_set_host_max returns the previous value (0 for a NULL queue). */
 uint64_t fcs_txq_set_host_max(fcs_txq_t *q, uint64_t bytes);
+int fcs_txq_set_sync_host(fcs_txq_t *q, int on);
 /* Batches that took no GPU step and frames whose FCS the host CRC computed, both by design (callers'
  * own frames and batches at or below the GPU minimum; not failures: those are fcs_txq_fallbacks), and
  * batches whose FCSs a GPU step computed. Any pointer may be NULL. */

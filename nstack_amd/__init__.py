@@ -30,7 +30,7 @@ EXPORTS = [
     "fcs_host_crc32",
     # include/nstack_txq.h — batched TX call site
     "fcs_txq_create", "fcs_txq_send", "fcs_txq_send_async", "fcs_txq_flush", "fcs_txq_destroy", "fcs_txq_stats", "fcs_txq_timing", "fcs_txq_last_error", "fcs_txq_fallbacks",
-    "fcs_txq_set_host_max", "fcs_txq_small_batches", "fcs_txq_sink_fd", "fcs_txq_sink_packet",
+    "fcs_txq_set_host_max", "fcs_txq_set_sync_host", "fcs_txq_small_batches", "fcs_txq_sink_fd", "fcs_txq_sink_packet",
     # include/nstack_pcap.h — frame batches on disk
     "fcs_pcap_scan", "fcs_pcap_read", "fcs_pcap_write",
     # include/nstack_inet.h — batched Internet checksums (opt-in)
@@ -147,6 +147,7 @@ def _bind(path: str) -> ctypes.CDLL:
         "fcs_txq_last_error": (c.c_char_p, [vp]),
         "fcs_txq_fallbacks": (None, [vp, c.POINTER(u64), c.POINTER(u64)]),
         "fcs_txq_set_host_max": (u64, [vp, u64]),
+        "fcs_txq_set_sync_host": (i32, [vp, i32]),
         "fcs_txq_small_batches": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
         "fcs_host_crc32": (u32, [vp, c.c_size_t]),
         "fcs_txq_sink_fd": (None, [vp, vp, vp, vp, u32]),
@@ -393,11 +394,12 @@ class TxQueue:
     threads are FCS'd together on the GPU and leave in one sendmmsg per batch."""
 
     def __init__(self, src_mac: bytes, fd: int, max_batch: int = 256, flush_usec: int = 0, sink=None,
-                 sink_ctx=None, lib=None, host_max=None):
+                 sink_ctx=None, lib=None, host_max=None, gpu_only=False):
         """sink: None (fcs_txq_sink_fd on fd) or a C sink function pointer (e.g. fcs_txq_sink_packet)
         with sink_ctx its context pointer; lib: the library to use (default: the product); host_max:
-        the GPU minimum in covered bytes (fcs_txq_set_host_max; None keeps the default, 0 sends every
-        batch to the GPU)."""
+        the GPU minimum of fire-and-forget batches in covered bytes (fcs_txq_set_host_max; None keeps
+        the default); gpu_only: every frame, synchronous ones too, through a batch and its GPU step
+        (host_max 0 and fcs_txq_set_sync_host off)."""
         L = self._L = lib or load()
         self._fd = ctypes.c_int(fd)
         self._mac = (ctypes.c_uint8 * 6)(*src_mac)
@@ -408,6 +410,9 @@ class TxQueue:
             raise FcsError(-errno.EINVAL, "fcs_txq_create")
         if host_max is not None:
             L.fcs_txq_set_host_max(self._q, host_max)
+        if gpu_only:
+            L.fcs_txq_set_host_max(self._q, 0)
+            L.fcs_txq_set_sync_host(self._q, 0)
 
     def send(self, dst: bytes, proto: int, payload: bytes) -> int:
         return self._L.fcs_txq_send(self._q, bytes(dst), proto, bytes(payload), len(payload))

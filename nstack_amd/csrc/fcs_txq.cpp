@@ -11,22 +11,21 @@
 // call (its results go through the library's own mapped memory), so arenas are always reused.
 //
 // Where the GPU does not pay, the host CRC (fcs_host_crc.cpp, carry-less folding, ~18 GB/s on one
-// MI355X host core) computes the FCS by design (counted in fcs_txq_small_batches, not as a failure):
-// - a synchronous caller (fcs_txq_send) computes its own frame's FCS in enqueue: it blocks for the
-//   batch anyway, the frame is hot in its core's cache, and the callers run in parallel; a GPU step
-//   (a launch and a completion round trip, 9-12 us) for the few frames synchronous callers put in a
-//   batch is slower than the reference's per-frame CRC (profiles/r06_txq_vs_reference.jsonl);
-// - fire-and-forget frames (fcs_txq_send_async) go to the GPU in one step per batch when their
-//   covered bytes exceed host_max, the GPU minimum; at or below it the flusher computes them. The
-//   default is the crossover measured on MI355X boxes (tools/tx_crossover.c: one GPU step against
-//   one host thread over the same frames, profiles/r06_tx_crossover.jsonl).
-// host_max 0 sends every frame, synchronous ones too, to the GPU step.
-//
-// Producers reserve slots with one atomic add on a reservation word, and the open batch is split
-// into up to 16 shards, each with its own word on its own cache line: a thread reserves in its
-// home shard (threads are dealt homes round-robin) and moves to higher shards only when that one
-// is full, so producers on different threads do not bounce one line between cores. Frames leave
-// in shard order, which keeps every thread's own frames in the order it sent them (see enqueue).
+// MI355X host core) computes the FCS by design (counted in fcs_txq_small_batches, not as a failure).
+// Measured on MI355X boxes (profiles/r06_txq_vs_reference.jsonl): a GPU step costs a launch and a
+// completion round trip (9-12 us) whatever it holds, and a hand-off between threads costs 1-2 us,
+// while the reference's own per-frame CRC costs 4.8 us per 1518-B frame and 0.2 us per 60-B one.
+// - A synchronous caller (fcs_txq_send) with none of its own frames still queued sends its frame
+//   itself: ether_send's body with the host CRC, the sink called with a batch of one on its own
+//   thread (sinks are thread-safe, as the reference's concurrent sendto calls are). Its frames keep
+//   their order (nothing of its own is queued), and it never waits for a batch it has no use for.
+//   A synchronous caller with fire-and-forget frames still queued joins the batch behind them and
+//   computes its own frame's FCS there (cache-hot, in parallel with the other callers).
+//   fcs_txq_set_sync_host(q, 0) sends synchronous frames through the batch and its GPU step instead.
+// - Fire-and-forget frames (fcs_txq_send_async) take one GPU step per batch when their covered bytes
+//   exceed host_max, the GPU minimum; at or below it the flusher computes them. Its frames are cold
+//   in the flusher's cache (the producers wrote them), and a fast host answer keeps the next batch
+//   small, so the in-queue scan favours the GPU from a few frames up: the default is 4 KiB.
 #include <arpa/inet.h>
 #include <linux/if_packet.h>
 #include <sys/socket.h>
@@ -58,11 +57,12 @@ constexpr uint32_t kSlot = 1518;        // ETHER_MAXLEN + ETHER_FCS_LEN: largest
 constexpr uint32_t kStride = 1536;      // arena slot pitch: whole cache lines, so producers filling
                                         // neighbouring slots never share a line
 constexpr uint32_t kMaxBatch = 65536;
-// Batches of at most this many covered bytes take the host CRC (see the file comment): from 128
-// frames up, one GPU step over n 1514-B frames in pinned memory takes about 15 + 0.037 n us and the
-// host CRC 0.082 n us on one thread, even at about 330 frames (500 KB); 576-B frames cross at a
-// similar byte count, 60-B frames never (the GPU step's per-frame cost exceeds the host's).
-constexpr uint64_t kHostMaxDefault = 512 * 1024;
+// Fire-and-forget batches of at most this many covered bytes take the host CRC (see the file
+// comment). tools/tx_crossover.c puts the crossover at ~500 KB when the host CRC reads cache-hot
+// frames; in the queue they are cold and batches that take the host path stay small, and the scan
+// of fire-and-forget producers (tools/txq_vs_reference.sh) was fastest with the GPU from a few
+// 1518-B frames up.
+constexpr uint64_t kHostMaxDefault = 4096;
 
 using Clock = std::chrono::steady_clock;
 
@@ -153,12 +153,15 @@ struct fcs_txq {
     std::condition_variable cv_flusher;   // producers / flush() -> flusher
     std::condition_variable cv_prod;      // flusher -> producers (batch swapped, results ready)
     uint64_t seq_done = 0;                // last batch handed to the sink
+    std::atomic<uint64_t> seq_sunk{0};    // the same, readable without mu (fcs_txq_send's direct path)
+    std::atomic<uint64_t> n_direct{0}, n_direct_errors{0};   // frames synchronous callers sent themselves
     uint64_t flush_target = 0;            // flush() wants batches <= this closed now
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
     uint64_t n_host_batches = 0, n_host_frames = 0;   // failed GPU steps answered by the host CRC
-    uint64_t n_small_batches = 0, n_small_frames = 0; // batches at most host_max bytes: host CRC by design
+    uint64_t n_small_batches = 0, n_small_frames = 0; // no GPU step / frames on the host CRC, by design
     uint64_t n_gpu_batches = 0;                       // batches the GPU computed
     std::atomic<uint64_t> host_max{kHostMaxDefault};  // see fcs_txq_set_host_max
+    std::atomic<bool> sync_host{true};                // see fcs_txq_set_sync_host
     uint64_t ns_ready = 0, ns_gpu = 0, ns_sink = 0, ns_busy = 0;   // flusher time split
     uint64_t ns_pickup = 0;               // first frame of a batch queued -> batch closed
     std::string last_error;               // fcs_last_error() of the latest failed GPU step
@@ -251,6 +254,7 @@ void flusher(fcs_txq *q) {
         if (wait_for_batch(q, seq, &closed_empty) == Leave::kStop) {   // stopping, nothing queued
             std::lock_guard<std::mutex> lk(q->mu);
             q->seq_done = seq - 1;
+            q->seq_sunk.store(seq - 1, std::memory_order_release);
             q->cv_prod.notify_all();
             return;
         }
@@ -352,6 +356,7 @@ void flusher(fcs_txq *q) {
             }
         }
         q->seq_done = seq;
+        q->seq_sunk.store(seq, std::memory_order_release);
         q->n_frames += n;
         q->n_batches++;
         q->cv_prod.notify_all();
@@ -407,6 +412,18 @@ fcs_txq_t *fcs_txq_create(const uint8_t src_mac[6], uint32_t max_batch, uint32_t
 }  // extern "C"
 
 namespace {
+// Assemble exactly as ether_send (:257-261): dst, src, htons(proto), payload, zero pad and zeroed
+// FCS slot; the FCS is filled in afterwards (:262-263).
+inline void assemble(uint8_t *f, const uint8_t *mac, const uint8_t dst[6], uint16_t proto, const uint8_t *buf,
+                     size_t bsize, size_t frame_size) {
+    std::memcpy(f, dst, 6);
+    std::memcpy(f + 6, mac, 6);
+    f[12] = (uint8_t)(proto >> 8);
+    f[13] = (uint8_t)proto;
+    if (bsize) std::memcpy(f + kHeaderLen, buf, bsize);
+    std::memset(f + kHeaderLen + bsize, 0, frame_size - kHeaderLen - bsize);
+}
+
 Floor &thread_floor(const fcs_txq *q) {
     thread_local std::unordered_map<uint64_t, Floor> floors;
     return floors[q->id];
@@ -479,21 +496,14 @@ int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf
         q->cv_flusher.notify_one();
     }
 
-    // assemble exactly as ether_send (:257-261): dst, src, htons(proto), payload, zero pad and
-    // zeroed FCS slot; the engine fills the FCS (:262-263)
     uint8_t *f = B.arena + (uint64_t)slot * kStride;
-    std::memcpy(f, dst, 6);
-    std::memcpy(f + 6, q->mac, 6);
-    f[12] = (uint8_t)(proto >> 8);
-    f[13] = (uint8_t)proto;
-    if (bsize) std::memcpy(f + kHeaderLen, buf, bsize);
-    std::memset(f + kHeaderLen + bsize, 0, frame_size - kHeaderLen - bsize);
+    assemble(f, q->mac, dst, proto, buf, bsize, frame_size);
     SlotMeta &m = B.meta[slot];
     m.w = w;
     m.covered = (uint32_t)(frame_size - kFcsLen);
     // A synchronous caller blocks for its batch anyway: it computes its own frame's FCS here, on its
-    // own core where the frame is cache-hot, in parallel with the other callers (host_max 0: no)
-    m.has_fcs = w && q->host_max.load(std::memory_order_relaxed) > 0;
+    // own core where the frame is cache-hot, in parallel with the other callers (unless sync_host is off)
+    m.has_fcs = w && q->sync_host.load(std::memory_order_relaxed);
     if (m.has_fcs) {
         const uint32_t c = fcs::host_crc32(f, m.covered);
         std::memcpy(f + m.covered, &c, 4);   // little-endian, as ether.c:263
@@ -501,11 +511,37 @@ int enqueue(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf
     m.ready.store(seq, std::memory_order_release);
     return (int)frame_size;
 }
+// ether_send's body (src/linux/ether.c:222-269) for one frame on the calling thread: assembled in a
+// stack buffer, its FCS from the host CRC, handed to the sink as a batch of one (concurrently with
+// other senders and the flusher, as the reference's threads call sendto concurrently).
+int send_direct(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize) {
+    if (!dst || (!buf && bsize)) return -EINVAL;
+    const size_t frame_size = kHeaderLen + std::max<size_t>(bsize, kMinPayload) + kFcsLen;   // :222-224
+    if (frame_size > kSlot) return -EMSGSIZE;                                                // :234-237
+    if (q->stop_req.load(std::memory_order_acquire)) return -ESHUTDOWN;
+    alignas(64) uint8_t f[kStride];
+    assemble(f, q->mac, dst, proto, buf, bsize, frame_size);
+    const uint32_t covered = (uint32_t)(frame_size - kFcsLen);
+    const uint32_t c = fcs::host_crc32(f, covered);
+    std::memcpy(f + covered, &c, 4);   // little-endian, as ether.c:263
+    uint8_t *fp = f;
+    uint32_t sz = (uint32_t)frame_size;
+    int res = -EIO;   // a sink that forgets the frame reports it as failed
+    q->sink(q->ctx, &fp, &sz, &res, 1);
+    q->n_direct.fetch_add(1, std::memory_order_relaxed);
+    if (res != (int)frame_size) q->n_direct_errors.fetch_add(1, std::memory_order_relaxed);
+    return res;
+}
 }  // namespace
 
 extern "C" {
 
 int fcs_txq_send(fcs_txq_t *q, const uint8_t dst[6], uint16_t proto, const uint8_t *buf, size_t bsize) {
+    // A synchronous caller with no frame of its own still queued sends its frame itself (see the file
+    // comment); one with queued fire-and-forget frames, or with sync_host off, goes through the batch.
+    if (q && q->sync_host.load(std::memory_order_relaxed) &&
+        thread_floor(q).seq <= q->seq_sunk.load(std::memory_order_acquire))
+        return send_direct(q, dst, proto, buf, bsize);
     Waiter w;
     const int rc = enqueue(q, dst, proto, buf, bsize, &w);
     if (rc < 0) return rc;
@@ -573,13 +609,19 @@ uint64_t fcs_txq_set_host_max(fcs_txq_t *q, uint64_t bytes) {
     return q->host_max.exchange(bytes);
 }
 
+int fcs_txq_set_sync_host(fcs_txq_t *q, int on) {
+    if (!q) return -EINVAL;
+    return q->sync_host.exchange(on != 0) ? 1 : 0;
+}
+
 void fcs_txq_small_batches(const fcs_txq_t *q, uint64_t *small_batches, uint64_t *small_frames,
                            uint64_t *gpu_batches) {
     if (!q) return;
     fcs_txq *m = const_cast<fcs_txq *>(q);
     std::lock_guard<std::mutex> lk(m->mu);
-    if (small_batches) *small_batches = m->n_small_batches;
-    if (small_frames) *small_frames = m->n_small_frames;
+    const uint64_t direct = m->n_direct.load(std::memory_order_relaxed);
+    if (small_batches) *small_batches = m->n_small_batches + direct;
+    if (small_frames) *small_frames = m->n_small_frames + direct;
     if (gpu_batches) *gpu_batches = m->n_gpu_batches;
 }
 
@@ -587,9 +629,10 @@ void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint
     if (!q) return;
     fcs_txq *m = const_cast<fcs_txq *>(q);
     std::lock_guard<std::mutex> lk(m->mu);
-    if (frames) *frames = m->n_frames;
-    if (batches) *batches = m->n_batches;
-    if (errors) *errors = m->n_errors;
+    const uint64_t direct = m->n_direct.load(std::memory_order_relaxed);   // batches of one
+    if (frames) *frames = m->n_frames + direct;
+    if (batches) *batches = m->n_batches + direct;
+    if (errors) *errors = m->n_errors + m->n_direct_errors.load(std::memory_order_relaxed);
 }
 
 const char *fcs_txq_last_error(const fcs_txq_t *q) {

@@ -36,9 +36,9 @@ def ether_send_frame(oracle, dst, proto, payload):
     return f + struct.pack("<I", oracle.oracle_ether_fcs(f, len(f)))   # :262-263
 
 
-@pytest.mark.parametrize("host_max", [0, None])   # every batch on the GPU / the default GPU minimum
+@pytest.mark.parametrize("gpu_only", [True, False])   # every frame through a GPU step / the defaults
 @pytest.mark.parametrize("max_batch,flush_usec", [(1, 0), (64, 200), (1024, 2000)])
-def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec, host_max):
+def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec, gpu_only):
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
     b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
@@ -59,7 +59,7 @@ def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec,
 
     rd = threading.Thread(target=reader)
     rd.start()
-    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=flush_usec, host_max=host_max) as q:
+    with na.TxQueue(MAC, a.fileno(), max_batch=max_batch, flush_usec=flush_usec, gpu_only=gpu_only) as q:
         def producer(t):
             for dst, proto, payload in plans[t]:
                 results[t].append((q.send(dst, proto, payload), 14 + max(len(payload), 56) + 4))
@@ -73,14 +73,14 @@ def test_concurrent_producers_byte_identical(dev, oracle, max_batch, flush_usec,
         small_batches, small_frames, gpu_batches = q.paths()
         assert q.fallbacks() == (0, 0)                           # no GPU step failed
         assert small_batches + gpu_batches == batches
-        if host_max == 0:
+        if gpu_only:
             assert gpu_batches == batches                        # every batch's FCSs came from the GPU
+            if max_batch == 1:
+                assert batches == total
     rd.join(timeout=60)
     a.close(), b.close()
     assert all(r == want for rs in results for r, want in rs)   # per-call return = frame_size
     assert frames == total and 1 <= batches <= total and errors == 0
-    if max_batch == 1:
-        assert batches == total
     assert Counter(got) == expect
     for f in got:                                                # every frame carries a valid FCS
         assert oracle.oracle_ether_fcs(f, len(f)) == 0x2144DF1C

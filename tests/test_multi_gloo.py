@@ -83,6 +83,13 @@ def _worker(rank, world, port, q, mode="fixed"):
             q.put((sizes, 0.0))
         dist.destroy_process_group()
         return
+    if mode == "host":   # bench.py's host-inclusive run at N > 1: synthetic run times, real gathering
+        secs = [0.10 * (rank + 1), 0.30 * (rank + 1), 0.20 * (rank + 1)]
+        allr, rep_max = bench.gather_host_times(torch, dist, world, rank, (rank + 1) << 30, secs, 0)
+        if rank == 0:
+            q.put((bench.host_aggregate(allr, rep_max), rep_max))
+        dist.destroy_process_group()
+        return
     if mode == "imix":
         ln = _imix(TOTAL)
         lo, hi = bench.shard_range(TOTAL, world, rank, ln)
@@ -182,3 +189,29 @@ def test_two_rank_imix_bench_path_shards_match_single_pass(world):
     assert sum(s[4] for s in sizes) == int(glob.sum())
     gathered = np.concatenate([np.array(s[2], dtype=np.uint32) for s in sizes])
     assert np.array_equal(gathered, _crcs_var(_oracle(), glob, 0, len(glob)))
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_host_inclusive_aggregate_over_ranks(world):
+    """bench.py's host-inclusive run at N > 1: each rank's bytes and the median of
+    its runs travel over gloo, the per-run maximum over ranks gives the aggregate: all ranks' bytes
+    over the median of the slowest rank's run times. Rank r moves (r + 1) GiB in 0.1/0.3/0.2 x (r + 1) s."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, "host")) for r in range(world)]
+    for p in procs:
+        p.start()
+    agg, rep_max = q.get(timeout=180)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert rep_max == pytest.approx([0.1 * world, 0.3 * world, 0.2 * world])
+    total = sum((r + 1) << 30 for r in range(world))
+    assert agg["bytes_all_ranks"] == total
+    assert agg["secs_max_rank"] == pytest.approx(0.2 * world)
+    assert agg["GB_s_aggregate"] == round(total / (0.2 * world) / 1e9, 2)
+    assert [r["rank"] for r in agg["per_rank"]] == list(range(world))
+    for r in agg["per_rank"]:   # each rank: its bytes over the median of its own runs
+        assert r["secs"] == pytest.approx(0.2 * (r["rank"] + 1), abs=1e-4)
+        assert r["GB_s"] == round(((r["rank"] + 1) << 30) / r["secs"] / 1e9, 2)

@@ -54,7 +54,7 @@ def test_no_gpu_host_crc_sends_every_frame(oracle):
     b.setblocking(False)
     res = []
     plans = [(bytes([k]) * 6, 0x0806 + k, bytes([k]) * (10 * k + (k % 3) * 500)) for k in range(10)]
-    with na.TxQueue(MAC, a.fileno(), max_batch=4, flush_usec=50, host_max=0) as q:   # every batch to the GPU
+    with na.TxQueue(MAC, a.fileno(), max_batch=4, flush_usec=50, gpu_only=True) as q:   # every batch to the GPU
         th = [threading.Thread(target=lambda p=p: res.append((q.send(*p), 14 + max(len(p[2]), 56) + 4)))
               for p in plans]
         for t in th:
@@ -119,32 +119,64 @@ def test_many_producers_no_lost_frames(max_batch, linger):
     a.close(), b.close()
 
 
-@pytest.mark.parametrize("host_max,expect_small", [(None, True), (1 << 30, True), (0, False)])
-def test_small_batches_take_the_host_crc_by_design(oracle, host_max, expect_small):
-    """Batches whose covered bytes total at most the GPU minimum (fcs_txq_set_host_max, default
-    96 KiB) are computed by the flusher with the library's host CRC: counted as small batches, not
-    as failure answers, with no GPU step at all (so this runs the same with or without a GPU).
-    host_max 0 sends every batch to the GPU step (here: no GPU, so failure answers)."""
+@pytest.mark.parametrize("gpu_only", [False, True])
+def test_sync_callers_send_their_own_frames(oracle, gpu_only):
+    """fcs_txq_send with nothing of the caller's own queued sends the frame itself (ether_send's body
+    with the library's host CRC, the sink called with a batch of one): counted as host-CRC batches by
+    design, no GPU step, no failure answer; so this runs the same with or without a GPU. gpu_only
+    (fcs_txq_set_sync_host off, host_max 0) sends every frame through a batch's GPU step instead
+    (here, without a GPU, answered by the host CRC after the failure and counted as such)."""
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     b.setblocking(False)
     plans = [(bytes([k]) * 6, 0x0800, bytes([k]) * (k * 150 % 1501)) for k in range(24)]
-    with na.TxQueue(MAC, a.fileno(), max_batch=8, flush_usec=0, host_max=host_max) as q:
+    with na.TxQueue(MAC, a.fileno(), max_batch=8, flush_usec=0, gpu_only=gpu_only) as q:
         res = [q.send(*p) for p in plans]
         q.flush()
         frames, batches, errors = q.stats()
         small_batches, small_frames, gpu_batches = q.paths()
         host_batches, host_frames = q.fallbacks()
-        if host_max is not None:
-            assert q.set_host_max(host_max) == host_max
     assert res == [14 + max(len(p[2]), 56) + 4 for p in plans]
     assert frames == 24 and errors == 0
-    if expect_small:
-        assert (small_batches, small_frames) == (batches, 24) and host_batches == 0 and gpu_batches == 0
+    if not gpu_only:
+        assert (small_batches, small_frames, batches) == (24, 24, 24) and host_batches == 0 and gpu_batches == 0
     else:
         assert small_batches == 0 and small_frames == 0
         if not _gpu_visible():
             assert (host_batches, host_frames) == (batches, 24)
     got = [b.recv(2048) for _ in range(24)]
+    assert Counter(got) == Counter(ether_send_frame(oracle, *p) for p in plans)
+    a.close(), b.close()
+
+
+@pytest.mark.parametrize("host_max,expect_small", [(None, None), (1 << 30, True), (0, False)])
+def test_async_batches_below_the_gpu_minimum_take_the_host_crc(oracle, host_max, expect_small):
+    """Fire-and-forget batches whose covered bytes total at most the GPU minimum
+    (fcs_txq_set_host_max, default 4 KiB) are computed by the flusher with the host CRC: counted as
+    small batches, not as failure answers. host_max 0 sends every batch to the GPU step (here, without
+    a GPU, answered by the host CRC after the failure)."""
+    a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
+    a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
+    b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
+    b.setblocking(False)
+    plans = [(bytes([k]) * 6, 0x0806, bytes([k]) * (k * 150 % 1501)) for k in range(40)]
+    with na.TxQueue(MAC, a.fileno(), max_batch=8, flush_usec=0, host_max=host_max) as q:
+        if host_max is None:
+            assert q.set_host_max(4096) == 4096   # the documented default
+        res = [q.send_async(*p) for p in plans]
+        q.flush()
+        frames, batches, errors = q.stats()
+        small_batches, small_frames, gpu_batches = q.paths()
+        host_batches, host_frames = q.fallbacks()
+    assert res == [14 + max(len(p[2]), 56) + 4 for p in plans]
+    assert frames == 40 and errors == 0
+    assert small_batches + gpu_batches + host_batches == batches
+    if expect_small:
+        assert (small_batches, small_frames) == (batches, 40) and host_batches == 0 and gpu_batches == 0
+    elif expect_small is False:
+        assert small_batches == 0 and small_frames == 0
+        if not _gpu_visible():
+            assert (host_batches, host_frames) == (batches, 40)
+    got = [b.recv(2048) for _ in range(40)]
     assert Counter(got) == Counter(ether_send_frame(oracle, *p) for p in plans)
     a.close(), b.close()
 

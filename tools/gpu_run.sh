@@ -7,7 +7,8 @@
 #   tests:PATH[,PATH]     the named test files only
 #   bench[:ARGS]          python bench.py ARGS (default: the driver's plain line) -> OUT/bench.json
 #   ranks2                the 2-rank bench rehearsal on one GPU (bench.py --gpus 2, self-launched)
-#   profile               tools/profile_round.sh OUT/prof (kernel trace + PMC traffic + rehearsal)
+#   profile[:TAG]         tools/profile_round.sh OUT/prof TAG (trace, PMC traffic, the bundle under
+#                         OUT/prof/bundle, then the plain line quoting it, rehearsals)
 #   ab:ARGS               python tools/ab.py ARGS (variants built by tools/variants.sh)
 #   pmc:ARGS              tools/pmc.sh OUT/pmc ARGS (SQ counter passes over tools/prof_fixed.py ARGS)
 #   py:SCRIPT[,ARGS]      python SCRIPT ARGS (a measurement tool under tools/)
@@ -38,7 +39,7 @@ for step in "$@"; do
         > "$out/$n-ranks2.json" 2> "$log"; rc=$?
       echo "ranks2 rc=$rc"; tail -c 1500 "$out/$n-ranks2.json" ;;
     profile)
-      timeout -k 10 1000 bash tools/profile_round.sh "$out/prof" > "$log" 2>&1; rc=$?
+      timeout -k 10 1100 bash tools/profile_round.sh "$out/prof" ${arg:-r06_final} > "$log" 2>&1; rc=$?
       echo "profile rc=$rc"; tail -8 "$log" ;;
     ab)
       timeout -k 10 600 python -u tools/ab.py ${arg//,/ } > "$log" 2>&1; rc=$?

@@ -3,10 +3,12 @@
  *
  *   tools/txq_bench [producers] [frames_per_producer] [payload|-1=random] [max_batch] [flush_usec]
  *                   [sink: null|sock] [mode: txq|async|dropin|reference|hostcrc] [host_max|-1]
+ *                   [sync_host: 1|0]
  *
- * txq:       P producer threads call fcs_txq_send (ether_send semantics) into one queue; host_max
- *            sets the queue's GPU minimum (fcs_txq_set_host_max; -1 keeps the default, 0 sends every
- *            batch to the GPU).
+ * txq:       P producer threads call fcs_txq_send (ether_send semantics) into one queue; sync_host 0
+ *            (fcs_txq_set_sync_host) makes their frames join batches and the GPU step instead of
+ *            being sent by the callers themselves; host_max sets the GPU minimum of fire-and-forget
+ *            batches (fcs_txq_set_host_max; -1 keeps the default, 0 sends every batch to the GPU).
  * async:     the same through fcs_txq_send_async (fire-and-forget; batches fill to max_batch).
  * reference: each producer runs the reference's ether_send body per frame
  *            (/root/reference/src/linux/ether.c:222-265): frame assembly in a stack buffer, the
@@ -43,6 +45,7 @@ enum { M_TXQ, M_ASYNC, M_DROPIN, M_REF, M_HOSTCRC };
 static const char *MODE_NAME[] = {"txq", "async", "dropin", "reference", "hostcrc"};
 static int P = 8, M = 20000, PAYLOAD = 1500, BATCH = 512, FLUSH_US = 0, SOCK = 0, MODE = M_TXQ;
 static long long HOST_MAX = -1;
+static int SYNC_HOST = 1;
 static fcs_txq_t *Q;
 static uint32_t (*ref_fcs)(const void *, size_t);   /* the reference's ether_fcs (reference mode) */
 static int sock_tx = -1, sock_rx = -1;
@@ -139,6 +142,7 @@ int main(int argc, char **argv) {
         for (int m = 0; m < 5; m++)
             if (!strcmp(argv[7], MODE_NAME[m])) MODE = m;
     if (argc > 8) HOST_MAX = atoll(argv[8]);
+    if (argc > 9) SYNC_HOST = atoi(argv[9]) != 0;
     if (P < 1 || P > 256) return fprintf(stderr, "producers: 1..256\n"), 1;
     const int queue = MODE == M_TXQ || MODE == M_ASYNC;
     if (MODE == M_REF) {
@@ -172,8 +176,10 @@ int main(int argc, char **argv) {
         /* warm the GPU step (first launch, mapped arrays) outside the timed region */
         const uint8_t d[6] = {2, 0, 0, 0, 0, 9}, pl[64] = {0};
         const uint64_t hm = fcs_txq_set_host_max(Q, 0);
+        fcs_txq_set_sync_host(Q, 0);
         for (int i = 0; i < 4; i++) fcs_txq_send(Q, d, 0x0800, pl, sizeof pl);
         fcs_txq_set_host_max(Q, hm);
+        fcs_txq_set_sync_host(Q, SYNC_HOST);
         while (SOCK && atomic_load(&sunk_frames) < 4) usleep(100);
     } else if (MODE == M_DROPIN) {
         uint8_t warm[64] = {0};
@@ -209,12 +215,13 @@ int main(int argc, char **argv) {
     }
     const double dt = t1 - t0;
     printf("{\"mode\": \"%s\", \"sink\": \"%s\", \"producers\": %d, \"frames\": %.0f, \"payload\": %d, "
-           "\"max_batch\": %d, \"flush_usec\": %d, \"host_max\": %lld, \"s\": %.4f, \"Mframes_s\": %.4f, "
+           "\"max_batch\": %d, \"flush_usec\": %d, \"host_max\": %lld, \"sync_host\": %d, \"s\": %.4f, \"Mframes_s\": %.4f, "
            "\"us_per_frame_per_thread\": %.3f, \"Gbit_s\": %.3f, \"mean_batch\": %.1f, \"gpu_batches\": %llu, "
            "\"host_small_batches\": %llu, \"host_small_frames\": %llu, \"bad_results\": %llu, \"sunk_frames\": %llu, "
            "\"queue_errors\": %llu, \"us_per_batch\": {\"ready\": %.1f, \"fcs\": %.1f, \"sink\": %.1f, \"busy\": %.1f, "
            "\"pickup\": %.1f, \"wall\": %.1f}}\n",
-           MODE_NAME[MODE], SOCK ? "socketpair" : "null", P, nf, PAYLOAD, queue ? BATCH : 1, FLUSH_US, host_max, dt,
+           MODE_NAME[MODE], SOCK ? "socketpair" : "null", P, nf, PAYLOAD, queue ? BATCH : 1, FLUSH_US, host_max,
+           queue ? SYNC_HOST : 1, dt,
            nf / dt / 1e6, dt * 1e6 * P / nf, (double)(atomic_load(&sunk_bytes) - bytes0) * 8 / dt / 1e9,
            batches ? (double)frames / batches : 1.0, (unsigned long long)gb, (unsigned long long)sb,
            (unsigned long long)sf, (unsigned long long)atomic_load(&bad_results),
