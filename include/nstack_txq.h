@@ -86,7 +86,7 @@ void fcs_txq_fallbacks(const fcs_txq_t *q, uint64_t *host_batches, uint64_t *hos
  *   batch and take its GPU step. Returns the previous setting (1 = on, the default) or -EINVAL.
  * - fcs_txq_send_async (fire-and-forget): the frames of one batch take one GPU step when their
  *   FCS-covered bytes total more than `bytes`, the GPU minimum; at or below it the flusher computes
- *   them. The default (4 KiB) comes from the in-queue scan of tools/txq_vs_reference.sh; it can be
+ *   them. The default (16 KiB) comes from the in-queue scan of tools/txq_vs_reference.sh; it can be
  *   overridden per process by NSTACK_TXQ_HOST_MAX_BYTES; 0 sends every batch to the GPU.
  *   fcs_txq_set_host_max returns the previous value (0 for a NULL queue). */
 uint64_t fcs_txq_set_host_max(fcs_txq_t *q, uint64_t bytes);
@@ -99,10 +99,12 @@ void fcs_txq_small_batches(const fcs_txq_t *q, uint64_t *small_batches, uint64_t
 
 /* ---- provided sinks ---- */
 /* ctx = pointer to an int file descriptor of a CONNECTED socket (e.g. a socketpair or a
- * connected AF_PACKET/UDP socket): one sendmmsg per batch, no per-message address. */
+ * connected AF_PACKET/UDP socket): one sendmmsg per batch (send for a batch of one), no
+ * per-message address. */
 void fcs_txq_sink_fd(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res, uint32_t n);
 /* AF_PACKET raw socket, as ether_send uses it (:241-253): ctx = struct fcs_txq_packet_ctx*.
- * Each frame's sockaddr_ll takes sll_protocol and sll_addr from the frame's own header. */
+ * Each frame's sockaddr_ll takes sll_protocol and sll_addr from the frame's own header; one
+ * sendmmsg per batch, sendto for a batch of one (exactly ether_send's call). */
 struct fcs_txq_packet_ctx {
     int fd;
     int ifindex;

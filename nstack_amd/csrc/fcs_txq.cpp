@@ -25,7 +25,7 @@
 // - Fire-and-forget frames (fcs_txq_send_async) take one GPU step per batch when their covered bytes
 //   exceed host_max, the GPU minimum; at or below it the flusher computes them. Its frames are cold
 //   in the flusher's cache (the producers wrote them), and a fast host answer keeps the next batch
-//   small, so the in-queue scan favours the GPU from a few frames up: the default is 4 KiB.
+//   small, so the in-queue scan favours the GPU from about ten full frames up: the default is 16 KiB.
 #include <arpa/inet.h>
 #include <linux/if_packet.h>
 #include <sys/socket.h>
@@ -59,10 +59,11 @@ constexpr uint32_t kStride = 1536;      // arena slot pitch: whole cache lines, 
 constexpr uint32_t kMaxBatch = 65536;
 // Fire-and-forget batches of at most this many covered bytes take the host CRC (see the file
 // comment). tools/tx_crossover.c puts the crossover at ~500 KB when the host CRC reads cache-hot
-// frames; in the queue they are cold and batches that take the host path stay small, and the scan
-// of fire-and-forget producers (tools/txq_vs_reference.sh) was fastest with the GPU from a few
-// 1518-B frames up.
-constexpr uint64_t kHostMaxDefault = 4096;
+// frames; in the queue they are cold, and batches that take the host path stay small. The scan of
+// fire-and-forget producers (tools/txq_vs_reference.sh, profiles/r06_txq_vs_reference.jsonl):
+// 1518-B frames as fast at 4-32 KiB as with every batch on the GPU, slower from 128 KiB; 78-B
+// frames 3x faster at 8-32 KiB (small batches answered at once, large ones on the GPU).
+constexpr uint64_t kHostMaxDefault = 16 * 1024;
 
 using Clock = std::chrono::steady_clock;
 
@@ -676,6 +677,12 @@ void send_batch(int fd, std::vector<mmsghdr> &m, uint32_t n, int *res) {
 
 void fcs_txq_sink_fd(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res, uint32_t n) {
     const int fd = *(const int *)ctx;
+    if (n == 1) {   // a synchronous sender's own frame: one send, as ether_send's one sendto
+        ssize_t r;
+        do r = send(fd, frames[0], sizes[0], 0); while (r < 0 && errno == EINTR);
+        res[0] = r < 0 ? -errno : (int)r;
+        return;
+    }
     static thread_local std::vector<mmsghdr> m;
     static thread_local std::vector<iovec> iov;
     m.assign(n, mmsghdr{});
@@ -690,6 +697,19 @@ void fcs_txq_sink_fd(void *ctx, uint8_t *const *frames, const uint32_t *sizes, i
 
 void fcs_txq_sink_packet(void *ctx, uint8_t *const *frames, const uint32_t *sizes, int *res, uint32_t n) {
     const fcs_txq_packet_ctx *pc = (const fcs_txq_packet_ctx *)ctx;
+    if (n == 1) {   // one frame: sendto with the frame's sockaddr_ll, exactly as ether_send (:241-265)
+        sockaddr_ll a{};
+        const uint8_t *f = frames[0];
+        a.sll_family = AF_PACKET;
+        a.sll_protocol = htons((uint16_t)((f[12] << 8) | f[13]));
+        a.sll_ifindex = pc->ifindex;
+        a.sll_halen = 6;
+        std::memcpy(a.sll_addr, f, 6);
+        ssize_t r;
+        do r = sendto(pc->fd, f, sizes[0], 0, (const sockaddr *)&a, sizeof a); while (r < 0 && errno == EINTR);
+        res[0] = r < 0 ? -errno : (int)r;
+        return;
+    }
     static thread_local std::vector<mmsghdr> m;
     static thread_local std::vector<iovec> iov;
     static thread_local std::vector<sockaddr_ll> sa;

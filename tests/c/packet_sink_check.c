@@ -1,14 +1,15 @@
 /* packet_sink_check.c — test infrastructure for fcs_txq_sink_packet (include/nstack_txq.h), the TX
  * queue's AF_PACKET sink, without CAP_NET_RAW.
  *
- * This executable defines sendmmsg itself; a symbol of the executable comes first in the dynamic
- * linker's global scope, so libnstack_fcs.so's call binds here instead of to libc (no LD_PRELOAD).
+ * This executable defines sendmmsg and sendto itself (the sink sends a batch of one frame with
+ * sendto, exactly ether_send's call); a symbol of the executable comes first in the dynamic
+ * linker's global scope, so libnstack_fcs.so's calls bind here instead of to libc (no LD_PRELOAD).
  * The stand-in records every message (fd, flags, msg_name bytes, iovec) and answers from a script,
  * so partial sends and errors reach the sink's per-frame result mapping:
  *
  *     packet_sink_check N IFINDEX SCRIPT
  *
- * SCRIPT is a comma list, one entry per sendmmsg call: a number k (accept the first k messages),
+ * SCRIPT is a comma list, one entry per sendmmsg/sendto call: a number k (accept the first k messages),
  * "A" (accept all), "E<errno>" (fail with that errno), "I" (fail with EINTR). Calls past the script
  * accept all. N frames are built as ether_send builds them (src/linux/ether.c:257-261, FCS bytes
  * left zero: the sink does not look at them) with varied destinations, protocols and lengths, and
@@ -78,6 +79,28 @@ int sendmmsg(int fd, struct mmsghdr *m, unsigned int vlen, int flags) {
         g_sent++;
     }
     return (int)take;
+}
+
+ssize_t sendto(int fd, const void *buf, size_t len, int flags, const struct sockaddr *addr, socklen_t alen) {
+    const char *e = script_entry(g_call);
+    printf("{\"call\": %d, \"fd\": %d, \"vlen\": 1, \"flags\": %d, \"entry\": \"%s\", \"kind\": \"sendto\"}\n",
+           g_call, fd, flags, e ? e : "A");
+    g_call++;
+    if (e && e[0] == 'E') {
+        errno = atoi(e + 1);
+        return -1;
+    }
+    if (e && e[0] == 'I') {
+        errno = EINTR;
+        return -1;
+    }
+    printf("{\"msg\": %d, \"namelen\": %u, \"name\": \"", g_sent, (unsigned)alen);
+    hex(addr, alen);
+    printf("\", \"iovlen\": 1, \"len\": %zu, \"head\": \"", len);
+    hex(buf, len < 14 ? len : 14);
+    printf("\", \"control\": 0}\n");
+    g_sent++;
+    return (ssize_t)len;
 }
 
 int main(int argc, char **argv) {

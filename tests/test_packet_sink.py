@@ -5,7 +5,8 @@ ether_send (/root/reference/src/linux/ether.c:244-255) sends each frame with sen
 sockaddr_ll { AF_PACKET, htons(proto), the interface's ifindex, halen 6, sll_addr = dst }, every
 other field zero, length sizeof(struct sockaddr_ll); a failed sendto makes that frame's result
 -errno (:265-269), else it is the bytes sent. The sink does the same for a whole batch with
-sendmmsg: tests/c/packet_sink_check defines sendmmsg itself (the executable's definition comes first
+sendmmsg, and sends a batch of one frame (a synchronous sender's own frame) with sendto, exactly
+ether_send's call: tests/c/packet_sink_check defines sendmmsg and sendto itself (the executable's definition comes first
 in the dynamic linker's lookup scope, so the library binds to it), records every message and answers
 from a script of partial sends, errors and EINTR. Expected values are built here from ether.c's
 layout, field by field."""
@@ -102,3 +103,16 @@ def test_partial_sends_and_errors_map_per_frame(check, script, expect):
         else:
             left -= min(int(e), left)
     assert left == 0
+
+
+@pytest.mark.parametrize("script,expect", [("A", "ok"), ("E105", -105), ("I,A", "ok"), ("I,I,E90", -90)])
+def test_single_frame_is_one_sendto(check, script, expect):
+    """A batch of one (fcs_txq_send's own frame): one sendto with ether_send's sockaddr_ll, EINTR
+    retried, any other error the frame's -errno."""
+    calls, msgs, res = run(check, 1, 7, script)
+    assert all(c.get("kind") == "sendto" and c["fd"] == 77 and c["flags"] == 0 for c in calls)
+    dst, proto, size = frame_of(0)
+    assert res["res"] == [size if expect == "ok" else expect]
+    assert len(msgs) == (1 if expect == "ok" else 0)
+    for m in msgs:
+        assert m["namelen"] == 20 and bytes.fromhex(m["name"]) == sockaddr_ll(dst, proto, 7) and m["len"] == size

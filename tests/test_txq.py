@@ -151,7 +151,7 @@ def test_sync_callers_send_their_own_frames(oracle, gpu_only):
 @pytest.mark.parametrize("host_max,expect_small", [(None, None), (1 << 30, True), (0, False)])
 def test_async_batches_below_the_gpu_minimum_take_the_host_crc(oracle, host_max, expect_small):
     """Fire-and-forget batches whose covered bytes total at most the GPU minimum
-    (fcs_txq_set_host_max, default 4 KiB) are computed by the flusher with the host CRC: counted as
+    (fcs_txq_set_host_max, default 16 KiB) are computed by the flusher with the host CRC: counted as
     small batches, not as failure answers. host_max 0 sends every batch to the GPU step (here, without
     a GPU, answered by the host CRC after the failure)."""
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
@@ -161,7 +161,7 @@ def test_async_batches_below_the_gpu_minimum_take_the_host_crc(oracle, host_max,
     plans = [(bytes([k]) * 6, 0x0806, bytes([k]) * (k * 150 % 1501)) for k in range(40)]
     with na.TxQueue(MAC, a.fileno(), max_batch=8, flush_usec=0, host_max=host_max) as q:
         if host_max is None:
-            assert q.set_host_max(4096) == 4096   # the documented default
+            assert q.set_host_max(16384) == 16384   # the documented default
         res = [q.send_async(*p) for p in plans]
         q.flush()
         frames, batches, errors = q.stats()
