@@ -155,7 +155,9 @@ struct fcs_txq {
     std::condition_variable cv_prod;      // flusher -> producers (batch swapped, results ready)
     uint64_t seq_done = 0;                // last batch handed to the sink
     std::atomic<uint64_t> seq_sunk{0};    // the same, readable without mu (fcs_txq_send's direct path)
-    std::atomic<uint64_t> n_direct{0}, n_direct_errors{0};   // frames synchronous callers sent themselves
+    struct alignas(64) DirectCount {      // frames synchronous callers sent themselves, per thread shard
+        std::atomic<uint64_t> frames{0}, errors{0};   //   (one shared line would bounce between cores)
+    } direct[kMaxShards];
     uint64_t flush_target = 0;            // flush() wants batches <= this closed now
     uint64_t n_frames = 0, n_batches = 0, n_errors = 0;
     uint64_t n_host_batches = 0, n_host_frames = 0;   // failed GPU steps answered by the host CRC
@@ -426,8 +428,14 @@ inline void assemble(uint8_t *f, const uint8_t *mac, const uint8_t dst[6], uint1
 }
 
 Floor &thread_floor(const fcs_txq *q) {
-    thread_local std::unordered_map<uint64_t, Floor> floors;
-    return floors[q->id];
+    thread_local std::unordered_map<uint64_t, Floor> floors;   // nodes: references stay valid
+    thread_local uint64_t last_id = ~0ull;
+    thread_local Floor *last = nullptr;
+    if (q->id != last_id) {   // the usual case is one queue per thread (one per ether handle)
+        last = &floors[q->id];
+        last_id = q->id;
+    }
+    return *last;
 }
 
 // Reserve a slot in the open batch (one fetch_add on the home shard's word, no lock), assemble the
@@ -529,8 +537,9 @@ int send_direct(fcs_txq *q, const uint8_t dst[6], uint16_t proto, const uint8_t 
     uint32_t sz = (uint32_t)frame_size;
     int res = -EIO;   // a sink that forgets the frame reports it as failed
     q->sink(q->ctx, &fp, &sz, &res, 1);
-    q->n_direct.fetch_add(1, std::memory_order_relaxed);
-    if (res != (int)frame_size) q->n_direct_errors.fetch_add(1, std::memory_order_relaxed);
+    fcs_txq::DirectCount &dc = q->direct[thread_number() % kMaxShards];
+    dc.frames.fetch_add(1, std::memory_order_relaxed);
+    if (res != (int)frame_size) dc.errors.fetch_add(1, std::memory_order_relaxed);
     return res;
 }
 }  // namespace
@@ -620,7 +629,8 @@ void fcs_txq_small_batches(const fcs_txq_t *q, uint64_t *small_batches, uint64_t
     if (!q) return;
     fcs_txq *m = const_cast<fcs_txq *>(q);
     std::lock_guard<std::mutex> lk(m->mu);
-    const uint64_t direct = m->n_direct.load(std::memory_order_relaxed);
+    uint64_t direct = 0;
+    for (const fcs_txq::DirectCount &dc : m->direct) direct += dc.frames.load(std::memory_order_relaxed);
     if (small_batches) *small_batches = m->n_small_batches + direct;
     if (small_frames) *small_frames = m->n_small_frames + direct;
     if (gpu_batches) *gpu_batches = m->n_gpu_batches;
@@ -630,10 +640,14 @@ void fcs_txq_stats(const fcs_txq_t *q, uint64_t *frames, uint64_t *batches, uint
     if (!q) return;
     fcs_txq *m = const_cast<fcs_txq *>(q);
     std::lock_guard<std::mutex> lk(m->mu);
-    const uint64_t direct = m->n_direct.load(std::memory_order_relaxed);   // batches of one
+    uint64_t direct = 0, derr = 0;   // batches of one
+    for (const fcs_txq::DirectCount &dc : m->direct) {
+        direct += dc.frames.load(std::memory_order_relaxed);
+        derr += dc.errors.load(std::memory_order_relaxed);
+    }
     if (frames) *frames = m->n_frames + direct;
     if (batches) *batches = m->n_batches + direct;
-    if (errors) *errors = m->n_errors + m->n_direct_errors.load(std::memory_order_relaxed);
+    if (errors) *errors = m->n_errors + derr;
 }
 
 const char *fcs_txq_last_error(const fcs_txq_t *q) {
