@@ -13,8 +13,10 @@
  * recvmmsg (MSG_WAITFORONE: block as the socket is configured for the first frame, then take
  * whatever else is queued, up to max_batch) and hands the batch out one frame per call.
  * With FCS_RXQ_TRAILER (a link that delivers the 4-byte FCS, e.g. rx-fcs on) every batch is
- * verified on the GPU in one call (CRC residue, ether_fcs_verify_host) before any of its frames is
- * handed out; frames that fail are dropped and counted, and the trailer is stripped from the rest.
+ * verified (CRC residue) before any of its frames is handed out: on the GPU in one call
+ * (pipelined with the next recvmmsg), or, below the GPU minimum (fcs_rxq_set_host_max), by the host
+ * CRC on the receiving thread; frames that fail are dropped and counted, and the trailer is
+ * stripped from the rest.
  * Deviations, both for frames the reference mishandles: a frame shorter than the header (plus
  * trailer) is dropped and counted (the reference's min() on a negative length is undefined), and a
  * frame longer than 1518 bytes (1514 + trailer) is dropped and counted (the reference truncates it
@@ -60,6 +62,16 @@ void fcs_rxq_stats(const fcs_rxq_t *q, uint64_t *frames, uint64_t *bad_fcs, uint
 /* Batches (and their frames) the host CRC checked because the GPU check failed. 0 on a healthy
  * GPU. Any pointer may be NULL. */
 void fcs_rxq_fallbacks(const fcs_rxq_t *q, uint64_t *host_batches, uint64_t *host_frames);
+/* GPU minimum: a received batch whose frames total at most `bytes` is checked by the library's host
+ * CRC (fcs_host_crc32) on the receiving thread, where recvmmsg has just put the frames (cache-hot);
+ * larger batches go to the GPU (pipelined with the next recvmmsg). Default 256 KiB, from the scan in
+ * tools/rxq_bench.c; NSTACK_RXQ_HOST_MAX_BYTES overrides it per process; 0 sends every batch to
+ * the GPU. Returns the previous value (0 for NULL). */
+uint64_t fcs_rxq_set_host_max(fcs_rxq_t *q, uint64_t bytes);
+/* Batches (and frames) the host CRC checked by design (at or below the GPU minimum; failures are
+ * fcs_rxq_fallbacks), and batches the GPU checked. Any pointer may be NULL. */
+void fcs_rxq_small_batches(const fcs_rxq_t *q, uint64_t *small_batches, uint64_t *small_frames,
+                           uint64_t *gpu_batches);
 void fcs_rxq_destroy(fcs_rxq_t *q);
 
 #ifdef __cplusplus

@@ -37,7 +37,8 @@ EXPORTS = [
     "inet_csum_batch_dev", "inet_csum_fixed_dev", "inet_csum_batch_host", "inet_csum_set_flat_threshold", "inet_csum_set_dma_threshold", "inet_ip_checksum",
     "inet_tcp_checksum", "inet_udp_checksum",
     # include/nstack_rxq.h — batched RX call site with FCS verification
-    "fcs_rxq_create", "fcs_rxq_receive", "fcs_rxq_stats", "fcs_rxq_fallbacks", "fcs_rxq_destroy",
+    "fcs_rxq_create", "fcs_rxq_receive", "fcs_rxq_stats", "fcs_rxq_fallbacks", "fcs_rxq_set_host_max",
+    "fcs_rxq_small_batches", "fcs_rxq_destroy",
 ]
 
 # include/nstack_inet.h modes: the reference function each result reproduces
@@ -164,6 +165,8 @@ def _bind(path: str) -> ctypes.CDLL:
         "fcs_rxq_receive": (i32, [vp, vp, vp, c.c_size_t]),
         "fcs_rxq_stats": (None, [vp] + [c.POINTER(u64)] * 5),
         "fcs_rxq_fallbacks": (None, [vp, c.POINTER(u64), c.POINTER(u64)]),
+        "fcs_rxq_set_host_max": (u64, [vp, u64]),
+        "fcs_rxq_small_batches": (None, [vp, c.POINTER(u64), c.POINTER(u64), c.POINTER(u64)]),
         "fcs_rxq_destroy": (None, [vp]),
         "inet_ip_checksum": (c.c_uint16, [vp, c.c_size_t]),
         "inet_tcp_checksum": (c.c_uint16, [u32, u32, vp, c.c_size_t]),
@@ -468,12 +471,17 @@ class RxQueue:
     queued, negative = -errno); with trailer=True every recvmmsg batch is FCS-verified on the GPU,
     failing frames are dropped and the 4-byte trailer is stripped."""
 
-    def __init__(self, fd: int, own_mac: bytes, max_batch: int = 64, trailer: bool = True, lib=None):
+    def __init__(self, fd: int, own_mac: bytes, max_batch: int = 64, trailer: bool = True, lib=None,
+                 host_max=None):
+        """host_max: the GPU minimum in bytes (fcs_rxq_set_host_max; None keeps the default, 0 checks
+        every batch on the GPU)."""
         L = self._L = lib or load()
         self._mac = (ctypes.c_uint8 * 6)(*own_mac)
         self._q = L.fcs_rxq_create(fd, self._mac, max_batch, 1 if trailer else 0)
         if not self._q:
             raise FcsError(-errno.EINVAL, "fcs_rxq_create")
+        if host_max is not None:
+            L.fcs_rxq_set_host_max(self._q, host_max)
         self._hdr = (ctypes.c_uint8 * 14)()
         self._buf = (ctypes.c_uint8 * 2048)()
 
@@ -496,6 +504,13 @@ class RxQueue:
         hb, hf = ctypes.c_uint64(0), ctypes.c_uint64(0)
         self._L.fcs_rxq_fallbacks(self._q, ctypes.byref(hb), ctypes.byref(hf))
         return int(hb.value), int(hf.value)
+
+    def paths(self):
+        """(small_batches, small_frames, gpu_batches): batches the host CRC checked by design (at or
+        below the GPU minimum) and batches the GPU checked."""
+        sb, sf, gb = ctypes.c_uint64(0), ctypes.c_uint64(0), ctypes.c_uint64(0)
+        self._L.fcs_rxq_small_batches(self._q, ctypes.byref(sb), ctypes.byref(sf), ctypes.byref(gb))
+        return int(sb.value), int(sf.value), int(gb.value)
 
     def close(self) -> None:
         if self._q:

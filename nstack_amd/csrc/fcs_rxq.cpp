@@ -8,6 +8,12 @@
 // (fcs_host_crc.cpp), counted per queue and in fcs_engine_host_batches: the
 // synchronous ether_fcs_verify_host answers a failed GPU step itself; a failed pipelined check
 // (mapped_submit / mapped_wait) or no usable GPU at all is answered here.
+//
+// A batch whose frames total at most host_max bytes is checked by the host CRC on the receiving
+// thread, by design (counted in fcs_rxq_small_batches, not as a failure): recvmmsg has just copied
+// its frames there, so they are cache-hot, and the host CRC (~18 GB/s on one MI355X-box core) checks
+// a 64-frame batch of 1518-B frames in ~5 us, less than a GPU step's launch and completion round
+// trip. The default comes from tools/rxq_bench.c's scan (profiles/r06_rxq_vs_reference.jsonl).
 #include <arpa/inet.h>
 #include <sys/socket.h>
 
@@ -32,6 +38,10 @@ constexpr uint32_t kSlot = 2048;        // receive slot: a longer frame shows up
 constexpr uint32_t kMaxBatch = 4096;
 constexpr uint32_t kResidue = 0x2144DF1Cu;   // CRC-32 of any frame followed by its own LE FCS
 constexpr size_t kMaxPinnedSpares = 64;   // pinned ok arrays taken to replace set-aside ones (then malloc'd)
+#ifndef FCS_RXQ_HOST_MAX
+#define FCS_RXQ_HOST_MAX (256 * 1024)
+#endif
+constexpr uint64_t kRxHostMaxDefault = FCS_RXQ_HOST_MAX;   // see the file comment
 }  // namespace
 
 // One receive buffer: recvmmsg slots plus the frame list the verify kernel reads. With the
@@ -59,7 +69,9 @@ struct fcs_rxq {
     std::vector<mmsghdr> msgs;
     std::vector<iovec> iov;
     uint64_t n_frames = 0, n_bad = 0, n_echo = 0, n_drop = 0, n_batches = 0;
-    uint64_t n_host_batches = 0, n_host_frames = 0;   // batches the host CRC checked
+    uint64_t n_host_batches = 0, n_host_frames = 0;   // batches the host CRC checked after a failure
+    uint64_t n_small_batches = 0, n_small_frames = 0, n_gpu_batches = 0;   // by design / on the GPU
+    uint64_t host_max = kRxHostMaxDefault;   // see fcs_rxq_set_host_max (under mu)
     // ok arrays of pipelined batches whose check failed after its launch: the kernel may still write
     // them, so they are never reused before fcs_rxq_destroy, whatever else fails (every one is set
     // aside; their number is bounded because the engine stops launching after repeated failures).
@@ -167,12 +179,26 @@ void host_check(fcs_rxq *q, RxBuf &B, bool launched) {
 }
 
 // Start B's trailer check (pipelined: launch only), or do it at once. Every frame handed out has
-// been checked, by the GPU or, when its step failed, by the host CRC.
+// been checked, by the GPU or the host CRC (by design below the GPU minimum, or when a GPU step
+// failed).
 void start_check(fcs_rxq *q, RxBuf &B) {
     if (!(q->flags & FCS_RXQ_TRAILER)) {
         B.state = RxBuf::kReady;
         return;
     }
+    uint64_t bytes = 0;
+    for (uint32_t i = 0; i < B.n; i++) bytes += B.len[i];
+    if (bytes <= q->host_max) {   // below the GPU minimum: the frames are cache-hot on this thread
+        for (uint32_t i = 0; i < B.n; i++) {
+            const uint32_t L = B.len[i];   // 0: runt or oversize, dropped anyway
+            B.ok[i] = L >= kFcsLen && fcs::host_crc32(B.arena + B.off[i], L) == kResidue;
+        }
+        q->n_small_batches++;
+        q->n_small_frames += B.n;
+        B.state = RxBuf::kReady;
+        return;
+    }
+    q->n_gpu_batches++;
     if (q->pipelined && B.ok_pinned) {
         if (fcs::mapped_submit(B.arena, (uint64_t)B.n * kSlot, B.off, B.len, B.ok, B.n, &B.ticket))
             return host_check(q, B, false);   // nothing launched
@@ -215,6 +241,7 @@ fcs_rxq_t *fcs_rxq_create(int fd, const uint8_t own_mac[6], uint32_t max_batch, 
         }
     }
     q->pipelined = pinned && (flags & FCS_RXQ_TRAILER);
+    if (const char *e = std::getenv("NSTACK_RXQ_HOST_MAX_BYTES")) q->host_max = std::strtoull(e, nullptr, 0);
     for (uint8_t *&sp : q->spare)
         if (!(sp = (uint8_t *)std::malloc(max_batch))) {
             fcs_rxq_destroy(q);
@@ -288,6 +315,24 @@ void fcs_rxq_stats(const fcs_rxq_t *q, uint64_t *frames, uint64_t *bad_fcs, uint
     if (echoes) *echoes = m->n_echo;
     if (dropped) *dropped = m->n_drop;
     if (batches) *batches = m->n_batches;
+}
+
+uint64_t fcs_rxq_set_host_max(fcs_rxq_t *q, uint64_t bytes) {
+    if (!q) return 0;
+    std::lock_guard<std::mutex> lk(q->mu);
+    const uint64_t old = q->host_max;
+    q->host_max = bytes;
+    return old;
+}
+
+void fcs_rxq_small_batches(const fcs_rxq_t *q, uint64_t *small_batches, uint64_t *small_frames,
+                           uint64_t *gpu_batches) {
+    if (!q) return;
+    fcs_rxq *m = const_cast<fcs_rxq *>(q);
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (small_batches) *small_batches = m->n_small_batches;
+    if (small_frames) *small_frames = m->n_small_frames;
+    if (gpu_batches) *gpu_batches = m->n_gpu_batches;
 }
 
 void fcs_rxq_fallbacks(const fcs_rxq_t *q, uint64_t *host_batches, uint64_t *host_frames) {

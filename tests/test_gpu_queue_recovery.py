@@ -237,7 +237,7 @@ def test_rx_gpu_failures_checked_by_host_crc(flib, skip, fails):
         a.send(f)
     h0 = flib.fcs_engine_host_batches()
     flib.fcs_debug_fail_batches(skip, fails)
-    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True, lib=flib) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True, lib=flib, host_max=0) as q:
         got = drain(q)
         frames, bad, echoes, dropped, batches = q.stats()
         hb, hf = q.fallbacks()
@@ -260,7 +260,7 @@ def test_rx_wait_failure_then_gpu_again(flib):
     for f in sent:                      # one batch: submit (call 1) runs, its wait (call 2) fails
         a.send(f)
     flib.fcs_debug_fail_batches(1, 1)
-    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True, lib=flib) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True, lib=flib, host_max=0) as q:
         got = drain(q)
         assert flib.fcs_debug_batch_faults_left() == 0
         assert q.fallbacks() == (1, 10)
@@ -293,7 +293,7 @@ def test_rx_live_sender_with_failures(flib):
     th.start()
     got = []
     deadline = time.time() + 60
-    with na.RxQueue(b.fileno(), OWN, max_batch=32, trailer=True, lib=flib) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=32, trailer=True, lib=flib, host_max=0) as q:
         i = 0
         while len(got) < len(good) and time.time() < deadline:
             if i % 50 == 0:

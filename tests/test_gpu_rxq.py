@@ -24,8 +24,9 @@ def ether_send_frame(payload, proto=0x0800, src=PEER, dst=OWN):
     return body + struct.pack("<I", zlib.crc32(body))
 
 
+@pytest.mark.parametrize("host_max", [0, None])   # every batch on the GPU / the default GPU minimum
 @pytest.mark.parametrize("max_batch", [1, 7, 64])
-def test_rx_verify_drops_corrupted_frames(max_batch):
+def test_rx_verify_drops_corrupted_frames(max_batch, host_max):
     a, b = socket.socketpair(socket.AF_UNIX, socket.SOCK_DGRAM)
     a.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 4 << 20)
     b.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 4 << 20)
@@ -47,7 +48,7 @@ def test_rx_verify_drops_corrupted_frames(max_batch):
     for f in sent:
         a.send(f)
     got = []
-    with na.RxQueue(b.fileno(), OWN, max_batch=max_batch, trailer=True) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=max_batch, trailer=True, host_max=host_max) as q:
         while True:
             n, dst, src, proto, pl = q.receive()
             if n == 0:
@@ -56,15 +57,20 @@ def test_rx_verify_drops_corrupted_frames(max_batch):
             assert dst == OWN and src == PEER
             got.append((n, proto, pl))
         frames, bad, echoes, dropped, batches = q.stats()
-        assert q.fallbacks() == (0, 0)                          # the GPU checked every batch
+        small_batches, small_frames, gpu_batches = q.paths()
+        assert q.fallbacks() == (0, 0)                          # no GPU check failed
+        assert small_batches + gpu_batches == batches
+        if host_max == 0:
+            assert gpu_batches == batches                       # the GPU checked every batch
     a.close(), b.close()
     assert got == good
     assert frames == len(sent) and dropped == 0
     assert bad + echoes + len(good) == len(sent) and bad > 0 and echoes > 0
 
 
+@pytest.mark.parametrize("host_max", [0, None])   # every batch on the GPU / the default GPU minimum
 @pytest.mark.parametrize("max_batch", [16, 64])
-def test_rx_pipeline_with_live_sender(max_batch):
+def test_rx_pipeline_with_live_sender(max_batch, host_max):
     """Frames arriving while batches are checked: the queue overlaps the GPU check of one batch
     with the recvmmsg of the next (two buffers). A sender thread pushes bursts with pauses, so
     the receiver meets full, partial and empty queues; every good frame must come out once, in
@@ -96,7 +102,7 @@ def test_rx_pipeline_with_live_sender(max_batch):
     th.start()
     got = []
     deadline = time.time() + 60
-    with na.RxQueue(b.fileno(), OWN, max_batch=max_batch, trailer=True) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=max_batch, trailer=True, host_max=host_max) as q:
         while len(got) < len(good) and time.time() < deadline:
             n, dst, src, proto, pl = q.receive()
             assert n >= 0, n
@@ -126,11 +132,11 @@ def test_rx_destroy_with_batches_in_flight():
     b.setblocking(False)
     for i in range(200):
         a.send(ether_send_frame(i.to_bytes(4, "little") * 20))
-    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=16, trailer=True, host_max=0) as q:
         n, *_rest, pl = q.receive()
         assert n > 0 and pl[:4] == (0).to_bytes(4, "little")
     got = 0
-    with na.RxQueue(b.fileno(), OWN, max_batch=64, trailer=True) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=64, trailer=True, host_max=0) as q:
         while q.receive()[0] > 0:
             got += 1
     a.close(), b.close()

@@ -54,14 +54,17 @@ def test_receive_semantics_without_trailer(pair):
 
 
 @pytest.mark.skipif(_gpu_visible(), reason="checks the no-GPU path")
-def test_trailer_mode_without_gpu_host_crc_checks(pair):
-    """No GPU: the host CRC checks each batch, so the good frames still come out in
-    order, the corrupted one is dropped, and the fallback is counted."""
+@pytest.mark.parametrize("host_max", [0, None])
+def test_trailer_mode_without_gpu_host_crc_checks(pair, host_max):
+    """No GPU: the host CRC checks each batch, so the good frames still come out in order and the
+    corrupted one is dropped. host_max 0 (every batch to the GPU): the failed GPU step is answered
+    by the host CRC and counted as such; the default GPU minimum: these small batches
+    are checked by the host CRC by design, counted apart, with no failure."""
     import struct
     import zlib
     a, b = pair
     good = [frame(PEER, 0x0800 + i, bytes([i]) * (46 + 100 * i)) for i in range(5)]
-    with na.RxQueue(b.fileno(), OWN, max_batch=3, trailer=True) as q:
+    with na.RxQueue(b.fileno(), OWN, max_batch=3, trailer=True, host_max=host_max) as q:
         for i, f in enumerate(good):
             t = bytearray(f + struct.pack("<I", zlib.crc32(f)))
             a.send(bytes(t))
@@ -77,9 +80,13 @@ def test_trailer_mode_without_gpu_host_crc_checks(pair):
             out.append((proto, pl))
         frames, bad, echoes, dropped, batches = q.stats()
         host_batches, host_frames = q.fallbacks()
+        small_batches, small_frames, gpu_batches = q.paths()
     assert out == [(0x0800 + i, bytes([i]) * (46 + 100 * i)) for i in range(5)]
     assert (frames, bad, echoes, dropped) == (6, 1, 0, 0)
-    assert host_batches == batches and host_frames == 6
+    if host_max == 0:
+        assert host_batches == batches and host_frames == 6 and small_batches == 0
+    else:
+        assert (small_batches, small_frames) == (batches, 6) and host_batches == 0 and gpu_batches == 0
 
 
 def test_bad_arguments():
