@@ -11,9 +11,11 @@
 //
 // A batch whose frames total at most host_max bytes is checked by the host CRC on the receiving
 // thread, by design (counted in fcs_rxq_small_batches, not as a failure): recvmmsg has just copied
-// its frames there, so they are cache-hot, and the host CRC (~18 GB/s on one MI355X-box core) checks
-// a 64-frame batch of 1518-B frames in ~5 us, less than a GPU step's launch and completion round
-// trip. The default comes from tools/rxq_bench.c's scan (profiles/r06_rxq_vs_reference.jsonl).
+// its frames there, so they are cache-hot, and the host CRC (~18 GB/s on one MI355X-box core) beats
+// a GPU step's launch and completion round trip on small batches. Larger batches go to the GPU,
+// whose check overlaps the next recvmmsg. The scan of tools/rxq_bench.c
+// (profiles/r06_rxq_vs_reference.jsonl): 16 x 1518 B (24 KB) 2.60 M frames/s on the host against
+// 1.61 on the GPU; 64 x 1518 B (97 KB) 2.26 against 2.56; 64 x 60 B 3.5 against 2.7. Hence 64 KiB.
 #include <arpa/inet.h>
 #include <sys/socket.h>
 
@@ -39,7 +41,7 @@ constexpr uint32_t kMaxBatch = 4096;
 constexpr uint32_t kResidue = 0x2144DF1Cu;   // CRC-32 of any frame followed by its own LE FCS
 constexpr size_t kMaxPinnedSpares = 64;   // pinned ok arrays taken to replace set-aside ones (then malloc'd)
 #ifndef FCS_RXQ_HOST_MAX
-#define FCS_RXQ_HOST_MAX (256 * 1024)
+#define FCS_RXQ_HOST_MAX (64 * 1024)
 #endif
 constexpr uint64_t kRxHostMaxDefault = FCS_RXQ_HOST_MAX;   // see the file comment
 }  // namespace
