@@ -20,6 +20,7 @@
 #include <sys/socket.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
@@ -40,10 +41,7 @@ constexpr uint32_t kSlot = 2048;        // receive slot: a longer frame shows up
 constexpr uint32_t kMaxBatch = 4096;
 constexpr uint32_t kResidue = 0x2144DF1Cu;   // CRC-32 of any frame followed by its own LE FCS
 constexpr size_t kMaxPinnedSpares = 64;   // pinned ok arrays taken to replace set-aside ones (then malloc'd)
-#ifndef FCS_RXQ_HOST_MAX
-#define FCS_RXQ_HOST_MAX (64 * 1024)
-#endif
-constexpr uint64_t kRxHostMaxDefault = FCS_RXQ_HOST_MAX;   // see the file comment
+constexpr uint64_t kRxHostMaxDefault = 64 * 1024;   // see the file comment
 }  // namespace
 
 // One receive buffer: recvmmsg slots plus the frame list the verify kernel reads. With the
@@ -73,7 +71,7 @@ struct fcs_rxq {
     uint64_t n_frames = 0, n_bad = 0, n_echo = 0, n_drop = 0, n_batches = 0;
     uint64_t n_host_batches = 0, n_host_frames = 0;   // batches the host CRC checked after a failure
     uint64_t n_small_batches = 0, n_small_frames = 0, n_gpu_batches = 0;   // by design / on the GPU
-    uint64_t host_max = kRxHostMaxDefault;   // see fcs_rxq_set_host_max (under mu)
+    std::atomic<uint64_t> host_max{kRxHostMaxDefault};   // see fcs_rxq_set_host_max
     // ok arrays of pipelined batches whose check failed after its launch: the kernel may still write
     // them, so they are never reused before fcs_rxq_destroy, whatever else fails (every one is set
     // aside; their number is bounded because the engine stops launching after repeated failures).
@@ -190,7 +188,7 @@ void start_check(fcs_rxq *q, RxBuf &B) {
     }
     uint64_t bytes = 0;
     for (uint32_t i = 0; i < B.n; i++) bytes += B.len[i];
-    if (bytes <= q->host_max) {   // below the GPU minimum: the frames are cache-hot on this thread
+    if (bytes <= q->host_max.load(std::memory_order_relaxed)) {   // below the GPU minimum: the frames are cache-hot on this thread
         for (uint32_t i = 0; i < B.n; i++) {
             const uint32_t L = B.len[i];   // 0: runt or oversize, dropped anyway
             B.ok[i] = L >= kFcsLen && fcs::host_crc32(B.arena + B.off[i], L) == kResidue;
@@ -243,7 +241,7 @@ fcs_rxq_t *fcs_rxq_create(int fd, const uint8_t own_mac[6], uint32_t max_batch, 
         }
     }
     q->pipelined = pinned && (flags & FCS_RXQ_TRAILER);
-    if (const char *e = std::getenv("NSTACK_RXQ_HOST_MAX_BYTES")) q->host_max = std::strtoull(e, nullptr, 0);
+    if (const char *e = std::getenv("NSTACK_RXQ_HOST_MAX_BYTES")) q->host_max.store(std::strtoull(e, nullptr, 0));
     for (uint8_t *&sp : q->spare)
         if (!(sp = (uint8_t *)std::malloc(max_batch))) {
             fcs_rxq_destroy(q);
@@ -321,10 +319,7 @@ void fcs_rxq_stats(const fcs_rxq_t *q, uint64_t *frames, uint64_t *bad_fcs, uint
 
 uint64_t fcs_rxq_set_host_max(fcs_rxq_t *q, uint64_t bytes) {
     if (!q) return 0;
-    std::lock_guard<std::mutex> lk(q->mu);
-    const uint64_t old = q->host_max;
-    q->host_max = bytes;
-    return old;
+    return q->host_max.exchange(bytes);   // not under mu: a receive may be blocked in recvmmsg
 }
 
 void fcs_rxq_small_batches(const fcs_rxq_t *q, uint64_t *small_batches, uint64_t *small_frames,
