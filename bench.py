@@ -255,7 +255,7 @@ def extra_configs(torch, na, dev, stream, reps=5, host_gib=4.0):
         d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         na.fill_splitmix_dev(d, nbytes, SEED + 4, 0, stream)
         torch.cuda.synchronize()
-        pinned[:] = d.cpu().numpy()
+        torch.from_numpy(pinned).copy_(d)   # D2H straight into the pinned arena (no pageable staging copy)
         del d
         torch.cuda.empty_cache()
         hout = np.zeros(n, dtype=np.uint32)
@@ -328,7 +328,7 @@ def host_inclusive_imix(torch, na, dev, stream, rng, host_gib=4.0):
         d = torch.empty(total, dtype=torch.uint8, device=dev)
         na.fill_splitmix_dev(d, total, SEED + 5, 0, stream)
         torch.cuda.synchronize()
-        pinned[:] = d.cpu().numpy()
+        torch.from_numpy(pinned).copy_(d)   # D2H straight into the pinned arena (no pageable staging copy)
         del d
         torch.cuda.empty_cache()
         out = np.zeros(n, dtype=np.uint32)
@@ -488,7 +488,7 @@ def host_inclusive_sharded(torch, na, dev, stream, world: int, rank: int, dist, 
         d = torch.empty(nbytes, dtype=torch.uint8, device=dev)
         na.fill_splitmix_dev(d, nbytes, SEED + 6, rank * nbytes, stream)   # this rank's slice of one stream
         torch.cuda.synchronize()
-        pinned[:] = d.cpu().numpy()
+        torch.from_numpy(pinned).copy_(d)   # D2H straight into the pinned arena (no pageable staging copy)
         del d
         torch.cuda.empty_cache()
         hout = np.zeros(n, dtype=np.uint32)
