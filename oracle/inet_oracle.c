@@ -33,72 +33,45 @@
 #include <string.h>
 
 static uint16_t bswap16(uint16_t x) { return (uint16_t)((x << 8) | (x >> 8)); }
-static uint32_t bswap32(uint32_t x)
+
+/* One's-complement accumulation as src/ip.c:46-59 and src/tcp.c:190-209 perform it: the running sum
+ * starts at 0xffff, each 16-bit word is added and an overflow past 0xffff is folded back at once by
+ * subtracting 0xffff; an odd trailing byte enters as the low byte of a zero word. Words are the bytes
+ * in host order (the reference memcpy's them into a uint16_t); this container and the reference's
+ * targets are little-endian, so word k is p[2k] | p[2k+1] << 8. */
+static uint32_t ones_fold_add(uint32_t acc, uint32_t w)
 {
-    return (x >> 24) | ((x >> 8) & 0xff00u) | ((x << 8) & 0xff0000u) | (x << 24);
+    acc += w;
+    return acc > 0xffffu ? acc - 0xffffu : acc;
 }
 
-/* src/ip.c:39-62 (this container is little-endian x86-64, like the reference's targets). */
+static uint32_t ones_sum_le16(uint32_t acc, const uint8_t *p, size_t n)
+{
+    const size_t pairs = n / 2;
+    for (size_t k = 0; k < pairs; k++)
+        acc = ones_fold_add(acc, (uint32_t) p[2 * k] | ((uint32_t) p[2 * k + 1] << 8));
+    if (n % 2)
+        acc = ones_fold_add(acc, p[n - 1]);
+    return acc;
+}
+
+/* src/ip.c:39-62: ~(running sum from 0xffff), truncated to 16 bits (:61). */
 uint16_t oracle_ip_checksum(const void *dp, size_t bsize)
 {
-    const uint8_t *data = (const uint8_t *) dp;
-    uint32_t acc = 0xffff;
-    uint16_t word;
-    size_t i;
-
-    for (i = 0; i + 1 < bsize; i += 2) {
-        memcpy(&word, data + i, 2);
-        acc += word;
-        if (acc > 0xffff)
-            acc -= 0xffff; /* ntohs(0xffff) == 0xffff */
-    }
-    if (bsize & 1) {
-        word = 0;
-        memcpy(&word, data + bsize - 1, 1);
-        acc += word;
-        if (acc > 0xffff)
-            acc -= 0xffff;
-    }
-    return (uint16_t) ~acc;
+    return (uint16_t) ~ones_sum_le16(0xffffu, (const uint8_t *) dp, bsize);
 }
 
-/* src/tcp.c:167-213; src/dst in host order. */
+/* src/tcp.c:167-213; src/dst in host order. The 12-byte pseudo header (:176-188) is summed first
+ * (:190-195), then the segment (:197-209); both use the accumulation above. */
 uint16_t oracle_tcp_checksum(uint32_t src, uint32_t dst, const void *dp, size_t bsize)
 {
-    const uint8_t *data = (const uint8_t *) dp;
-    uint32_t acc = 0xffff;
-    uint16_t word;
-    size_t i;
-    uint8_t ph[12];
-    const uint32_t s = bswap32(src), d = bswap32(dst); /* htonl */
-    const uint16_t l = bswap16((uint16_t) bsize);       /* htons(bsize) truncates to 16 bits */
-
-    memcpy(ph, &s, 4);
-    memcpy(ph + 4, &d, 4);
-    ph[8] = 0;
-    ph[9] = 6; /* IP_PROTO_TCP */
-    memcpy(ph + 10, &l, 2);
-
-    for (i = 0; i + 1 < 12; i += 2) {
-        memcpy(&word, ph + i, 2);
-        acc += word;
-        if (acc > 0xffff)
-            acc -= 0xffff;
-    }
-    for (i = 0; i + 1 < bsize; i += 2) {
-        memcpy(&word, data + i, 2);
-        acc += word;
-        if (acc > 0xffff)
-            acc -= 0xffff;
-    }
-    if (bsize & 1) {
-        word = 0;
-        memcpy(&word, data + bsize - 1, 1);
-        acc += word;
-        if (acc > 0xffff)
-            acc -= 0xffff;
-    }
-    return (uint16_t) ~acc;
+    const uint8_t ph[12] = {
+        (uint8_t)(src >> 24), (uint8_t)(src >> 16), (uint8_t)(src >> 8), (uint8_t) src,   /* htonl(src) */
+        (uint8_t)(dst >> 24), (uint8_t)(dst >> 16), (uint8_t)(dst >> 8), (uint8_t) dst,   /* htonl(dst) */
+        0, 6,                                                   /* zero, IP_PROTO_TCP */
+        (uint8_t)(bsize >> 8), (uint8_t) bsize,                 /* htons(bsize), truncated to 16 bits */
+    };
+    return (uint16_t) ~ones_sum_le16(ones_sum_le16(0xffffu, ph, sizeof ph), (const uint8_t *) dp, bsize);
 }
 
 /* src/udp.c:136-174; src/dst are the raw in_addr_t values the caller passes. */
