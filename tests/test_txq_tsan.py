@@ -1,11 +1,14 @@
-"""ThreadSanitizer and AddressSanitizer + UBSan runs of the TX queue's host code (tools/tsan/run.sh;
-CPU only).
+"""ThreadSanitizer and AddressSanitizer + UBSan runs of the TX and RX queues' host code
+(tools/tsan/run.sh; CPU only).
 
 The multi-producer reservation, hand-offs and flusher of fcs_txq.cpp are built with
 -fsanitize=thread (and, separately, -fsanitize=address,undefined) against a stubbed GPU step
 (tools/tsan/gpu_stub.cpp) and driven by 1 to 4096 producers' worth of frames at several queue
 capacities and linger times; the run fails on any sanitizer report (leaks included under ASan) or
-a lost or duplicated frame. Keeping it in the CPU suite also keeps the engine's host-only headers
+a lost or duplicated frame. The RX queue (fcs_rxq.cpp) receives good, corrupted, runt, oversize
+and own-MAC frames over an AF_UNIX socketpair with the stubbed check failing every third call or
+never, and with another thread changing its GPU minimum; every good frame must come out once, in
+order, with exact drop counters. Keeping it in the CPU suite also keeps the engine's host-only headers
 buildable without ROCm (the harness compiles them with plain g++).
 """
 import os
