@@ -1,9 +1,9 @@
 """The library's own host CRC (fcs_host_crc32, nstack_amd/csrc/fcs_host_crc.cpp): what the host forms
 answer a failed GPU step with and what the TX queue computes batches below its GPU minimum with
-(nstack_txq.h, fcs_txq_set_host_max). Both of its forms (carry-less folding, slice-by-16 tables) must
-give the reference's ether_fcs (src/ether_fcs.c:4-19) on the golden vectors (generated from the
-compiled reference), the known answers, and every length and alignment around the folding's 16- and
-64-byte steps, checked against the oracle and zlib. No GPU is involved."""
+(nstack_txq.h, fcs_txq_set_host_max). Each of its forms (carry-less folding 128 or 512 bits wide,
+slice-by-16 tables) must give the reference's ether_fcs (src/ether_fcs.c:4-19) on the golden vectors
+(generated from the compiled reference), the known answers, and every length and alignment around
+the folding's 16-, 64- and 256-byte steps, checked against the oracle and zlib. No GPU is involved."""
 import ctypes
 import os
 import random
@@ -43,7 +43,8 @@ def test_every_length_and_alignment(oracle):
     buf = bytes(r.randrange(256) for _ in range(4096 + 64))
     raw = ctypes.create_string_buffer(buf, len(buf))
     L = na.load()
-    for n in list(range(0, 600)) + [1023, 1024, 1025, 1514, 1518, 1522, 2047, 2048, 4000]:
+    for n in list(range(0, 600)) + [767, 768, 769, 1023, 1024, 1025, 1279, 1280, 1281, 1514, 1518, 1522, 2047,
+                                     2048, 4000]:
         for a in range(16):
             p = ctypes.addressof(raw) + a
             want = oracle.oracle_ether_fcs(p, n)
@@ -58,14 +59,17 @@ def test_large_buffers_against_zlib():
         assert _crc(b) == zlib.crc32(b), n
 
 
-def test_tables_form_matches():
-    """NSTACK_FCS_HOST_CRC=tables: the slice-by-16 form alone (CPUs without PCLMULQDQ)."""
+@pytest.mark.parametrize("form", ["tables", "pclmul"])
+def test_narrower_forms_match(form):
+    """NSTACK_FCS_HOST_CRC=tables: the slice-by-16 form alone (CPUs without PCLMULQDQ); =pclmul: the
+    128-bit folding alone (CPUs without AVX-512 VPCLMULQDQ). The default run above takes the widest
+    form the CPU has."""
     code = ("import random, zlib, nstack_amd as na\n"
             "L = na.load(); r = random.Random(3)\n"
-            "bad = [n for n in list(range(0, 300)) + [1514, 9000, 100003]\n"
+            "bad = [n for n in list(range(0, 600)) + [1514, 1518, 9000, 100003]\n"
             "       for b in [r.randbytes(n)] if L.fcs_host_crc32(b, n) != zlib.crc32(b)]\n"
             "print(len(bad))\n")
-    env = dict(os.environ, NSTACK_FCS_HOST_CRC="tables")
+    env = dict(os.environ, NSTACK_FCS_HOST_CRC=form)
     p = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, cwd=ROOT,
                        timeout=120)
     assert p.returncode == 0, p.stderr[-2000:]
