@@ -64,8 +64,8 @@ void fcs_rxq_stats(const fcs_rxq_t *q, uint64_t *frames, uint64_t *bad_fcs, uint
 void fcs_rxq_fallbacks(const fcs_rxq_t *q, uint64_t *host_batches, uint64_t *host_frames);
 /* GPU minimum: a received batch whose frames total at most `bytes` is checked by the library's host
  * CRC (fcs_host_crc32) on the receiving thread, where recvmmsg has just put the frames (cache-hot);
- * larger batches go to the GPU (pipelined with the next recvmmsg). Default 64 KiB, from the scan in
- * tools/rxq_bench.c; NSTACK_RXQ_HOST_MAX_BYTES overrides it per process; 0 sends every batch to
+ * larger batches go to the GPU (pipelined with the next recvmmsg). Default 256 KiB, from the scan of
+ * tools/rxq_host_max_scan.sh; NSTACK_RXQ_HOST_MAX_BYTES overrides it per process; 0 sends every batch to
  * the GPU. Returns the previous value (0 for NULL). */
 uint64_t fcs_rxq_set_host_max(fcs_rxq_t *q, uint64_t bytes);
 /* Batches (and frames) the host CRC checked by design (at or below the GPU minimum; failures are

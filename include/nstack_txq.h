@@ -78,7 +78,7 @@ const char *fcs_txq_last_error(const fcs_txq_t *q);
 void fcs_txq_fallbacks(const fcs_txq_t *q, uint64_t *host_batches, uint64_t *host_frames);
 /* Where the GPU does not pay, the library's host CRC (fcs_host_crc32) computes the FCS, by design:
  * a GPU step costs a launch and a completion round trip (9-12 us on MI355X) whatever it holds, a
- * hand-off between threads 1-2 us, and the host CRC about 0.08 us per 1518-B frame.
+ * hand-off between threads 1-2 us, and the host CRC about 0.03 us per 1518-B frame.
  * - fcs_txq_send (synchronous): a caller with none of its own frames queued sends its frame itself
  *   (ether_send's body with the host CRC; the sink gets a batch of one on the caller's thread); a
  *   caller with fire-and-forget frames queued joins their batch (order kept) and computes its own

@@ -11,11 +11,13 @@
 //
 // A batch whose frames total at most host_max bytes is checked by the host CRC on the receiving
 // thread, by design (counted in fcs_rxq_small_batches, not as a failure): recvmmsg has just copied
-// its frames there, so they are cache-hot, and the host CRC (~18 GB/s on one MI355X-box core) beats
-// a GPU step's launch and completion round trip on small batches. Larger batches go to the GPU,
-// whose check overlaps the next recvmmsg. The scan of tools/rxq_bench.c
-// (profiles/r06_rxq_vs_reference.jsonl): 16 x 1518 B (24 KB) 2.60 M frames/s on the host against
-// 1.61 on the GPU; 64 x 1518 B (97 KB) 2.26 against 2.56; 64 x 60 B 3.5 against 2.7. Hence 64 KiB.
+// its frames there, so they are cache-hot, and the host CRC (four-lane carry-less folding, ~32 ns
+// per 1518-B frame on one MI355X-box core) beats a GPU step's launch and completion round trip on
+// small batches. Larger batches go to the GPU, whose check overlaps the next recvmmsg. The scan of
+// tools/rxq_host_max_scan.sh (profiles/r06_rxq_host_max_scan.jsonl, medians of three, M frames/s):
+// 64 x 1518 B (97 KB) 2.85 on the host against 2.69 on the GPU; 256 x 1518 B (389 KB) 2.93 with
+// 256 KiB against 2.73 with 1 MiB (the batch on the host); 46-B payloads flat from 64 KiB up.
+// Hence 256 KiB.
 #include <arpa/inet.h>
 #include <sys/socket.h>
 
@@ -41,7 +43,7 @@ constexpr uint32_t kSlot = 2048;        // receive slot: a longer frame shows up
 constexpr uint32_t kMaxBatch = 4096;
 constexpr uint32_t kResidue = 0x2144DF1Cu;   // CRC-32 of any frame followed by its own LE FCS
 constexpr size_t kMaxPinnedSpares = 64;   // pinned ok arrays taken to replace set-aside ones (then malloc'd)
-constexpr uint64_t kRxHostMaxDefault = 64 * 1024;   // see the file comment
+constexpr uint64_t kRxHostMaxDefault = 256 * 1024;   // see the file comment
 }  // namespace
 
 // One receive buffer: recvmmsg slots plus the frame list the verify kernel reads. With the

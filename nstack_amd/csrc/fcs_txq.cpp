@@ -10,8 +10,8 @@
 // frames still leave. The engine never leaves a kernel that can write into the arena after a failed
 // call (its results go through the library's own mapped memory), so arenas are always reused.
 //
-// Where the GPU does not pay, the host CRC (fcs_host_crc.cpp, carry-less folding, ~18 GB/s on one
-// MI355X host core) computes the FCS by design (counted in fcs_txq_small_batches, not as a failure).
+// Where the GPU does not pay, the host CRC (fcs_host_crc.cpp, carry-less folding, ~47 GB/s on 1518-B
+// frames on one MI355X-box core) computes the FCS by design (counted in fcs_txq_small_batches, not as a failure).
 // Measured on MI355X boxes (profiles/r06_txq_vs_reference.jsonl): a GPU step costs a launch and a
 // completion round trip (9-12 us) whatever it holds, and a hand-off between threads costs 1-2 us,
 // while the reference's own per-frame CRC costs 4.8 us per 1518-B frame and 0.2 us per 60-B one.
