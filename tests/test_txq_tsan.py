@@ -8,7 +8,9 @@ capacities and linger times; the run fails on any sanitizer report (leaks includ
 a lost or duplicated frame. The RX queue (fcs_rxq.cpp) receives good, corrupted, runt, oversize
 and own-MAC frames over an AF_UNIX socketpair with the stubbed check failing every third call or
 never, and with another thread changing its GPU minimum; every good frame must come out once, in
-order, with exact drop counters. Keeping it in the CPU suite also keeps the engine's host-only headers
+order, with exact drop counters. Under ASan the pcap reader (fcs_pcap.cpp) also takes 3000
+corrupted captures (bit flips, bad record lengths, truncation, the other byte order, pcapng):
+every call returns a count or -errno without touching memory outside its buffers. Keeping it in the CPU suite also keeps the engine's host-only headers
 buildable without ROCm (the harness compiles them with plain g++).
 """
 import os

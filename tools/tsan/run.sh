@@ -1,6 +1,7 @@
 #!/bin/bash
 # ThreadSanitizer run of the TX queue's lock-free reservation and hand-offs, and of the RX queue's
-# double-buffered receive (host code only; the GPU step is stubbed by gpu_stub.cpp). Exits non-zero on a sanitizer report or a lost/duplicated frame.
+# double-buffered receive (host code only; the GPU step is stubbed by gpu_stub.cpp); with
+# SAN=address,undefined also a mutation fuzz of the pcap reader (fcs_pcap.cpp). Exits non-zero on a sanitizer report or a lost/duplicated frame.
 #   bash tools/tsan/run.sh            ThreadSanitizer
 #   SAN=address,undefined bash tools/tsan/run.sh   AddressSanitizer + UBSan over the same cases
 set -eu
@@ -27,4 +28,10 @@ for f in 0 3; do
       UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1" timeout -k 5 300 "${OUT}_rx" $c
   done
 done
+if [ "$SAN" != thread ]; then   # the pcap reader is single-threaded: memory errors only
+  g++ -std=c++17 -O1 -g -fsanitize="$SAN" -fno-sanitize-recover=all -I"$ROOT/include" \
+      "$HERE/pcap_fuzz.cpp" "$ROOT/nstack_amd/csrc/fcs_pcap.cpp" -o "${OUT}_pcap" -lpthread
+  ASAN_OPTIONS="detect_leaks=1 exitcode=66" UBSAN_OPTIONS="halt_on_error=1 print_stacktrace=1" \
+    timeout -k 5 300 "${OUT}_pcap" 3000
+fi
 echo "$SAN: clean"
