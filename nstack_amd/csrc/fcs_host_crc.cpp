@@ -194,7 +194,6 @@ FCS_AVX512 uint32_t fold_crc_wide(const uint8_t *p, size_t n, uint32_t c, size_t
 enum Form { kTables, kPclmul, kWide };
 Form host_form() {
     static const Form f = [] {
-        __builtin_cpu_init();   // a caller may run before the CPU-model constructor (static init)
         const char *e = std::getenv("NSTACK_FCS_HOST_CRC");
         if ((e && !std::strcmp(e, "tables")) || !__builtin_cpu_supports("pclmul") || !__builtin_cpu_supports("sse4.1"))
             return kTables;
